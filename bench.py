@@ -1,0 +1,263 @@
+#!/usr/bin/env python3
+"""Headline benchmark: complex stencil SpMV GB/s (% of HBM peak) + GMRES iters/s.
+
+BASELINE.json metric: "complex stencil SpMV GB/s (% HBM peak) + GMRES iters/sec,
+N=4096^2".  Workload at N=1 = BASELINE config 3: 4096 x 4096 Marmousi-like
+heterogeneous velocity, wave_num 100 (>= 20.5 points per wavelength), b=12, C=81,
+alpha=2, shifted-Laplace (beta=0.5) preconditioned GMRES(20).
+
+A "step" is one operator apply (y = A x) over the whole grid, inputs resident in
+HBM.  value = algorithmic bytes of all steps on all ranks / wall time of the timed
+region (max over ranks); algorithmic bytes = 40 B per unknown (read u 16 + write y
+16 + read 1/c^2 8).
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+one process per GPU, row-slab decomposition with RCCL halo exchange overlapped
+with the interior stencil; weak scaling -- the grid grows to n = 4096 sqrt(N)
+(rounded to 32) so every GPU keeps ~4096^2 unknowns.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+
+
+def parse():
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200, help="timed operator applies")
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--n", type=int, default=0, help="global grid size (default 4096*sqrt(N))")
+    p.add_argument("--medium", default="marmousi", choices=["marmousi", "const", "c1"])
+    p.add_argument("--wave-num", type=float, default=100.0)
+    p.add_argument("--b", type=int, default=12)
+    p.add_argument("--C", type=float, default=81.0)
+    p.add_argument("--alpha", type=float, default=2.0)
+    p.add_argument("--precond", default="sl", choices=["sl", "jacobi", "none"])
+    p.add_argument("--sl-sweeps", type=int, default=2)
+    p.add_argument("--gmres-iters", type=int, default=40, help="timed inner GMRES iterations")
+    p.add_argument("--restart", type=int, default=20)
+    p.add_argument("--no-gmres", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-gmres-iters", type=int, default=4)
+    p.add_argument("--virtual-slabs", type=int, default=1)
+    return p.parse_args()
+
+
+def relaunch_distributed(args):
+    """`python bench.py --gpus N` without a launcher: start torch.distributed.run as a
+    child (nothing here has touched the GPU) and exit with its status."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", "--master-port",
+           str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def local_f1(omega, n, j0, j1, r1=.5, r2=.125):
+    """rows [j0, j1) of init_f1_mat(r1, r2, omega, n) (code.py:53-58), flattened."""
+    import numpy as np
+    x = np.linspace(0, 1, n + 2)[1:-1]
+    yy = x[j0:j1, None]
+    return np.exp(-(4 * omega / np.pi) ** 2 * ((x[None, :] - r1) ** 2 + (yy - r2) ** 2)).ravel()
+
+
+def make_medium(kind, n, cols):
+    import helmholtz_preconditioner_amd as H
+    if kind == "marmousi":
+        return H.marmousi_like_c_mat(n, cols=cols)
+    if kind == "const":
+        return H.constant_c_mat(n)
+    return H.init_c1_mat(.5, .5, n)
+
+
+def cpu_baseline(args, n, omega, h, eta, c_mat):
+    """Reference CPU path on this host (rank 0, N=1): the oracle's CSR (identical to
+    build_A_matrix, pinned by tests/golden) with scipy csr_matvec (single-threaded) and
+    scipy gmres with the same preconditioner (OpenBLAS threads)."""
+    import numpy as np
+    from oracle import helmholtz_oracle as O
+    t0 = time.perf_counter()
+    A = O.build_A_matrix(args.b, args.C, eta, omega, h, n, c_mat)
+    t_build = time.perf_counter() - t0
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal(n * n) + 1j * rng.standard_normal(n * n)
+    A @ x
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        A @ x
+    t_spmv = (time.perf_counter() - t0) / reps
+    bpp = 32 if args.medium == "const" else 40
+    out = {"value": round(bpp * n * n / t_spmv / 1e9, 3), "unit": "GB/s", "cores": 1,
+           "kind": "port",
+           "sample": f"{reps} scipy csr_matvec applies of the identical {n}x{n} operator "
+                     f"(oracle CSR, {A.nnz} nnz), {t_spmv * 1e3:.1f} ms each; CSR build "
+                     f"{t_build:.1f} s untimed"}
+    if not args.no_gmres and args.cpu_gmres_iters > 0:
+        if args.precond == "sl":
+            M, _ = O.shifted_laplace_jacobi(args.b, args.C, eta, omega, h, n, c_mat, beta=0.5,
+                                            sweeps=args.sl_sweeps, damping=0.7)
+        elif args.precond == "jacobi":
+            M = O.jacobi_preconditioner(A)
+        else:
+            M = None
+        f = local_f1(omega, n, 0, n)
+        t0 = time.perf_counter()
+        O.gmres_reference(A, f, M=M, rtol=1e-14, restart=args.restart, maxiter=args.cpu_gmres_iters)
+        t_g = time.perf_counter() - t0
+        thr = os.environ.get("OPENBLAS_NUM_THREADS", str(os.cpu_count()))
+        out["gmres_iters_per_s"] = round(args.cpu_gmres_iters / t_g, 4)
+        out["gmres_sample"] = (f"{args.cpu_gmres_iters} scipy gmres inner iterations "
+                               f"({args.precond} preconditioner), OpenBLAS threads={thr}")
+    return out
+
+
+def main():
+    args = parse()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world_env == 1:
+        sys.exit(relaunch_distributed(args))
+
+    import numpy as np
+    import helmholtz_preconditioner_amd as H
+    from helmholtz_preconditioner_amd import dist
+
+    rank, world, _ = dist.env_rank_world()
+    ctx = dist.init_from_env(virtual_slabs=args.virtual_slabs)
+    H.set_default_context(ctx)
+
+    n = args.n or int(round(4096 * math.sqrt(world) / 32) * 32)
+    omega, h, eta = H.problem_params(n, args.b, args.wave_num, args.alpha)
+    j0, j1 = dist.slab_bounds(n, world, rank)
+    t0 = time.perf_counter()
+    c_mat = make_medium(args.medium, n, (j0, j1))
+    A = H.build_A_matrix(args.b, args.C, eta, omega, h, n, c_mat, context=ctx)
+    t_init = time.perf_counter() - t0
+    assert (A.row_begin, A.row_end) == (j0, j1)
+    bpp = A.bytes_per_point
+
+    # ---------------- SpMV: K timed steps, inputs resident in HBM ----------------
+    x, y = A.vector(), A.vector()
+    x.fill_hash(2024)
+    if args.warmup > 0:
+        A.time_apply(x, y, args.warmup)
+    ctx.barrier()
+    t0 = time.perf_counter()
+    dev_ms, kern_ms = A.time_apply(x, y, args.steps)
+    ctx.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed = float(ctx.allreduce_max([elapsed])[0])
+    value = bpp * float(n) * n * args.steps / elapsed / 1e9
+    # roofline of the dominant kernel (the interior stencil launch on this rank)
+    interior_rows = (j1 - j0) - (1 if (world > 1 and rank > 0) else 0) \
+        - (1 if (world > 1 and rank < world - 1) else 0)
+    achieved = bpp * float(interior_rows) * n / (kern_ms * 1e-3) / 1e9
+    achieved_min = float(ctx.allreduce_max([-achieved])[0]) * -1.0
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "complex128",
+        "data": f"synthetic: {args.medium}-like velocity (seeded), hash-filled complex input",
+        "config": {
+            "workload": f"config3: {n}x{n} {args.medium} velocity, matrix-free PML stencil apply "
+                        f"(+ GMRES({args.restart}) {args.precond}-preconditioned)",
+            "n": n, "unknowns": n * n, "wave_num": args.wave_num, "b": args.b, "C": args.C,
+            "alpha": args.alpha, "bytes_per_unknown": bpp,
+            "parallelism": f"row-slab x{world} (RCCL halo)" if world > 1 else "single GPU",
+        },
+        "pct_hbm_peak": round(100.0 * value / (HBM_PEAK_GBPS * world), 2),
+        "device_ms_per_step": round(dev_ms / args.steps, 5),
+        "init_s": round(t_init, 3),
+    }
+    result["roofline"] = {
+        "bound": "hbm",
+        "achieved": round(achieved_min, 1),
+        "peak": HBM_PEAK_GBPS,
+        "unit": "GB/s",
+        "frac": round(achieved_min / HBM_PEAK_GBPS, 4),
+        "traffic": None,
+        "kernel": "stencil_kernel<EPI_AX,false> (interior rows)",
+        "kernel_ms": round(kern_ms, 5),
+        "bytes_per_launch": bpp * interior_rows * n,
+    }
+    del x, y
+
+    # ---------------- GMRES(restart): timed inner iterations ----------------
+    if not args.no_gmres and args.gmres_iters > 0:
+        f = A.vector(local_f1(omega, n, j0, j1))
+        if args.precond == "sl":
+            M = H.ShiftedLaplace(A, beta=0.5, sweeps=args.sl_sweeps, damping=0.7)
+        elif args.precond == "jacobi":
+            M = H.Jacobi(A)
+        else:
+            M = None
+        H.gmres(A, f, rtol=1e-14, restart=args.restart, maxiter=2, M=M,
+                callback=lambda r: None, callback_type="legacy")  # warm-up
+        ctx.barrier()
+        t0 = time.perf_counter()
+        xs, info, hist = H.gmres(A, f, rtol=1e-14, restart=args.restart, maxiter=args.gmres_iters,
+                                 M=M, callback=lambda r: None, callback_type="legacy",
+                                 return_history=True)
+        ctx.barrier()
+        tg = float(ctx.allreduce_max([time.perf_counter() - t0])[0])
+        its = len(hist)
+        # algorithmic bytes / iteration (CGS, lazy normalisation): SpMV 40N + projection
+        # 16(j+2)N + update 16(j+3)N, + preconditioner sweeps 56N each (SURVEY 8d style)
+        js = [i % args.restart for i in range(its)]
+        N = float(n) * n
+        pre = {"sl": bpp + 16 + 56 * (args.sl_sweeps - 1), "jacobi": 0, "none": 0}[args.precond]
+        gbytes = sum((bpp + pre) * N + 16 * (j + 2) * N + 16 * (j + 3) * N for j in js)
+        result["gmres"] = {
+            "iters_per_s": round(its / tg, 3),
+            "iterations": its,
+            "restart": args.restart,
+            "precond": {"sl": f"shifted-Laplace(beta=0.5, {args.sl_sweeps} damped-Jacobi sweeps)",
+                        "jacobi": "Jacobi", "none": "none"}[args.precond],
+            "ms_per_iter": round(tg * 1e3 / its, 4),
+            "algorithmic_GBps": round(gbytes / tg / 1e9, 1),
+            "final_rel_presid": float(hist[-1]) if its else None,
+        }
+        del f, xs
+
+    # ---------------- CPU baseline (rank 0, N=1) ----------------
+    if world == 1 and not args.no_cpu_baseline:
+        if args.medium == "marmousi":
+            c_full = c_mat  # N=1: the full field was generated
+        else:
+            c_full = c_mat
+        result["cpu_baseline"] = cpu_baseline(args, n, omega, h, eta, c_full)
+    elif world > 1:
+        result["cpu_baseline"] = None
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ctx.barrier()
+
+
+if __name__ == "__main__":
+    main()

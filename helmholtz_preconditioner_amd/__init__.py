@@ -1,0 +1,30 @@
+"""MI355X-native Helmholtz operator apply and GMRES solve.
+
+Drop-in for the hot path of bocchs/helmholtz-preconditioner (code.py):
+
+    from helmholtz_preconditioner_amd import build_A_matrix, gmres, init_c1_f1
+    omega, h, eta = problem_params(n, b, wave_num, alpha)          # code.py:442-444
+    c_mat, f_mat = init_c1_f1(omega, n)                             # code.py:447
+    A = build_A_matrix(b, const, eta, omega, h, n, c_mat)           # code.py:450
+    u, exit_code = gmres(A, f_mat.flatten(), M='jacobi', rtol=1e-3) # code.py:516
+
+The kernels are hand-written HIP for gfx950 in ``csrc/`` and are reached through
+the C ABI in ``include/helmholtz_amd.h`` (ctypes shim ``_ffi.py``).  Importing
+this package fails if that library has not been built; there is no CPU path.
+"""
+from ._ffi import HHError  # noqa: F401  (raises ImportError if the .so is missing)
+from .context import Context, default_context, device_count, set_default_context, unique_id  # noqa: F401
+from .media import (constant_c_mat, init_c1_f1, init_c1_f2, init_c1_mat, init_c2_f1,  # noqa: F401
+                    init_c2_f2, init_c2_mat, init_f1_mat, init_f2_mat, marmousi_like_c_mat,
+                    problem_params)
+from .operator import (DeviceOperator, DevicePreconditioner, DeviceVector, Jacobi,  # noqa: F401
+                       ShiftedLaplace, build_A_matrix)
+from .solver import gmres  # noqa: F401
+
+__all__ = [
+    "build_A_matrix", "gmres", "DeviceOperator", "DeviceVector", "Jacobi", "ShiftedLaplace",
+    "Context", "default_context", "set_default_context", "device_count", "unique_id",
+    "init_c1_mat", "init_c2_mat", "init_f1_mat", "init_f2_mat", "init_c1_f1", "init_c1_f2",
+    "init_c2_f1", "init_c2_f2", "constant_c_mat", "marmousi_like_c_mat", "problem_params",
+    "HHError",
+]

@@ -1,0 +1,48 @@
+// complex128 arithmetic on double2 (x = re, y = im) for gfx950 device code.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace hh {
+
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) {
+  return make_double2(a.x + b.x, a.y + b.y);
+}
+__device__ __forceinline__ double2 csub(double2 a, double2 b) {
+  return make_double2(a.x - b.x, a.y - b.y);
+}
+__device__ __forceinline__ double2 cscale(double2 a, double s) {
+  return make_double2(a.x * s, a.y * s);
+}
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+  return make_double2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
+}
+// a * b + c
+__device__ __forceinline__ double2 cfma(double2 a, double2 b, double2 c) {
+  return make_double2(fma(a.x, b.x, fma(-a.y, b.y, c.x)), fma(a.x, b.y, fma(a.y, b.x, c.y)));
+}
+// conj(a) * b + c
+__device__ __forceinline__ double2 cfma_conj(double2 a, double2 b, double2 c) {
+  return make_double2(fma(a.x, b.x, fma(a.y, b.y, c.x)), fma(a.x, b.y, fma(-a.y, b.x, c.y)));
+}
+__device__ __forceinline__ double cabs2(double2 a) { return fma(a.x, a.x, a.y * a.y); }
+__device__ __forceinline__ double2 cconj(double2 a) { return make_double2(a.x, -a.y); }
+// a / b for well-scaled stencil diagonals (|b| ~ 1e2 .. 1e10): one reciprocal.
+__device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
+  const double inv = 1.0 / fma(b.x, b.x, b.y * b.y);
+  return make_double2(fma(a.x, b.x, a.y * b.y) * inv, fma(a.y, b.x, -a.x * b.y) * inv);
+}
+// Smith's algorithm (the one numpy uses) for the small Hessenberg arithmetic.
+__device__ __forceinline__ double2 cdiv_smith(double2 a, double2 b) {
+  if (fabs(b.x) >= fabs(b.y)) {
+    if (b.x == 0.0 && b.y == 0.0) return make_double2(a.x / 0.0, a.y / 0.0);
+    const double rat = b.y / b.x;
+    const double scl = 1.0 / (b.x + b.y * rat);
+    return make_double2((a.x + a.y * rat) * scl, (a.y - a.x * rat) * scl);
+  } else {
+    const double rat = b.x / b.y;
+    const double scl = 1.0 / (b.y + b.x * rat);
+    return make_double2((a.x * rat + a.y) * scl, (a.y * rat - a.x) * scl);
+  }
+}
+
+}  // namespace hh

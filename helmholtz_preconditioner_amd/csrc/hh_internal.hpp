@@ -1,0 +1,124 @@
+// Internal declarations shared by the HIP kernels and the host runtime.
+// gfx950 (MI355X) only: 64-wide wavefronts, double2 = one 16-byte complex128.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace hh {
+
+constexpr int kWave = 64;
+constexpr int kStencilThreads = 256;   // one 256-wide strip of the fast axis i per block
+constexpr int kReduceThreads = 256;
+constexpr int kMaxProj = 32;           // max basis vectors per multidot/update launch
+constexpr int kMaxNorms = 2;           // norm accumulators a stencil epilogue may produce
+
+// Stencil epilogues (what the kernel writes after computing (A u) at a point).
+enum Epi : int {
+  EPI_AX = 0,        // out0 = s * A u
+  EPI_JAC = 1,       // out0 = s * A u / D
+  EPI_RES = 2,       // r = b - A u; out0 = r                    acc0 = |r|^2
+  EPI_RES_JAC = 3,   // r = b - A u; out0 = r / D                acc0 = |r|^2, acc1 = |r/D|^2
+  EPI_RES_SL = 4,    // r = b - A u; out0 = r; out1 = damp r / Dbeta   acc0 = |r|^2
+  EPI_SL_FIRST = 5,  // t = s * A u; out0 = t; out1 = damp t / Dbeta
+  EPI_SL_SWEEP = 6,  // z' = z + damp (r - Abeta z) / Dbeta   (u = z, in1 = r)
+};
+
+// Pointwise (no-neighbour) operations that need only the diagonal.
+enum PointOp : int {
+  PT_DIAG = 0,       // out0 = D
+  PT_JAC = 1,        // out0 = in0 / D                       acc0 = |out0|^2
+  PT_SL_FIRST = 2,   // out0 = damp in0 / Dbeta
+  PT_COPY_NORM = 3,  // out0 = in0 (if distinct)             acc0 = |out0|^2
+};
+
+struct StencilArgs {
+  const double2* u;        // input slab [nl][n]
+  const double2* halo_lo;  // global row j0-1 (zero row at the bottom boundary)
+  const double2* halo_hi;  // global row j1   (zero row at the top boundary)
+  const double* invc2;     // 1/c^2 [nl][n] (row j, column i), or nullptr
+  double invc2_const;      // used when invc2 == nullptr
+  const double2* tab_i;    // [3][n]: AW = s1((i-1/2)h)/h^2, AE = s1((i+1/2)h)/h^2, R1 = 1/s1(ih)
+  const double2* tab_j;    // [nl][4]: R2 = 1/s2(jh), BS = s2((j-1/2)h)/h^2, BN = s2((j+1/2)h)/h^2,
+                           //          OM = omega^2 * R2
+  int n, nl;
+  int row_begin, row_end;  // local rows computed by this launch
+  int rows_per_block;      // strip height marched by one block
+  int tiles_x, tiles_y, tiles_per_xcd;  // XCD-aware tile map
+  double2 mshift;          // mass-term multiplier for the shifted operator (EPI_SL_*)
+  double damping;          // damped-Jacobi weight (EPI_SL_*)
+  const double* in_scale;  // lazily-normalised input: A (s u) = s (A u); nullptr -> 1
+  const double2* in1;      // b (EPI_RES*) or r (EPI_SL_SWEEP)
+  double2* out0;
+  double2* out1;
+  double* partials;        // [blocks][kMaxNorms] when the epilogue accumulates norms
+};
+
+struct PointArgs {
+  const double2* in0;
+  double2* out0;
+  const double* invc2;
+  double invc2_const;
+  const double2* tab_i;
+  const double2* tab_j;
+  int n, nl;
+  double2 mshift;
+  double damping;
+  double* partials;        // [blocks][kMaxNorms]
+};
+
+// Kernel launchers (kernels.hip).  All are asynchronous on `stream`.
+void launch_stencil(int epi, bool const_c, const StencilArgs& a, int nblocks_out[1],
+                    hipStream_t stream);
+int stencil_grid_blocks(int n, int rows, int rows_per_block);
+int stencil_rows_per_block(int n, int rows);
+void launch_point(int op, bool const_c, const PointArgs& a, int blocks, hipStream_t stream);
+int point_blocks(size_t len);
+
+// Krylov kernels.
+//   multidot: partials[blk][2K+2] = sum conj(V_k) w (K vectors, stride ldv), |w|^2 at [2K]
+void launch_multidot(const double2* V, size_t ldv, int K, const double2* w, size_t len,
+                     double* partials, int blocks, hipStream_t stream);
+//   update: w_out = w - sum_k coef_k V_k, coef_k = scale_k^2 * raw_k (raw from reduced dots);
+//   acc |w_out|^2 into partials[blk][0]
+void launch_update(const double2* V, size_t ldv, int K, const double* raw, const double* scale,
+                   const double2* w, double2* w_out, size_t len, double* partials, int blocks,
+                   hipStream_t stream);
+//   xupdate: x += sum_k y_k V_k  (y complex, device, already including scales)
+void launch_xupdate(const double2* V, size_t ldv, int K, const double2* y, double2* x,
+                    size_t len, int blocks, hipStream_t stream);
+int stream_blocks(size_t len);
+// Deterministic reduction of `count` partial rows of width `width` (fixed order):
+// out[k] = sum_b partials[b*width + k] for k < cols.  One block per column.
+void launch_reduce(const double* partials, int count, int width, int cols, double* out,
+                   hipStream_t stream);
+// out[k] += in[k], k < count (tiny, one block).
+void launch_add_small(const double* in, double* out, int count, hipStream_t stream);
+// Hash fill of a slab vector (global element offset `goff`).
+void launch_fill_hash(double2* v, size_t len, size_t goff, uint64_t seed, hipStream_t stream);
+void launch_scale_copy(const double2* in, double2* out, size_t len, double s, hipStream_t stream);
+
+// GMRES device state machine step (single wave, krylov.hip).
+struct GivensState {
+  // Device buffers (complex as double2).
+  double2* H;      // [restart][restart+1]   H[col*(restart+1) + k]
+  double2* G;      // [restart][2] (c, s)
+  double2* S;      // [restart+1]
+  double* vscale;  // [restart+1] real scales of the stored basis vectors
+  double2* ycoef;  // [restart] x-update coefficients y_k * vscale_k
+  double* status;  // [8]: 0 presid, 1 breakdown, 2 h0, 3 h1, 4 rnorm, 5 mnorm
+  int restart;
+};
+// After multidot+update reductions: column `col` of H from raw dots (red_dots, 2*(col+1)
+// doubles + |w|^2 at [2*(col+1)]) and |w_new|^2 (red_norm[0]).
+void launch_gmres_column(const GivensState& g, int col, const double* red_dots,
+                         const double* red_norm, double eps, hipStream_t stream);
+// Start of a cycle: S[0] = ||Mr||, vscale[0] = 1/||Mr|| from red[idx_m]; status[4] = ||r||.
+void launch_gmres_start(const GivensState& g, const double* red, int idx_r, int idx_m,
+                        hipStream_t stream);
+// End of a cycle: triangular solve for y, ycoef_k = y_k * vscale_k.
+void launch_gmres_solve(const GivensState& g, int col, hipStream_t stream);
+
+}  // namespace hh

@@ -1,0 +1,351 @@
+// Krylov (GMRES) kernels for gfx950: fused multi-dot projection, fused update + norm,
+// solution update, fixed-order reductions and the single-wave Hessenberg/Givens step.
+//
+// Replaces the per-iteration Python/OpenBLAS work of scipy.sparse.linalg.gmres
+// (scipy 1.15.3 _isolve/iterative.py:748-800) that code.py:516 runs:
+//   MGS loop np.vdot / axpy over N-vectors  -> one multidot pass + one update pass (CGS),
+//   np.linalg.norm(w) (h0, h1)               -> fused into those passes,
+//   lartg + rotation of the Hessenberg column-> gmres_column_kernel (one lane),
+//   triangular solve, x += y @ v             -> gmres_solve_kernel + xupdate.
+// Every reduction is two-level and fixed-order (wave butterfly -> LDS -> per-block partial ->
+// one block per output summing partials in index order), so results are reproducible
+// run to run and identical on every rank after the RCCL allreduce.
+#include "hh_internal.hpp"
+#include "hh_complex.hpp"
+
+namespace hh {
+namespace {
+
+constexpr int kT = 256;  // threads per streaming block
+
+// Block-reduce NV doubles held per thread; lane results land in partials[blk*width + k].
+template <int NV>
+__device__ __forceinline__ void block_reduce_vec(double (&v)[NV], double* partials, int width) {
+  __shared__ double red[NV][kT / kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    double x = v[k];
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    if (lane == 0) red[k][wave] = x;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < NV; k += kT) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < kT / kWave; ++w) s += red[k][w];
+    partials[(size_t)blockIdx.x * width + k] = s;
+  }
+}
+
+// partials[blk][2K+2]: [2k, 2k+1] = sum_p conj(V_k[p]) w[p];  [2K] = sum |w|^2.
+template <int K>
+__global__ __launch_bounds__(kT) void multidot_kernel(const double2* __restrict__ V, size_t ldv,
+                                                      const double2* __restrict__ w, size_t len,
+                                                      double* __restrict__ partials) {
+  double2 acc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc[k] = make_double2(0.0, 0.0);
+  double nrm = 0.0;
+  const size_t stride = (size_t)gridDim.x * kT;
+  for (size_t p = (size_t)blockIdx.x * kT + threadIdx.x; p < len; p += stride) {
+    const double2 wv = w[p];
+    nrm = fma(wv.x, wv.x, fma(wv.y, wv.y, nrm));
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = cfma_conj(V[(size_t)k * ldv + p], wv, acc[k]);
+  }
+  double v[2 * K + 1];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    v[2 * k] = acc[k].x;
+    v[2 * k + 1] = acc[k].y;
+  }
+  v[2 * K] = nrm;
+  block_reduce_vec<2 * K + 1>(v, partials, 2 * K + 2);
+}
+
+// w_out = w - sum_k (s_k * (s_k * raw_k)) V_k; partials[blk][kMaxNorms]: [0] = |w_out|^2.
+template <int K>
+__global__ __launch_bounds__(kT) void update_kernel(const double2* __restrict__ V, size_t ldv,
+                                                    const double* __restrict__ raw,
+                                                    const double* __restrict__ scale,
+                                                    const double2* w, double2* w_out, size_t len,
+                                                    double* __restrict__ partials) {
+  double2 coef[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const double s = scale[k];
+    const double2 hk = cscale(make_double2(raw[2 * k], raw[2 * k + 1]), s);  // H[col][k]
+    coef[k] = cscale(hk, s);                                                    // h_k * s_k
+  }
+  double nrm = 0.0;
+  const size_t stride = (size_t)gridDim.x * kT;
+  for (size_t p = (size_t)blockIdx.x * kT + threadIdx.x; p < len; p += stride) {
+    double2 wv = w[p];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double2 vk = V[(size_t)k * ldv + p];
+      wv = csub(wv, cmul(coef[k], vk));
+    }
+    w_out[p] = wv;
+    nrm = fma(wv.x, wv.x, fma(wv.y, wv.y, nrm));
+  }
+  double v[1] = {nrm};
+  block_reduce_vec<1>(v, partials, kMaxNorms);
+}
+
+// x += sum_k y_k V_k.
+template <int K>
+__global__ __launch_bounds__(kT) void xupdate_kernel(const double2* __restrict__ V, size_t ldv,
+                                                     const double2* __restrict__ y,
+                                                     double2* __restrict__ x, size_t len) {
+  double2 c[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) c[k] = y[k];
+  const size_t stride = (size_t)gridDim.x * kT;
+  for (size_t p = (size_t)blockIdx.x * kT + threadIdx.x; p < len; p += stride) {
+    double2 t = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int k = 0; k < K; ++k) t = cfma(c[k], V[(size_t)k * ldv + p], t);
+    x[p] = cadd(x[p], t);
+  }
+}
+
+// One block per output column: out[k] = sum_b partials[b*width + k] in fixed order.
+__global__ __launch_bounds__(kT) void reduce_kernel(const double* __restrict__ partials, int count,
+                                                    int width, double* __restrict__ out) {
+  __shared__ double sh[kT];
+  const int k = blockIdx.x;
+  double s = 0.0;
+  for (int b = threadIdx.x; b < count; b += kT) s += partials[(size_t)b * width + k];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = kT / 2; off > 0; off >>= 1) {
+    if (threadIdx.x < off) sh[threadIdx.x] += sh[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[k] = sh[0];
+}
+
+__global__ void add_small_kernel(const double* in, double* out, int count) {
+  for (int k = threadIdx.x; k < count; k += blockDim.x) out[k] += in[k];
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kT) void fill_hash_kernel(double2* v, size_t len, size_t goff,
+                                                       uint64_t seed) {
+  const size_t stride = (size_t)gridDim.x * kT;
+  for (size_t p = (size_t)blockIdx.x * kT + threadIdx.x; p < len; p += stride) {
+    const uint64_t g = (uint64_t)(goff + p);
+    const uint64_t a = splitmix64(seed ^ (2 * g));
+    const uint64_t b = splitmix64(seed ^ (2 * g + 1));
+    // 53-bit uniforms in [-1, 1)
+    const double re = (double)(a >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+    const double im = (double)(b >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+    v[p] = make_double2(re, im);
+  }
+}
+
+__global__ __launch_bounds__(kT) void scale_copy_kernel(const double2* in, double2* out,
+                                                        size_t len, double s) {
+  const size_t stride = (size_t)gridDim.x * kT;
+  for (size_t p = (size_t)blockIdx.x * kT + threadIdx.x; p < len; p += stride)
+    out[p] = cscale(in[p], s);
+}
+
+// LAPACK (3.10+) zlartg main branch: [c s; -conj(s) c] [f; g] = [r; 0], c real >= 0.
+__device__ void zlartg(double2 f, double2 g, double* c, double2* s, double2* r) {
+  if (g.x == 0.0 && g.y == 0.0) {
+    *c = 1.0;
+    *s = make_double2(0.0, 0.0);
+    *r = f;
+    return;
+  }
+  if (f.x == 0.0 && f.y == 0.0) {
+    const double d = hypot(g.x, g.y);
+    *c = 0.0;
+    *s = make_double2(g.x / d, -g.y / d);
+    *r = make_double2(d, 0.0);
+    return;
+  }
+  const double f2 = cabs2(f);
+  const double g2 = cabs2(g);
+  const double h2 = f2 + g2;
+  const double cc = sqrt(f2 / h2);
+  *c = cc;
+  *r = make_double2(f.x / cc, f.y / cc);
+  const double d = sqrt(f2 * h2);
+  const double2 fd = make_double2(f.x / d, f.y / d);
+  *s = cmul(cconj(g), fd);
+}
+
+__global__ void gmres_column_kernel(GivensState g, int col, const double* rd, const double* rn,
+                                    double eps) {
+  if (threadIdx.x != 0) return;
+  const int R1 = g.restart + 1;
+  double2* h = g.H + (size_t)col * R1;
+  for (int k = 0; k <= col; ++k) h[k] = cscale(make_double2(rd[2 * k], rd[2 * k + 1]), g.vscale[k]);
+  const double h0 = sqrt(rd[2 * (col + 1)]);
+  const double h1 = sqrt(rn[0]);
+  h[col + 1] = make_double2(h1, 0.0);
+  double brk = 0.0;
+  if (h1 <= eps * h0) {
+    h[col + 1] = make_double2(0.0, 0.0);
+    brk = 1.0;
+  } else {
+    g.vscale[col + 1] = 1.0 / h1;
+  }
+  for (int k = 0; k < col; ++k) {
+    const double c = g.G[2 * k].x;
+    const double2 s = g.G[2 * k + 1];
+    const double2 n0 = h[k], n1 = h[k + 1];
+    h[k] = cadd(cscale(n0, c), cmul(s, n1));
+    h[k + 1] = cadd(cmul(make_double2(-s.x, s.y), n0), cscale(n1, c));  // -conj(s)*n0 + c*n1
+  }
+  double c;
+  double2 s, r;
+  zlartg(h[col], h[col + 1], &c, &s, &r);
+  g.G[2 * col] = make_double2(c, 0.0);
+  g.G[2 * col + 1] = s;
+  h[col] = r;
+  h[col + 1] = make_double2(0.0, 0.0);
+  const double2 Sc = g.S[col];
+  const double2 tmp = cmul(make_double2(-s.x, s.y), Sc);  // -conj(s) * S[col]
+  g.S[col] = cscale(Sc, c);
+  g.S[col + 1] = tmp;
+  g.status[0] = hypot(tmp.x, tmp.y);
+  g.status[1] = brk;
+  g.status[2] = h0;
+  g.status[3] = h1;
+}
+
+__global__ void gmres_start_kernel(GivensState g, const double* red, int idx_r, int idx_m) {
+  if (threadIdx.x != 0) return;
+  const double rn = sqrt(red[idx_r]);
+  const double mn = sqrt(red[idx_m]);
+  for (int k = 0; k <= g.restart; ++k) g.S[k] = make_double2(0.0, 0.0);
+  g.S[0] = make_double2(mn, 0.0);
+  g.vscale[0] = 1.0 / mn;
+  g.status[4] = rn;
+  g.status[5] = mn;
+}
+
+__global__ void gmres_solve_kernel(GivensState g, int col) {
+  if (threadIdx.x != 0) return;
+  const int R1 = g.restart + 1;
+  auto H = [&](int c, int k) -> double2& { return g.H[(size_t)c * R1 + k]; };
+  if (H(col, col).x == 0.0 && H(col, col).y == 0.0) g.S[col] = make_double2(0.0, 0.0);
+  double2 y[kMaxProj];
+  for (int k = 0; k <= col; ++k) y[k] = g.S[k];
+  for (int k = col; k > 0; --k) {
+    if (y[k].x != 0.0 || y[k].y != 0.0) {
+      y[k] = cdiv_smith(y[k], H(k, k));
+      const double2 t = y[k];
+      for (int m = 0; m < k; ++m) y[m] = csub(y[m], cmul(t, H(k, m)));
+    }
+  }
+  if (y[0].x != 0.0 || y[0].y != 0.0) y[0] = cdiv_smith(y[0], H(0, 0));
+  for (int k = 0; k <= col; ++k) g.ycoef[k] = cscale(y[k], g.vscale[k]);
+}
+
+template <int K>
+void md_launch(const double2* V, size_t ldv, const double2* w, size_t len, double* part,
+               int blocks, hipStream_t s) {
+  hipLaunchKernelGGL((multidot_kernel<K>), dim3(blocks), dim3(kT), 0, s, V, ldv, w, len, part);
+}
+template <int K>
+void up_launch(const double2* V, size_t ldv, const double* raw, const double* scale,
+               const double2* w, double2* wo, size_t len, double* part, int blocks,
+               hipStream_t s) {
+  hipLaunchKernelGGL((update_kernel<K>), dim3(blocks), dim3(kT), 0, s, V, ldv, raw, scale, w, wo,
+                     len, part);
+}
+template <int K>
+void xu_launch(const double2* V, size_t ldv, const double2* y, double2* x, size_t len, int blocks,
+               hipStream_t s) {
+  hipLaunchKernelGGL((xupdate_kernel<K>), dim3(blocks), dim3(kT), 0, s, V, ldv, y, x, len);
+}
+
+template <int... Ks>
+struct KTable {
+  using MD = void (*)(const double2*, size_t, const double2*, size_t, double*, int, hipStream_t);
+  using UP = void (*)(const double2*, size_t, const double*, const double*, const double2*,
+                      double2*, size_t, double*, int, hipStream_t);
+  using XU = void (*)(const double2*, size_t, const double2*, double2*, size_t, int, hipStream_t);
+  static constexpr MD md[] = {md_launch<Ks>...};
+  static constexpr UP up[] = {up_launch<Ks>...};
+  static constexpr XU xu[] = {xu_launch<Ks>...};
+};
+using Table = KTable<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21,
+                     22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32>;
+static_assert(kMaxProj == 32, "table covers 1..kMaxProj");
+
+}  // namespace
+
+int stream_blocks(size_t len) {
+  size_t b = (len + kT - 1) / kT;
+  if (b > 1024) b = 1024;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+void launch_multidot(const double2* V, size_t ldv, int K, const double2* w, size_t len,
+                     double* partials, int blocks, hipStream_t stream) {
+  Table::md[K - 1](V, ldv, w, len, partials, blocks, stream);
+}
+
+void launch_update(const double2* V, size_t ldv, int K, const double* raw, const double* scale,
+                   const double2* w, double2* w_out, size_t len, double* partials, int blocks,
+                   hipStream_t stream) {
+  Table::up[K - 1](V, ldv, raw, scale, w, w_out, len, partials, blocks, stream);
+}
+
+void launch_xupdate(const double2* V, size_t ldv, int K, const double2* y, double2* x,
+                    size_t len, int blocks, hipStream_t stream) {
+  Table::xu[K - 1](V, ldv, y, x, len, blocks, stream);
+}
+
+void launch_reduce(const double* partials, int count, int width, int cols, double* out,
+                   hipStream_t stream) {
+  hipLaunchKernelGGL(reduce_kernel, dim3(cols), dim3(kT), 0, stream, partials, count, width, out);
+}
+
+void launch_add_small(const double* in, double* out, int count, hipStream_t stream) {
+  hipLaunchKernelGGL(add_small_kernel, dim3(1), dim3(kT), 0, stream, in, out, count);
+}
+
+void launch_fill_hash(double2* v, size_t len, size_t goff, uint64_t seed, hipStream_t stream) {
+  hipLaunchKernelGGL(fill_hash_kernel, dim3(stream_blocks(len)), dim3(kT), 0, stream, v, len, goff,
+                     seed);
+}
+
+void launch_scale_copy(const double2* in, double2* out, size_t len, double s,
+                       hipStream_t stream) {
+  hipLaunchKernelGGL(scale_copy_kernel, dim3(stream_blocks(len)), dim3(kT), 0, stream, in, out,
+                     len, s);
+}
+
+void launch_gmres_column(const GivensState& g, int col, const double* red_dots,
+                         const double* red_norm, double eps, hipStream_t stream) {
+  hipLaunchKernelGGL(gmres_column_kernel, dim3(1), dim3(kWave), 0, stream, g, col, red_dots,
+                     red_norm, eps);
+}
+
+void launch_gmres_start(const GivensState& g, const double* red, int idx_r, int idx_m,
+                        hipStream_t stream) {
+  hipLaunchKernelGGL(gmres_start_kernel, dim3(1), dim3(kWave), 0, stream, g, red, idx_r, idx_m);
+}
+
+void launch_gmres_solve(const GivensState& g, int col, hipStream_t stream) {
+  hipLaunchKernelGGL(gmres_solve_kernel, dim3(1), dim3(kWave), 0, stream, g, col);
+}
+
+}  // namespace hh

@@ -1,0 +1,1008 @@
+// Host runtime behind the C ABI (include/helmholtz_amd.h): device context + RCCL rank,
+// the row-slab operator (PML tables, pre-transposed 1/c^2), halo exchange, apply modes,
+// preconditioners and the restarted GMRES driver with scipy's control flow.
+//
+// Reference boundary (code.py, bocchs/helmholtz-preconditioner):
+//   build_A_matrix(b, const, eta, omega, h, n, c_mat)  code.py:202   -> hh_op_create
+//   A @ x (LinearOperator.matvec -> csr_matvec)          code.py:516   -> hh_op_apply(_dev)
+//   scipy.sparse.linalg.gmres(A, f, M=M, tol=1e-3, ...)  code.py:516   -> hh_gmres
+//   M slot LinearOperator(matvec=...)                    code.py:510   -> hh_op_set_precond
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <complex>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "../../include/helmholtz_amd.h"
+#include "hh_internal.hpp"
+
+using cd = std::complex<double>;
+
+namespace hh {
+
+thread_local std::string g_err = "";
+
+struct Error {
+  int code;
+};
+
+[[noreturn]] static void fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  throw Error{code};
+}
+
+#define HIPC(expr)                                                                        \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      ::hh::fail(HH_ERR_HIP, "%s:%d %s -> %s", __FILE__, __LINE__, #expr,                 \
+                 hipGetErrorString(e_));                                                  \
+  } while (0)
+
+#define NCCLC(expr)                                                                       \
+  do {                                                                                    \
+    ncclResult_t r_ = (expr);                                                             \
+    if (r_ != ncclSuccess)                                                                \
+      ::hh::fail(HH_ERR_RCCL, "%s:%d %s -> %s", __FILE__, __LINE__, #expr,                \
+                 ncclGetErrorString(r_));                                                 \
+  } while (0)
+
+#define REQUIRE(cond, ...)                                                                \
+  do {                                                                                    \
+    if (!(cond)) ::hh::fail(HH_ERR_INVALID, __VA_ARGS__);                                 \
+  } while (0)
+
+template <class T>
+static T* dalloc(size_t count) {
+  if (count == 0) count = 1;
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, count * sizeof(T));
+  if (e != hipSuccess)
+    fail(HH_ERR_ALLOC, "hipMalloc(%zu bytes) failed: %s", count * sizeof(T), hipGetErrorString(e));
+  return static_cast<T*>(p);
+}
+
+static void dfree(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+// --------------------------------------------------------------- PML profiles
+// sigma1/sigma2/s1/s2 exactly as code.py:11-33 (s2 one-sided: quirk Q4).
+static double sigma1(double x, double C, double eta) {
+  if (x <= eta) return C / eta * ((x - eta) / eta) * ((x - eta) / eta);
+  if (x >= 1 - eta) return C / eta * ((x - 1 + eta) / eta) * ((x - 1 + eta) / eta);
+  return 0.0;
+}
+static double sigma2(double x, double C, double eta) {
+  if (x <= eta) return C / eta * ((x - eta) / eta) * ((x - eta) / eta);
+  return 0.0;
+}
+static cd s1(double x, double C, double eta, cd om) {
+  return 1.0 / (1.0 + cd(0, 1) * sigma1(x, C, eta) / om);
+}
+static cd s2(double x, double C, double eta, cd om) {
+  return 1.0 / (1.0 + cd(0, 1) * sigma2(x, C, eta) / om);
+}
+static double2 d2(cd z) { return make_double2(z.real(), z.imag()); }
+
+}  // namespace hh
+
+using namespace hh;
+
+struct hh_ctx {
+  int device = 0, rank = 0, world = 1, vslabs = 1;
+  ncclComm_t comm = nullptr;
+  hipStream_t stream = nullptr;   // compute
+  hipStream_t cstream = nullptr;  // halo exchange
+  hipEvent_t ev_in = nullptr, ev_halo = nullptr;
+  double* dscratch = nullptr;     // device scratch for host collectives
+  double* hpinned = nullptr;      // pinned host staging
+};
+
+namespace {
+struct Slab {
+  int j0 = 0, j1 = 0, nl = 0;  // global 0-based layers [j0, j1)
+  size_t off = 0;              // element offset inside the rank-local vector
+  double* invc2 = nullptr;     // [nl][n]
+  double2* tab_j = nullptr;    // [nl][4]
+  double2* halo_lo_buf = nullptr;
+  double2* halo_hi_buf = nullptr;
+  int rpb = 16;
+};
+}  // namespace
+
+struct hh_op {
+  hh_ctx* ctx = nullptr;
+  int n = 0, b = 0;
+  double C = 0, eta = 0, h = 0;
+  cd omega, mscale;
+  bool const_c = false;
+  double invc2_const = 1.0;
+  int jb = 0, je = 0;
+  size_t nloc = 0;
+  std::vector<Slab> slabs;
+  double2* tab_i = nullptr;
+  double2* zero_row = nullptr;
+  // preconditioner
+  int pkind = HH_PREC_NONE;
+  double beta = 0.5, damping = 1.0;
+  int sweeps = 1;
+  double2 mshift = make_double2(1.0, 0.0);
+  // reductions
+  double* partials = nullptr;
+  size_t partials_cap = 0;  // doubles
+  double* red = nullptr;    // 256 doubles
+  // scratch
+  double2* hx = nullptr;
+  double2* hy = nullptr;
+  double2* scrT = nullptr;
+  double2* scrZ = nullptr;
+  double2* scrR = nullptr;
+  // GMRES workspace
+  double2* V = nullptr;
+  int V_cols = 0;
+  double2* gbuf = nullptr;
+  GivensState gs{};
+  double* status_h = nullptr;
+  // timing hooks
+  hipEvent_t tk0 = nullptr, tk1 = nullptr;
+  hh_stats stats{};
+};
+
+struct hh_vec {
+  hh_op* op = nullptr;
+  double2* d = nullptr;
+};
+
+namespace {
+
+void ensure_scratch(hh_op* op) {
+  if (!op->scrT) op->scrT = dalloc<double2>(op->nloc);
+  if (!op->scrZ) op->scrZ = dalloc<double2>(op->nloc);
+}
+
+void allreduce_sum_dev(hh_op* op, double* d, int count) {
+  hh_ctx* c = op->ctx;
+  if (c->world > 1)
+    NCCLC(ncclAllReduce(d, d, count, ncclFloat64, ncclSum, c->comm, c->stream));
+}
+
+// Halo exchange for rank-local vector `in` and stencil launch of `epi` over all slabs.
+// Returns the number of partial rows written at op->partials.
+int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
+                const double2* in1, double2* out0, double2* out1, bool shifted) {
+  hh_ctx* c = op->ctx;
+  const int n = op->n;
+  const int S = (int)op->slabs.size();
+  const bool lo_x = c->world > 1 && c->rank > 0;             // cross-rank halo below
+  const bool hi_x = c->world > 1 && c->rank < c->world - 1;  // cross-rank halo above
+  if (lo_x || hi_x) {
+    HIPC(hipEventRecord(c->ev_in, c->stream));
+    HIPC(hipStreamWaitEvent(c->cstream, c->ev_in, 0));
+    NCCLC(ncclGroupStart());
+    if (lo_x) {
+      const Slab& s0 = op->slabs[0];
+      NCCLC(ncclRecv(s0.halo_lo_buf, 2 * (size_t)n, ncclFloat64, c->rank - 1, c->comm, c->cstream));
+      NCCLC(ncclSend(in + s0.off, 2 * (size_t)n, ncclFloat64, c->rank - 1, c->comm, c->cstream));
+    }
+    if (hi_x) {
+      const Slab& sl = op->slabs[S - 1];
+      NCCLC(ncclRecv(sl.halo_hi_buf, 2 * (size_t)n, ncclFloat64, c->rank + 1, c->comm, c->cstream));
+      NCCLC(ncclSend(in + sl.off + (size_t)(sl.nl - 1) * n, 2 * (size_t)n, ncclFloat64,
+                     c->rank + 1, c->comm, c->cstream));
+    }
+    NCCLC(ncclGroupEnd());
+    HIPC(hipEventRecord(c->ev_halo, c->cstream));
+  }
+
+  auto make_args = [&](int si) {
+    const Slab& s = op->slabs[si];
+    StencilArgs a{};
+    a.u = in + s.off;
+    // Local neighbour slabs on the same device are read in place; cross-rank halos land in
+    // the receive buffers; the global boundary reads a zero row (homogeneous Dirichlet).
+    if (si > 0) a.halo_lo = in + op->slabs[si - 1].off + (size_t)(op->slabs[si - 1].nl - 1) * n;
+    else a.halo_lo = lo_x ? s.halo_lo_buf : op->zero_row;
+    if (si < S - 1) a.halo_hi = in + op->slabs[si + 1].off;
+    else a.halo_hi = hi_x ? s.halo_hi_buf : op->zero_row;
+    a.invc2 = op->const_c ? nullptr : s.invc2;
+    a.invc2_const = op->invc2_const;
+    a.tab_i = op->tab_i;
+    a.tab_j = s.tab_j;
+    a.n = n;
+    a.nl = s.nl;
+    a.mshift = shifted ? op->mshift : make_double2(1.0, 0.0);
+    a.damping = op->damping;
+    a.in_scale = in_scale;
+    a.in1 = in1 ? in1 + s.off : nullptr;
+    a.out0 = out0 ? out0 + s.off : nullptr;
+    a.out1 = out1 ? out1 + s.off : nullptr;
+    return a;
+  };
+
+  int nparts = 0;
+  auto launch_rows = [&](int si, int r0, int r1, int rpb) {
+    if (r1 <= r0) return;
+    StencilArgs a = make_args(si);
+    a.row_begin = r0;
+    a.row_end = r1;
+    a.rows_per_block = rpb;
+    a.partials = op->partials + (size_t)nparts * kMaxNorms;
+    int written = 0;
+    launch_stencil(epi, op->const_c, a, &written, c->stream);
+    nparts += written;
+  };
+
+  // interior (independent of cross-rank halos) first, then the dependent boundary rows
+  bool first = true;
+  for (int si = 0; si < S; ++si) {
+    const Slab& s = op->slabs[si];
+    const int r0 = (si == 0 && lo_x) ? 1 : 0;
+    const int r1 = (si == S - 1 && hi_x) ? s.nl - 1 : s.nl;
+    if (first && op->tk0) HIPC(hipEventRecord(op->tk0, c->stream));
+    launch_rows(si, r0, r1, s.rpb);
+    if (first && op->tk1) HIPC(hipEventRecord(op->tk1, c->stream));
+    first = false;
+  }
+  if (lo_x || hi_x) {
+    HIPC(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+    const Slab& s0 = op->slabs[0];
+    const Slab& sl = op->slabs[S - 1];
+    if (S == 1 && s0.nl == 1) {
+      launch_rows(0, 0, 1, 1);
+    } else {
+      if (lo_x) launch_rows(0, 0, 1, 1);
+      if (hi_x) launch_rows(S - 1, sl.nl - 1, sl.nl, 1);
+    }
+  }
+  HIPC(hipGetLastError());
+  op->stats.spmv_count++;
+  return nparts;
+}
+
+// Pointwise op over all local slabs; returns partial rows written.
+int run_point(hh_op* op, int pt, const double2* in0, double2* out0, bool shifted) {
+  hh_ctx* c = op->ctx;
+  int nparts = 0;
+  for (const Slab& s : op->slabs) {
+    PointArgs a{};
+    a.in0 = in0 ? in0 + s.off : nullptr;
+    a.out0 = out0 ? out0 + s.off : nullptr;
+    a.invc2 = op->const_c ? nullptr : s.invc2;
+    a.invc2_const = op->invc2_const;
+    a.tab_i = op->tab_i;
+    a.tab_j = s.tab_j;
+    a.n = op->n;
+    a.nl = s.nl;
+    a.mshift = shifted ? op->mshift : make_double2(1.0, 0.0);
+    a.damping = op->damping;
+    a.partials = op->partials + (size_t)nparts * kMaxNorms;
+    const int blocks = point_blocks((size_t)s.nl * op->n);
+    launch_point(pt, op->const_c, a, blocks, c->stream);
+    nparts += blocks;
+  }
+  HIPC(hipGetLastError());
+  return nparts;
+}
+
+// reduce the first `cols` columns of `nparts` partial rows (row width kMaxNorms) into
+// op->red[dst..dst+cols), then allreduce across ranks
+void reduce_norms(hh_op* op, int nparts, int dst, int cols) {
+  launch_reduce(op->partials, nparts, kMaxNorms, cols, op->red + dst, op->ctx->stream);
+  allreduce_sum_dev(op, op->red + dst, cols);
+}
+
+// SL sweeps: z_1 already computed into `z1dst`; performs sweeps 2..s with r = T; the last
+// iterate lands in `out`.  `z1dst` must be chosen by sl_first_dst().
+void sl_sweeps(hh_op* op, const double2* T, double2* z1dst, double2* out) {
+  double2* cur = z1dst;
+  for (int k = 2; k <= op->sweeps; ++k) {
+    double2* dst = ((op->sweeps - k) % 2 == 0) ? out : op->scrZ;
+    if (dst == cur) dst = (cur == out) ? op->scrZ : out;
+    run_stencil(op, EPI_SL_SWEEP, cur, nullptr, T, dst, nullptr, true);
+    cur = dst;
+  }
+  if (cur != out) launch_scale_copy(cur, out, op->nloc, 1.0, op->ctx->stream);
+}
+double2* sl_first_dst(hh_op* op, double2* out) {
+  return ((op->sweeps - 1) % 2 == 0) ? out : op->scrZ;
+}
+
+// out = M A (s * v)
+void apply_MA(hh_op* op, const double2* v, const double* vs, double2* out) {
+  switch (op->pkind) {
+    case HH_PREC_NONE:
+      run_stencil(op, EPI_AX, v, vs, nullptr, out, nullptr, false);
+      break;
+    case HH_PREC_JACOBI:
+      run_stencil(op, EPI_JAC, v, vs, nullptr, out, nullptr, false);
+      break;
+    case HH_PREC_SHIFTED_LAPLACE: {
+      ensure_scratch(op);
+      double2* z1 = sl_first_dst(op, out);
+      run_stencil(op, EPI_SL_FIRST, v, vs, nullptr, op->scrT, z1, true);
+      sl_sweeps(op, op->scrT, z1, out);
+      break;
+    }
+  }
+}
+
+// out = M r (no norms).  r and out must differ.
+void apply_M(hh_op* op, const double2* r, double2* out) {
+  switch (op->pkind) {
+    case HH_PREC_NONE:
+      launch_scale_copy(r, out, op->nloc, 1.0, op->ctx->stream);
+      break;
+    case HH_PREC_JACOBI:
+      run_point(op, PT_JAC, r, out, false);
+      break;
+    case HH_PREC_SHIFTED_LAPLACE: {
+      ensure_scratch(op);
+      double2* z1 = sl_first_dst(op, out);
+      run_point(op, PT_SL_FIRST, r, z1, true);
+      sl_sweeps(op, r, z1, out);
+      break;
+    }
+  }
+}
+
+// |v|^2 -> op->red[dst] (allreduced)
+void norm2(hh_op* op, const double2* v, int dst) {
+  const int np = run_point(op, PT_COPY_NORM, v, nullptr, false);
+  reduce_norms(op, np, dst, 1);
+}
+
+// v0 = M (b - A x); red[dst] = |b - A x|^2, red[dst+1] = |v0|^2
+void residual(hh_op* op, const double2* b, const double2* x, double2* v0, int dst) {
+  switch (op->pkind) {
+    case HH_PREC_NONE: {
+      const int np = run_stencil(op, EPI_RES, x, nullptr, b, v0, nullptr, false);
+      reduce_norms(op, np, dst, 1);
+      HIPC(hipMemcpyAsync(op->red + dst + 1, op->red + dst, sizeof(double),
+                          hipMemcpyDeviceToDevice, op->ctx->stream));
+      break;
+    }
+    case HH_PREC_JACOBI: {
+      const int np = run_stencil(op, EPI_RES_JAC, x, nullptr, b, v0, nullptr, false);
+      reduce_norms(op, np, dst, 2);
+      break;
+    }
+    case HH_PREC_SHIFTED_LAPLACE: {
+      ensure_scratch(op);
+      // r must survive the sweeps: it lives in scrR, distinct from scrT/scrZ/v0.
+      if (!op->scrR) op->scrR = dalloc<double2>(op->nloc);
+      double2* z1 = sl_first_dst(op, v0);
+      const int np = run_stencil(op, EPI_RES_SL, x, nullptr, b, op->scrR, z1, true);
+      reduce_norms(op, np, dst, 1);  // red[dst] = |r|^2
+      sl_sweeps(op, op->scrR, z1, v0);
+      norm2(op, v0, dst + 1);
+      break;
+    }
+  }
+}
+
+void read_dev(hh_op* op, const double* dsrc, double* hdst, int count) {
+  HIPC(hipMemcpyAsync(op->status_h, dsrc, count * sizeof(double), hipMemcpyDeviceToHost,
+                      op->ctx->stream));
+  HIPC(hipStreamSynchronize(op->ctx->stream));
+  std::memcpy(hdst, op->status_h, count * sizeof(double));
+}
+
+void ensure_gmres(hh_op* op, int restart) {
+  REQUIRE(restart >= 1 && restart <= kMaxProj - 1, "restart must be in [1, %d]", kMaxProj - 1);
+  if (op->V && op->V_cols >= restart + 1) return;
+  dfree(op->V);
+  dfree(op->gbuf);
+  op->V = dalloc<double2>(op->nloc * (size_t)(restart + 1));
+  op->V_cols = restart + 1;
+  const int R1 = restart + 1;
+  const size_t nH = (size_t)restart * R1, nG = 2 * (size_t)restart, nS = R1, nY = restart;
+  const size_t total2 = nH + nG + nS + nY + (R1 + 8 + 1) / 2 + 8;
+  op->gbuf = dalloc<double2>(total2);
+  HIPC(hipMemset(op->gbuf, 0, total2 * sizeof(double2)));
+  GivensState& g = op->gs;
+  g.H = op->gbuf;
+  g.G = g.H + nH;
+  g.S = g.G + nG;
+  g.ycoef = g.S + nS;
+  g.vscale = reinterpret_cast<double*>(g.ycoef + nY);
+  g.status = g.vscale + R1 + 1;
+  g.restart = restart;
+}
+
+}  // namespace
+
+// ======================================================================== C ABI
+#define HH_API extern "C" __attribute__((visibility("default")))
+#define GUARD_BEGIN try {
+#define GUARD_END                                  \
+  }                                                \
+  catch (const Error& e) {                         \
+    return e.code;                                 \
+  }                                                \
+  catch (const std::exception& e) {                \
+    g_err = e.what();                              \
+    return HH_ERR_STATE;                           \
+  }                                                \
+  return HH_OK;
+
+HH_API int hh_abi_version(void) { return HH_ABI_VERSION; }
+HH_API const char* hh_last_error(void) { return g_err.c_str(); }
+
+HH_API int hh_device_count(int* count) {
+  GUARD_BEGIN
+  REQUIRE(count, "null count");
+  HIPC(hipGetDeviceCount(count));
+  GUARD_END
+}
+
+HH_API int hh_comm_unique_id(unsigned char id_out[128]) {
+  GUARD_BEGIN
+  REQUIRE(id_out, "null id");
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  ncclUniqueId id;
+  NCCLC(ncclGetUniqueId(&id));
+  std::memcpy(id_out, &id, 128);
+  GUARD_END
+}
+
+HH_API int hh_ctx_create(int device, int rank, int world, const unsigned char* nccl_id,
+                         int virtual_slabs, hh_ctx** out) {
+  GUARD_BEGIN
+  REQUIRE(out, "null ctx out");
+  REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank %d / world %d", rank, world);
+  REQUIRE(virtual_slabs >= 1 && virtual_slabs <= 64, "virtual_slabs must be in [1, 64]");
+  REQUIRE(world == 1 || nccl_id, "world > 1 needs an nccl id");
+  int ndev = 0;
+  HIPC(hipGetDeviceCount(&ndev));
+  REQUIRE(device >= 0 && device < ndev, "device %d not present (%d devices)", device, ndev);
+  HIPC(hipSetDevice(device));
+  hh_ctx* c = new hh_ctx();
+  c->device = device;
+  c->rank = rank;
+  c->world = world;
+  c->vslabs = virtual_slabs;
+  try {
+    HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPC(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    HIPC(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
+    HIPC(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
+    c->dscratch = dalloc<double>(256);
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpinned), 256 * sizeof(double)));
+    if (world > 1) {
+      ncclUniqueId id;
+      std::memcpy(&id, nccl_id, 128);
+      NCCLC(ncclCommInitRank(&c->comm, world, id, rank));
+    }
+  } catch (...) {
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->cstream) (void)hipStreamDestroy(c->cstream);
+    delete c;
+    throw;
+  }
+  *out = c;
+  GUARD_END
+}
+
+HH_API int hh_ctx_destroy(hh_ctx* c) {
+  GUARD_BEGIN
+  if (!c) return HH_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  if (c->comm) ncclCommDestroy(c->comm);
+  (void)hipEventDestroy(c->ev_in);
+  (void)hipEventDestroy(c->ev_halo);
+  (void)hipStreamDestroy(c->stream);
+  (void)hipStreamDestroy(c->cstream);
+  dfree(c->dscratch);
+  if (c->hpinned) (void)hipHostFree(c->hpinned);
+  delete c;
+  GUARD_END
+}
+
+static void host_allreduce(hh_ctx* c, double* v, int count, ncclRedOp_t op) {
+  REQUIRE(v && count >= 0 && count <= 256, "bad allreduce buffer");
+  if (c->world == 1 || count == 0) return;
+  HIPC(hipSetDevice(c->device));
+  HIPC(hipMemcpyAsync(c->dscratch, v, count * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  NCCLC(ncclAllReduce(c->dscratch, c->dscratch, count, ncclFloat64, op, c->comm, c->stream));
+  HIPC(hipMemcpyAsync(c->hpinned, c->dscratch, count * sizeof(double), hipMemcpyDeviceToHost,
+                      c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  std::memcpy(v, c->hpinned, count * sizeof(double));
+}
+
+HH_API int hh_ctx_allreduce_max(hh_ctx* c, double* v, int count) {
+  GUARD_BEGIN
+  REQUIRE(c, "null ctx");
+  host_allreduce(c, v, count, ncclMax);
+  GUARD_END
+}
+
+HH_API int hh_ctx_allreduce_sum(hh_ctx* c, double* v, int count) {
+  GUARD_BEGIN
+  REQUIRE(c, "null ctx");
+  host_allreduce(c, v, count, ncclSum);
+  GUARD_END
+}
+
+HH_API int hh_ctx_barrier(hh_ctx* c) {
+  GUARD_BEGIN
+  REQUIRE(c, "null ctx");
+  HIPC(hipSetDevice(c->device));
+  HIPC(hipStreamSynchronize(c->stream));
+  double one = 1.0;
+  host_allreduce(c, &one, 1, ncclSum);
+  HIPC(hipDeviceSynchronize());
+  GUARD_END
+}
+
+HH_API int hh_ctx_synchronize(hh_ctx* c) {
+  GUARD_BEGIN
+  REQUIRE(c, "null ctx");
+  HIPC(hipSetDevice(c->device));
+  HIPC(hipDeviceSynchronize());
+  GUARD_END
+}
+
+// ------------------------------------------------------------------ operator
+HH_API int hh_op_create(hh_ctx* c, int n, int b, double cconst, double eta, double omega_re,
+                        double omega_im, double h, const double* c_mat, double c_const,
+                        double mass_scale_re, double mass_scale_im, hh_op** out) {
+  GUARD_BEGIN
+  REQUIRE(c && out, "null ctx/op");
+  REQUIRE(n >= 1, "n must be >= 1 (got %d)", n);
+  REQUIRE(n >= c->world * c->vslabs, "n=%d too small for %d ranks x %d slabs", n, c->world,
+          c->vslabs);
+  REQUIRE(h > 0 && eta > 0, "h and eta must be positive");
+  REQUIRE(c_mat || c_const > 0, "constant medium needs c_const > 0");
+  HIPC(hipSetDevice(c->device));
+  hh_op* op = new hh_op();
+  try {
+    op->ctx = c;
+    op->n = n;
+    op->b = b;
+    op->C = cconst;
+    op->eta = eta;
+    op->h = h;
+    op->omega = cd(omega_re, omega_im);
+    op->mscale = cd(mass_scale_re, mass_scale_im);
+    op->const_c = (c_mat == nullptr);
+    op->invc2_const = op->const_c ? 1.0 / (c_const * c_const) : 1.0;
+    // rank slab: balanced contiguous split of the n layers
+    op->jb = (int)((long)c->rank * n / c->world);
+    op->je = (int)((long)(c->rank + 1) * n / c->world);
+    op->nloc = (size_t)(op->je - op->jb) * n;
+    const cd om = op->omega;
+    const cd om2 = om * om * op->mscale;
+    const double ih2 = 1.0 / (h * h);
+    // per-i table (fast axis): AW, AE, R1
+    std::vector<double2> ti(3 * (size_t)n);
+    for (int ii = 0; ii < n; ++ii) {
+      const double i = ii + 1;
+      ti[ii] = d2(s1((i - .5) * h, cconst, eta, om) * ih2);
+      ti[n + ii] = d2(s1((i + .5) * h, cconst, eta, om) * ih2);
+      ti[2 * n + ii] = d2(1.0 / s1(i * h, cconst, eta, om));
+    }
+    op->tab_i = dalloc<double2>(3 * (size_t)n);
+    HIPC(hipMemcpy(op->tab_i, ti.data(), ti.size() * sizeof(double2), hipMemcpyHostToDevice));
+    op->zero_row = dalloc<double2>(n);
+    HIPC(hipMemset(op->zero_row, 0, n * sizeof(double2)));
+    // local slabs
+    const int rows = op->je - op->jb;
+    size_t off = 0;
+    std::vector<double> col;
+    for (int s = 0; s < c->vslabs; ++s) {
+      Slab sl;
+      sl.j0 = op->jb + (int)((long)s * rows / c->vslabs);
+      sl.j1 = op->jb + (int)((long)(s + 1) * rows / c->vslabs);
+      sl.nl = sl.j1 - sl.j0;
+      sl.off = off;
+      off += (size_t)sl.nl * n;
+      sl.rpb = stencil_rows_per_block(n, sl.nl);
+      std::vector<double2> tj(4 * (size_t)sl.nl);
+      for (int jl = 0; jl < sl.nl; ++jl) {
+        const double j = sl.j0 + jl + 1;
+        const cd r2 = 1.0 / s2(j * h, cconst, eta, om);
+        tj[4 * jl + 0] = d2(r2);
+        tj[4 * jl + 1] = d2(s2((j - .5) * h, cconst, eta, om) * ih2);
+        tj[4 * jl + 2] = d2(s2((j + .5) * h, cconst, eta, om) * ih2);
+        tj[4 * jl + 3] = d2(om2 * r2);
+      }
+      sl.tab_j = dalloc<double2>(tj.size());
+      HIPC(hipMemcpy(sl.tab_j, tj.data(), tj.size() * sizeof(double2), hipMemcpyHostToDevice));
+      if (!op->const_c) {
+        // invc2[jl][ii] = 1 / c_mat[ii, j-1]^2  (c_mat read as c_mat[i-1, j-1]: quirk Q3),
+        // transposed once here so the kernel streams it along i with unit stride.
+        std::vector<double> buf((size_t)sl.nl * n);
+        const size_t ld = (size_t)n + 2;
+        constexpr int TB = 64;
+        for (int ib = 0; ib < n; ib += TB)
+          for (int jb2 = 0; jb2 < sl.nl; jb2 += TB)
+            for (int ii = ib; ii < std::min(n, ib + TB); ++ii) {
+              const double* src = c_mat + (size_t)ii * ld + sl.j0;
+              for (int jl = jb2; jl < std::min(sl.nl, jb2 + TB); ++jl) {
+                const double cv = src[jl];
+                buf[(size_t)jl * n + ii] = 1.0 / (cv * cv);
+              }
+            }
+        sl.invc2 = dalloc<double>(buf.size());
+        HIPC(hipMemcpy(sl.invc2, buf.data(), buf.size() * sizeof(double), hipMemcpyHostToDevice));
+      }
+      sl.halo_lo_buf = dalloc<double2>(n);
+      sl.halo_hi_buf = dalloc<double2>(n);
+      HIPC(hipMemset(sl.halo_lo_buf, 0, n * sizeof(double2)));
+      HIPC(hipMemset(sl.halo_hi_buf, 0, n * sizeof(double2)));
+      op->slabs.push_back(sl);
+    }
+    // partial-sum workspace: stencil tiles (+ boundary rows) of every slab, or streaming blocks
+    size_t tiles = 0;
+    for (const Slab& sl : op->slabs) {
+      tiles += (size_t)stencil_grid_blocks(n, sl.nl, sl.rpb) +
+               2 * (size_t)((n + kStencilThreads - 1) / kStencilThreads) + 8;
+    }
+    size_t cap = std::max(tiles * kMaxNorms, (size_t)1024 * (2 * kMaxProj + 2));
+    cap = std::max(cap, (size_t)c->vslabs * 2048 * kMaxNorms);
+    op->partials = dalloc<double>(cap);
+    op->partials_cap = cap;
+    op->red = dalloc<double>(256);
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&op->status_h), 256 * sizeof(double)));
+    HIPC(hipDeviceSynchronize());
+  } catch (...) {
+    delete op;  // device memory of a failed create is reclaimed at process exit
+    throw;
+  }
+  *out = op;
+  GUARD_END
+}
+
+HH_API int hh_op_destroy(hh_op* op) {
+  GUARD_BEGIN
+  if (!op) return HH_OK;
+  (void)hipSetDevice(op->ctx->device);
+  (void)hipStreamSynchronize(op->ctx->stream);
+  for (Slab& s : op->slabs) {
+    dfree(s.invc2);
+    dfree(s.tab_j);
+    dfree(s.halo_lo_buf);
+    dfree(s.halo_hi_buf);
+  }
+  dfree(op->tab_i);
+  dfree(op->zero_row);
+  dfree(op->partials);
+  dfree(op->red);
+  dfree(op->hx);
+  dfree(op->hy);
+  dfree(op->scrT);
+  dfree(op->scrZ);
+  dfree(op->scrR);
+  dfree(op->V);
+  dfree(op->gbuf);
+  if (op->status_h) (void)hipHostFree(op->status_h);
+  delete op;
+  GUARD_END
+}
+
+HH_API int hh_op_local_rows(hh_op* op, int* j_begin, int* j_end) {
+  GUARD_BEGIN
+  REQUIRE(op && j_begin && j_end, "null argument");
+  *j_begin = op->jb;
+  *j_end = op->je;
+  GUARD_END
+}
+
+HH_API int hh_op_set_precond(hh_op* op, int kind, double beta, int sweeps, double damping) {
+  GUARD_BEGIN
+  REQUIRE(op, "null op");
+  REQUIRE(kind == HH_PREC_NONE || kind == HH_PREC_JACOBI || kind == HH_PREC_SHIFTED_LAPLACE,
+          "unknown preconditioner kind %d", kind);
+  if (kind == HH_PREC_SHIFTED_LAPLACE) {
+    REQUIRE(sweeps >= 1 && sweeps <= 64, "sweeps must be in [1, 64]");
+    REQUIRE(damping > 0, "damping must be positive");
+  }
+  op->pkind = kind;
+  op->beta = beta;
+  op->sweeps = kind == HH_PREC_SHIFTED_LAPLACE ? sweeps : 1;
+  op->damping = kind == HH_PREC_SHIFTED_LAPLACE ? damping : 1.0;
+  // A_beta mass term: omega^2 (1 + i beta) / (s1 s2 c^2) == build_A_matrix(c / sqrt(1 + i beta))
+  op->mshift = make_double2(1.0, beta);
+  GUARD_END
+}
+
+static void apply_mode(hh_op* op, const double2* x, double2* y, int mode) {
+  switch (mode) {
+    case HH_APPLY_A: run_stencil(op, EPI_AX, x, nullptr, nullptr, y, nullptr, false); break;
+    case HH_APPLY_JACOBI_A: run_stencil(op, EPI_JAC, x, nullptr, nullptr, y, nullptr, false); break;
+    case HH_APPLY_PREC:
+      REQUIRE(x != y, "in-place preconditioner apply not supported");
+      apply_M(op, x, y);
+      break;
+    case HH_APPLY_PREC_A: apply_MA(op, x, nullptr, y); break;
+    default: fail(HH_ERR_INVALID, "unknown apply mode %d", mode);
+  }
+}
+
+HH_API int hh_op_apply(hh_op* op, const double* x, double* y, int mode) {
+  GUARD_BEGIN
+  REQUIRE(op && x && y, "null argument");
+  HIPC(hipSetDevice(op->ctx->device));
+  if (!op->hx) op->hx = dalloc<double2>(op->nloc);
+  if (!op->hy) op->hy = dalloc<double2>(op->nloc);
+  hipStream_t s = op->ctx->stream;
+  HIPC(hipMemcpyAsync(op->hx, x, op->nloc * sizeof(double2), hipMemcpyHostToDevice, s));
+  // hy doubles as residual scratch for the SL preconditioner: use a fresh target buffer
+  double2* dst = op->hy;
+  apply_mode(op, op->hx, dst, mode);
+  HIPC(hipMemcpyAsync(y, dst, op->nloc * sizeof(double2), hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  GUARD_END
+}
+
+HH_API int hh_op_diagonal(hh_op* op, double* d) {
+  GUARD_BEGIN
+  REQUIRE(op && d, "null argument");
+  HIPC(hipSetDevice(op->ctx->device));
+  if (!op->hy) op->hy = dalloc<double2>(op->nloc);
+  run_point(op, PT_DIAG, nullptr, op->hy, false);
+  HIPC(hipMemcpyAsync(d, op->hy, op->nloc * sizeof(double2), hipMemcpyDeviceToHost,
+                      op->ctx->stream));
+  HIPC(hipStreamSynchronize(op->ctx->stream));
+  GUARD_END
+}
+
+// ------------------------------------------------------------------ vectors
+HH_API int hh_vec_create(hh_op* op, hh_vec** v) {
+  GUARD_BEGIN
+  REQUIRE(op && v, "null argument");
+  HIPC(hipSetDevice(op->ctx->device));
+  hh_vec* x = new hh_vec();
+  x->op = op;
+  try {
+    x->d = dalloc<double2>(op->nloc);
+    HIPC(hipMemset(x->d, 0, op->nloc * sizeof(double2)));
+  } catch (...) {
+    delete x;
+    throw;
+  }
+  *v = x;
+  GUARD_END
+}
+
+HH_API int hh_vec_destroy(hh_vec* v) {
+  GUARD_BEGIN
+  if (!v) return HH_OK;
+  (void)hipSetDevice(v->op->ctx->device);
+  (void)hipStreamSynchronize(v->op->ctx->stream);
+  dfree(v->d);
+  delete v;
+  GUARD_END
+}
+
+HH_API int hh_vec_upload(hh_vec* v, const double* host) {
+  GUARD_BEGIN
+  REQUIRE(v && host, "null argument");
+  HIPC(hipSetDevice(v->op->ctx->device));
+  HIPC(hipMemcpyAsync(v->d, host, v->op->nloc * sizeof(double2), hipMemcpyHostToDevice,
+                      v->op->ctx->stream));
+  HIPC(hipStreamSynchronize(v->op->ctx->stream));
+  GUARD_END
+}
+
+HH_API int hh_vec_download(hh_vec* v, double* host) {
+  GUARD_BEGIN
+  REQUIRE(v && host, "null argument");
+  HIPC(hipSetDevice(v->op->ctx->device));
+  HIPC(hipMemcpyAsync(host, v->d, v->op->nloc * sizeof(double2), hipMemcpyDeviceToHost,
+                      v->op->ctx->stream));
+  HIPC(hipStreamSynchronize(v->op->ctx->stream));
+  GUARD_END
+}
+
+HH_API int hh_vec_fill_hash(hh_vec* v, uint64_t seed) {
+  GUARD_BEGIN
+  REQUIRE(v, "null vec");
+  hh_op* op = v->op;
+  HIPC(hipSetDevice(op->ctx->device));
+  launch_fill_hash(v->d, op->nloc, (size_t)op->jb * op->n, seed, op->ctx->stream);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(op->ctx->stream));
+  GUARD_END
+}
+
+HH_API int hh_op_apply_dev(hh_op* op, const hh_vec* x, hh_vec* y, int mode) {
+  GUARD_BEGIN
+  REQUIRE(op && x && y && x->op == op && y->op == op, "vectors must belong to this operator");
+  REQUIRE(x != y, "in-place apply not supported (the stencil reads neighbours)");
+  HIPC(hipSetDevice(op->ctx->device));
+  apply_mode(op, x->d, y->d, mode);
+  HIPC(hipStreamSynchronize(op->ctx->stream));
+  GUARD_END
+}
+
+HH_API int hh_op_time_apply(hh_op* op, const hh_vec* x, hh_vec* y, int mode, int iters,
+                            double* total_ms, double* kernel_ms) {
+  GUARD_BEGIN
+  REQUIRE(op && x && y && x != y && iters >= 1 && total_ms && kernel_ms, "bad arguments");
+  HIPC(hipSetDevice(op->ctx->device));
+  hipStream_t s = op->ctx->stream;
+  std::vector<hipEvent_t> k0(iters), k1(iters);
+  for (int i = 0; i < iters; ++i) {
+    HIPC(hipEventCreate(&k0[i]));
+    HIPC(hipEventCreate(&k1[i]));
+  }
+  hipEvent_t t0, t1;
+  HIPC(hipEventCreate(&t0));
+  HIPC(hipEventCreate(&t1));
+  HIPC(hipStreamSynchronize(s));
+  HIPC(hipEventRecord(t0, s));
+  for (int i = 0; i < iters; ++i) {
+    op->tk0 = k0[i];
+    op->tk1 = k1[i];
+    apply_mode(op, x->d, y->d, mode);
+  }
+  op->tk0 = op->tk1 = nullptr;
+  HIPC(hipEventRecord(t1, s));
+  HIPC(hipEventSynchronize(t1));
+  float ms = 0.f;
+  HIPC(hipEventElapsedTime(&ms, t0, t1));
+  *total_ms = ms;
+  double ksum = 0.0;
+  for (int i = 0; i < iters; ++i) {
+    float km = 0.f;
+    HIPC(hipEventElapsedTime(&km, k0[i], k1[i]));
+    ksum += km;
+    (void)hipEventDestroy(k0[i]);
+    (void)hipEventDestroy(k1[i]);
+  }
+  *kernel_ms = ksum / iters;
+  (void)hipEventDestroy(t0);
+  (void)hipEventDestroy(t1);
+  GUARD_END
+}
+
+HH_API int hh_op_last_stats(hh_op* op, hh_stats* st) {
+  GUARD_BEGIN
+  REQUIRE(op && st, "null argument");
+  *st = op->stats;
+  GUARD_END
+}
+
+// ------------------------------------------------------------------- GMRES
+// Control flow of scipy 1.15.3 gmres (iterative.py:582-840), which code.py:516 calls.
+HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double atol,
+                    int restart, long maxiter, int legacy_maxiter, int reorth, double* hist,
+                    long hist_cap, hh_gmres_callback cb, void* user, long* iters_out,
+                    int* info_out, double* rnorm_out, double* bnorm_out) {
+  GUARD_BEGIN
+  REQUIRE(op && bv && xv && bv->op == op && xv->op == op && bv != xv, "bad vectors");
+  REQUIRE(maxiter >= 1, "maxiter must be >= 1");
+  REQUIRE(rtol >= 0 && atol >= 0, "tolerances must be non-negative");
+  hh_ctx* c = op->ctx;
+  HIPC(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const auto t_start = std::chrono::steady_clock::now();
+  op->stats = hh_stats{};
+  if (restart > (long)op->n * op->n) restart = (int)((long)op->n * op->n);
+  ensure_gmres(op, restart);
+  const size_t L = op->nloc;
+  const size_t ldv = L;
+  double2* V = op->V;
+  const double2* b = bv->d;
+  double2* x = xv->d;
+  GivensState& g = op->gs;
+  const double eps = std::numeric_limits<double>::epsilon();
+  const int blocks = stream_blocks(L);
+  double st[8];
+
+  // red[4] = |b|^2 (= |r|^2 while x0 == 0), red[2] = |x0|^2
+  norm2(op, b, 4);
+  norm2(op, x, 2);
+  read_dev(op, op->red, st, 6);
+  const double bnrm2 = std::sqrt(st[4]);
+  const bool x_any = st[2] > 0.0;
+  if (bnorm_out) *bnorm_out = bnrm2;
+  atol = std::max(atol, rtol * bnrm2);
+  auto finish = [&](long it, int info, double rn) {
+    if (iters_out) *iters_out = it;
+    if (info_out) *info_out = info;
+    if (rnorm_out) *rnorm_out = rn;
+    op->stats.inner_iterations = it;
+    op->stats.solve_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+  };
+  if (bnrm2 == 0.0) {
+    launch_scale_copy(b, x, L, 1.0, s);
+    HIPC(hipStreamSynchronize(s));
+    finish(0, 0, 0.0);
+    return HH_OK;
+  }
+  // Mb_nrm2 = ||psolve(b)||; V[0] = M b, red[5] = |M b|^2 (= |M r|^2 while x0 == 0)
+  apply_M(op, b, V);
+  norm2(op, V, 5);
+  read_dev(op, op->red + 5, st, 1);
+  const double Mb_nrm2 = std::sqrt(st[0]);
+  double ptol_max_factor = 1.0;
+  double ptol = Mb_nrm2 * std::min(ptol_max_factor, atol / bnrm2);
+  double presid = 0.0, rnorm = 0.0;
+  long inner = 0;
+  bool legacy = legacy_maxiter != 0;
+
+  for (long iteration = 0; iteration < maxiter; ++iteration) {
+    if (iteration == 0) {
+      if (x_any) residual(op, b, x, V, 4);  // V[0] = M (b - A x0); red[4..5]
+      read_dev(op, op->red + 4, st, 1);
+      if (std::sqrt(st[0]) < atol) {
+        finish(0, 0, std::sqrt(st[0]));
+        return HH_OK;
+      }
+    }
+    // v[0] = psolve(r) / ||psolve(r)||, S[0] = ||psolve(r)|| (lazy scale)
+    launch_gmres_start(g, op->red, 4, 5, s);
+    bool breakdown = false;
+    int col = 0;
+    for (col = 0; col < restart; ++col) {
+      double2* vcol = V + (size_t)col * ldv;
+      double2* w = V + (size_t)(col + 1) * ldv;
+      apply_MA(op, vcol, g.vscale + col, w);  // w = M A v_col
+      const int K = col + 1;
+      // classical Gram-Schmidt: raw dots u_k^H w (+ |w|^2), then w -= sum h_k v_k, |w|^2
+      launch_multidot(V, ldv, K, w, L, op->partials, blocks, s);
+      launch_reduce(op->partials, blocks, 2 * K + 2, 2 * K + 1, op->red + 16, s);
+      allreduce_sum_dev(op, op->red + 16, 2 * K + 1);
+      launch_update(V, ldv, K, op->red + 16, g.vscale, w, w, L, op->partials, blocks, s);
+      launch_reduce(op->partials, blocks, kMaxNorms, 1, op->red + 8, s);
+      allreduce_sum_dev(op, op->red + 8, 1);
+      if (reorth) {
+        // CGS2: project once more; the H column is the sum of both passes' dots, h0 stays
+        // the first pass's |w| (scipy's h0 is taken before orthogonalisation).
+        launch_multidot(V, ldv, K, w, L, op->partials, blocks, s);
+        launch_reduce(op->partials, blocks, 2 * K + 2, 2 * K, op->red + 96, s);
+        allreduce_sum_dev(op, op->red + 96, 2 * K);
+        launch_update(V, ldv, K, op->red + 96, g.vscale, w, w, L, op->partials, blocks, s);
+        launch_reduce(op->partials, blocks, kMaxNorms, 1, op->red + 8, s);
+        allreduce_sum_dev(op, op->red + 8, 1);
+        launch_add_small(op->red + 96, op->red + 16, 2 * K, s);
+      }
+      launch_gmres_column(g, col, op->red + 16, op->red + 8, eps, s);
+      HIPC(hipGetLastError());
+      read_dev(op, g.status, st, 4);
+      presid = st[0];
+      breakdown = st[1] != 0.0;
+      inner += 1;
+      if (hist && inner - 1 < hist_cap) hist[inner - 1] = presid / bnrm2;
+      if (cb) cb(user, inner, presid / bnrm2);
+      if (legacy && inner == maxiter) break;
+      if (presid <= ptol || breakdown) break;
+    }
+    if (col == restart) col = restart - 1;  // loop ran to completion
+    op->stats.restarts++;
+    launch_gmres_solve(g, col, s);
+    launch_xupdate(V, ldv, col + 1, g.ycoef, x, L, blocks, s);
+    residual(op, b, x, V, 4);  // r = b - A x; V[0] = M r for the next cycle
+    read_dev(op, op->red + 4, st, 1);
+    rnorm = std::sqrt(st[0]);
+    if (legacy && inner == maxiter) {
+      finish(inner, rnorm <= atol ? 0 : (int)std::min<long>(maxiter, 0x7fffffff), rnorm);
+      return HH_OK;
+    }
+    if (rnorm <= atol) break;
+    else if (breakdown) break;
+    else if (presid <= ptol) ptol_max_factor = std::max(eps, 0.25 * ptol_max_factor);
+    else ptol_max_factor = std::min(1.0, 1.5 * ptol_max_factor);
+    ptol = presid * std::min(ptol_max_factor, atol / rnorm);
+  }
+  finish(inner, rnorm <= atol ? 0 : (int)std::min<long>(maxiter, 0x7fffffff), rnorm);
+  GUARD_END
+}

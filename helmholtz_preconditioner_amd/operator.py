@@ -1,0 +1,245 @@
+"""Device Helmholtz operator: drop-in for the reference's ``build_A_matrix`` / ``A @ x``.
+
+Reference (bocchs/helmholtz-preconditioner, code.py):
+  build_A_matrix(b, const, eta, omega, h, n, c_mat) -> scipy sparse A   code.py:202-219
+  A @ x   (scipy csr_matvec inside gmres, A passed at code.py:516)
+
+Here ``build_A_matrix`` returns a :class:`DeviceOperator`, a
+``scipy.sparse.linalg.LinearOperator`` whose matvec runs the hand-written gfx950
+stencil kernel (helmholtz_preconditioner_amd/csrc/stencil.hip).  The CSR matrix is
+never assembled: the operator holds 1-D PML tables and the pre-transposed 1/c^2
+field of its row slab in HBM.  It therefore drops into
+``scipy.sparse.linalg.gmres(A, f, ...)`` unchanged (each matvec is a host<->device
+round trip), and into this package's device-resident :func:`gmres`.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import scipy.sparse.linalg
+
+from . import _ffi
+from ._ffi import check, lib
+from .context import Context, default_context
+
+
+def _medium_arguments(c_mat, n):
+    """Map the reference's c_mat to (host array | None, c_const, mass_scale).
+
+    * real (n+2)^2 array -> streamed 1/c^2 field (or a constant medium when every
+      entry is equal: then no 2-D field is stored or read);
+    * complex c_mat = |c| * z with one phase z for every entry (the shifted-Laplace
+      trick c_mat / sqrt(1 + i beta)) -> |c| field and mass scale 1/z^2, which gives the
+      reference's omega^2 / (s1 s2 c_mat^2) exactly in exact arithmetic.
+    """
+    c = np.asarray(c_mat)
+    if c.ndim != 2 or c.shape[0] < n + 2 or c.shape[1] < n + 2:
+        raise ValueError(f"c_mat must be at least ({n + 2}, {n + 2}); got {c.shape}")
+    # the reference reads c_mat[i-1, j-1] for i, j in 1..n only (code.py:108)
+    used = c[:n, :n]
+    mass = 1.0 + 0.0j
+    if np.iscomplexobj(used):
+        mag = np.abs(used)
+        if np.any(mag == 0):
+            raise ValueError("c_mat has zero entries")
+        phase = used / mag
+        z = phase.flat[0]
+        if not np.allclose(phase, z, rtol=0, atol=1e-14):
+            raise ValueError("complex c_mat must have a single common phase (c / sqrt(1 + i beta))")
+        mass = 1.0 / (z * z)
+        used = mag
+        c = np.abs(c)
+    used = np.asarray(used, dtype=np.float64)
+    if np.all(used == used.flat[0]):
+        return None, float(used.flat[0]), mass
+    full = np.ascontiguousarray(np.asarray(c, dtype=np.float64)[: n + 2, : n + 2])
+    return full, 0.0, mass
+
+
+class DeviceVector:
+    """A complex vector resident in HBM, laid out as this rank's slab of the operator."""
+
+    def __init__(self, op: "DeviceOperator", data=None):
+        self.op = op
+        h = ctypes.c_void_p()
+        check(lib.hh_vec_create(op.handle, ctypes.byref(h)))
+        self._h = h
+        if data is not None:
+            self.upload(data)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def upload(self, data):
+        a = np.ascontiguousarray(np.ravel(data), dtype=np.complex128)
+        if a.size != self.op.local_size:
+            raise ValueError(f"expected {self.op.local_size} values, got {a.size}")
+        check(lib.hh_vec_upload(self._h, _ffi.dptr(a)))
+
+    def download(self):
+        out = np.empty(self.op.local_size, dtype=np.complex128)
+        check(lib.hh_vec_download(self._h, _ffi.dptr(out)))
+        return out
+
+    def fill_hash(self, seed: int = 0):
+        check(lib.hh_vec_fill_hash(self._h, ctypes.c_uint64(seed)))
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self.op._h is not None:
+            lib.hh_vec_destroy(self._h)
+        self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceOperator(scipy.sparse.linalg.LinearOperator):
+    """The PML Helmholtz operator A of code.py:202, applied matrix-free on the GPU.
+
+    ``shape`` is (local, local): the whole N = n^2 system on a single rank, this
+    rank's slab when the context spans several ranks.
+    """
+
+    def __init__(self, b, const, eta, omega, h, n, c_mat, context: Context | None = None):
+        self.ctx = context or default_context()
+        self.b, self.const, self.eta, self.omega, self.h, self.n = b, const, eta, complex(omega), h, n
+        host, c_const, mass = _medium_arguments(c_mat, n)
+        self.constant_medium = host is None
+        hnd = ctypes.c_void_p()
+        check(lib.hh_op_create(self.ctx.handle, int(n), int(b), float(const), float(eta),
+                               self.omega.real, self.omega.imag, float(h),
+                               None if host is None else _ffi.dptr(host), float(c_const),
+                               mass.real, mass.imag, ctypes.byref(hnd)))
+        self._h = hnd
+        jb, je = ctypes.c_int(), ctypes.c_int()
+        check(lib.hh_op_local_rows(hnd, ctypes.byref(jb), ctypes.byref(je)))
+        self.row_begin, self.row_end = jb.value, je.value
+        self.local_size = (je.value - jb.value) * n
+        self._precond = (_ffi.HH_PREC_NONE, 0.5, 1, 1.0)
+        super().__init__(dtype=np.complex128, shape=(self.local_size, self.local_size))
+
+    # ----------------------------------------------------------------- plumbing
+    @property
+    def handle(self):
+        if self._h is None:
+            raise RuntimeError("operator destroyed")
+        return self._h
+
+    @property
+    def bytes_per_point(self) -> int:
+        """Algorithmic HBM bytes of one apply per unknown."""
+        return 32 if self.constant_medium else 40
+
+    def set_preconditioner(self, kind: int, beta: float = 0.5, sweeps: int = 1, damping: float = 1.0):
+        check(lib.hh_op_set_precond(self.handle, int(kind), float(beta), int(sweeps), float(damping)))
+        self._precond = (kind, beta, sweeps, damping)
+
+    def vector(self, data=None) -> DeviceVector:
+        return DeviceVector(self, data)
+
+    # ----------------------------------------------------------- LinearOperator
+    def _apply_host(self, x, mode):
+        x = np.asarray(x)
+        shape = x.shape
+        a = np.ascontiguousarray(np.ravel(x), dtype=np.complex128)
+        if a.size != self.local_size:
+            raise ValueError(f"dimension mismatch: {a.size} != {self.local_size}")
+        y = np.empty_like(a)
+        check(lib.hh_op_apply(self.handle, _ffi.dptr(a), _ffi.dptr(y), int(mode)))
+        return y.reshape(shape)
+
+    def _matvec(self, x):
+        return self._apply_host(x, _ffi.HH_APPLY_A)
+
+    def _rmatvec(self, x):
+        # A is complex-symmetric (A^T == A), so A^H x = conj(A conj(x)).
+        return np.conj(self._apply_host(np.conj(x), _ffi.HH_APPLY_A))
+
+    def _adjoint(self):
+        return scipy.sparse.linalg.LinearOperator(self.shape, matvec=self._rmatvec,
+                                                  rmatvec=self._matvec, dtype=self.dtype)
+
+    def diagonal(self):
+        """A.diagonal() of the local slab (c5 of code.py:107-109)."""
+        d = np.empty(self.local_size, dtype=np.complex128)
+        check(lib.hh_op_diagonal(self.handle, _ffi.dptr(d)))
+        return d
+
+    def apply_device(self, x: DeviceVector, y: DeviceVector, mode: int = _ffi.HH_APPLY_A):
+        check(lib.hh_op_apply_dev(self.handle, x.handle, y.handle, int(mode)))
+
+    def time_apply(self, x: DeviceVector, y: DeviceVector, iters: int, mode: int = _ffi.HH_APPLY_A):
+        """(total_ms, avg stencil-kernel ms) over `iters` back-to-back device applies."""
+        t, k = ctypes.c_double(), ctypes.c_double()
+        check(lib.hh_op_time_apply(self.handle, x.handle, y.handle, int(mode), int(iters),
+                                   ctypes.byref(t), ctypes.byref(k)))
+        return t.value, k.value
+
+    def stats(self):
+        s = _ffi.HHStats()
+        check(lib.hh_op_last_stats(self.handle, ctypes.byref(s)))
+        return {f: getattr(s, f) for f, _ in _ffi.HHStats._fields_}
+
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            lib.hh_op_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def build_A_matrix(b, const, eta, omega, h, n, c_mat, context: Context | None = None):
+    """Drop-in for ``build_A_matrix`` (code.py:202): same arguments, same operator.
+
+    Returns a :class:`DeviceOperator` (a LinearOperator) instead of a scipy CSR
+    matrix; ``A @ x`` / ``A.matvec(x)`` / ``A.diagonal()`` behave like the CSR's.
+    """
+    return DeviceOperator(b, const, eta, omega, h, n, c_mat, context=context)
+
+
+# ----------------------------------------------------------------- preconditioners
+class DevicePreconditioner(scipy.sparse.linalg.LinearOperator):
+    """An M for the reference's preconditioner slot (code.py:510-511) that runs on the
+    device.  Pass it as ``M=`` to :func:`helmholtz_preconditioner_amd.gmres`; it is also
+    a LinearOperator (host round trip) so ``scipy.sparse.linalg.gmres`` accepts it."""
+
+    kind = _ffi.HH_PREC_NONE
+
+    def __init__(self, A: DeviceOperator, beta=0.5, sweeps=1, damping=1.0):
+        self.A, self.beta, self.sweeps, self.damping = A, beta, sweeps, damping
+        super().__init__(dtype=np.complex128, shape=A.shape)
+
+    def configure(self):
+        self.A.set_preconditioner(self.kind, self.beta, self.sweeps, self.damping)
+
+    def _matvec(self, x):
+        self.configure()
+        return self.A._apply_host(x, _ffi.HH_APPLY_PREC)
+
+
+class Jacobi(DevicePreconditioner):
+    """M = diag(A)^-1 (BASELINE config 2), fused into the stencil epilogue."""
+
+    kind = _ffi.HH_PREC_JACOBI
+
+    def __init__(self, A: DeviceOperator):
+        super().__init__(A)
+
+
+class ShiftedLaplace(DevicePreconditioner):
+    """M ~= A_beta^-1, A_beta = build_A_matrix(..., c_mat / sqrt(1 + i beta)) (BASELINE
+    config 3), approximated by `sweeps` damped-Jacobi sweeps from a zero guess."""
+
+    kind = _ffi.HH_PREC_SHIFTED_LAPLACE
+
+    def __init__(self, A: DeviceOperator, beta=0.5, sweeps=4, damping=0.7):
+        super().__init__(A, beta, sweeps, damping)

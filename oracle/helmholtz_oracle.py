@@ -1,0 +1,244 @@
+"""CPU oracle for the Helmholtz operator apply and GMRES solve.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in the product package
+(`helmholtz_preconditioner_amd`) imports this module.  Only `tests/`,
+`__graft_entry__.smoke()` and the `cpu_baseline` leg of `bench.py` may use
+it, and only as the checker / reported CPU baseline, never as the thing
+measured or shipped.
+
+What it is: a vectorised numpy/scipy restatement of the reference's hot path
+(`/root/reference/code.py`, bocchs/helmholtz-preconditioner):
+
+* PML profiles            sigma1/sigma2/s1/s2    code.py:11-33
+* stencil coefficients    get_A_diag_block_coeffs code.py:70-115,
+                          get_upper/lower_A_block code.py:130-154
+* sparse assembly         get_A_block / build_A_matrix code.py:157-219
+* apply                   ``A @ x`` (scipy csr_matvec; A passed at code.py:516)
+* solve                   scipy.sparse.linalg.gmres(A, f, M=..., tol=...) code.py:516
+  -- scipy is the reference's third-party dependency; the container pins
+  scipy 1.15.3 (no requirements file in the reference).  The solve leg calls
+  scipy's own gmres, with ``rtol=`` instead of the removed ``tol=``.
+* inputs                  init_c1_mat/init_c2_mat/init_f1_mat/init_f2_mat code.py:39-66
+
+Parity pinning: every function here is checked in ``tests/test_oracle.py``
+against golden vectors in ``tests/golden/`` that were produced by importing
+the reference ``code.py`` itself (script: ``tests/golden/make_golden.py``).
+
+Quirks reproduced as-is:
+  Q3  velocity read as c_mat[i-1, j-1] (transposed, shifted one cell),
+  Q4  sigma2 is one-sided (PML only at x2 <= eta; Dirichlet top).
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.sparse
+import scipy.sparse.linalg
+
+__all__ = [
+    "sigma1", "sigma2", "s1", "s2", "stencil_coefficients", "build_A_matrix",
+    "init_c1_mat", "init_c2_mat", "init_f1_mat", "init_f2_mat",
+    "jacobi_preconditioner", "shifted_laplace_jacobi", "gmres_reference",
+    "problem_params", "slab_apply_emulated",
+]
+
+
+# --------------------------------------------------------------------------
+# PML profiles (code.py:11-33), vectorised.  Scalar branch logic kept exactly.
+# --------------------------------------------------------------------------
+def sigma1(x, const, eta):
+    """Two-sided PML damping, code.py:11-18."""
+    x = np.asarray(x, dtype=np.float64)
+    lo = const / eta * ((x - eta) / eta) ** 2
+    hi = const / eta * ((x - 1 + eta) / eta) ** 2
+    return np.where(x <= eta, lo, np.where(x >= 1 - eta, hi, 0.0))
+
+
+def sigma2(x, const, eta):
+    """One-sided (bottom only) PML damping, code.py:20-25 (quirk Q4)."""
+    x = np.asarray(x, dtype=np.float64)
+    lo = const / eta * ((x - eta) / eta) ** 2
+    return np.where(x <= eta, lo, 0.0)
+
+
+def s1(x, const, eta, omega):
+    """s1 = (1 + i*sigma1/omega)^-1, code.py:27-29."""
+    return 1.0 / (1 + 1j * sigma1(x, const, eta) / omega)
+
+
+def s2(x, const, eta, omega):
+    """s2 = (1 + i*sigma2/omega)^-1, code.py:31-33."""
+    return 1.0 / (1 + 1j * sigma2(x, const, eta) / omega)
+
+
+# --------------------------------------------------------------------------
+# Stencil coefficients.  Unknown p = (j-1)*n + (i-1); i is the fast axis
+# (x1 = i*h), j the slow axis / layer (x2 = j*h)  -- code.py:81-113, 206-218.
+# --------------------------------------------------------------------------
+def stencil_coefficients(const, eta, omega, h, n, c_mat):
+    """Return (W, E, S, N, D) as (n, n) complex arrays indexed [j-1, i-1].
+
+    W = c1 (neighbour i-1), E = c2 (i+1), S = c3 (j-1), N = c4 (j+1),
+    D = c5 (diagonal); formulas of code.py:83-109.  Coefficients of neighbours
+    outside 1..n are returned too (they still enter D, code.py:107-109) but are
+    dropped by the assembly.  ``c_mat`` is (n+2, n+2) real (or complex for the
+    shifted-Laplace operator) and is read as c_mat[i-1, j-1] (quirk Q3).
+    """
+    idx = np.arange(1, n + 1, dtype=np.float64)
+    I = idx[None, :]          # i along columns (fast axis)
+    J = idx[:, None]          # j along rows   (slow axis)
+    inv_h2 = 1 / h ** 2
+    W = inv_h2 * (s1((I - .5) * h, const, eta, omega) / s2(J * h, const, eta, omega))
+    E = inv_h2 * (s1((I + .5) * h, const, eta, omega) / s2(J * h, const, eta, omega))
+    S = inv_h2 * (s2((J - .5) * h, const, eta, omega) / s1(I * h, const, eta, omega))
+    N = inv_h2 * (s2((J + .5) * h, const, eta, omega) / s1(I * h, const, eta, omega))
+    # c_mat[i-1, j-1] at (row j-1, col i-1) of our [j, i] layout -> transpose.
+    cc = np.asarray(c_mat)[:n, :n].T
+    D = omega ** 2 / (s1(I * h, const, eta, omega) * s2(J * h, const, eta, omega) * cc ** 2) \
+        - (W + E + S + N)
+    return W, E, S, N, D
+
+
+def build_A_matrix(b, const, eta, omega, h, n, c_mat):
+    """Global N x N CSR operator, same signature as code.py:202.
+
+    Offsets {-n, -1, 0, +1, +n}; the +-1 entries are structurally absent at
+    layer boundaries (block_diag of per-layer tridiagonals, code.py:213-218).
+    ``b`` is unused by the assembly, exactly as in the reference.
+    """
+    W, E, S, N, D = stencil_coefficients(const, eta, omega, h, n, c_mat)
+    NN = n * n
+    lower1 = W[:, 1:]                     # entry (p, p-1) for i >= 2
+    upper1 = E[:, :-1]                    # entry (p, p+1) for i <= n-1
+    rows_l1 = (np.arange(n)[:, None] * n + np.arange(1, n)[None, :]).ravel()
+    rows_u1 = (np.arange(n)[:, None] * n + np.arange(0, n - 1)[None, :]).ravel()
+    rows_d = np.arange(NN)
+    rows_ln = np.arange(n, NN)            # (p, p-n) for j >= 2 : coefficient S at row p
+    rows_un = np.arange(0, NN - n)        # (p, p+n) for j <= n-1 : coefficient N at row p
+    rows = np.concatenate([rows_ln, rows_l1, rows_d, rows_u1, rows_un])
+    cols = np.concatenate([rows_ln - n, rows_l1 - 1, rows_d, rows_u1 + 1, rows_un + n])
+    vals = np.concatenate([S[1:, :].ravel(), lower1.ravel(), D.ravel(), upper1.ravel(),
+                           N[:-1, :].ravel()])
+    A = scipy.sparse.csr_matrix((vals, (rows, cols)), shape=(NN, NN), dtype=np.complex128)
+    A.sort_indices()
+    return A
+
+
+# --------------------------------------------------------------------------
+# Inputs (code.py:39-66)
+# --------------------------------------------------------------------------
+def init_c1_mat(r1, r2, n):
+    x_i = np.linspace(0, 1, n + 2)
+    xx, yy = np.meshgrid(x_i, x_i)
+    return 4 / 3 * (1 - .5 * np.exp(-32 * ((xx - r1) ** 2 + (yy - r2) ** 2)))
+
+
+def init_c2_mat(n):
+    x_i = np.linspace(0, 1, n + 2)
+    xx, yy = np.meshgrid(x_i, x_i)
+    return 4 / 3 * (1 - .5 * np.exp(-32 * ((xx - .5) ** 2)))
+
+
+def init_f1_mat(r1, r2, omega, n):
+    x_i = np.linspace(0, 1, n + 2)
+    xx, yy = np.meshgrid(x_i[1:-1], x_i[1:-1])
+    return np.exp(-(4 * omega / np.pi) ** 2 * ((xx - r1) ** 2 + (yy - r2) ** 2))
+
+
+def init_f2_mat(r1, r2, d1, d2, omega, n):
+    x_i = np.linspace(0, 1, n + 2)
+    xx, yy = np.meshgrid(x_i[1:-1], x_i[1:-1])
+    return np.exp(-4 * omega * ((xx - r1) ** 2 + (yy - r2) ** 2)) \
+        * np.exp(1j * omega * (xx * d1 + yy * d2))
+
+
+def problem_params(n, b, wave_num, alpha):
+    """omega, h, eta exactly as run_solver derives them (code.py:442-444)."""
+    omega = 2 * np.pi * wave_num + 1j * alpha
+    h = 1 / (n + 1)
+    eta = b * h
+    return omega, h, eta
+
+
+# --------------------------------------------------------------------------
+# Preconditioners filling the reference's M slot (code.py:510-511).
+# --------------------------------------------------------------------------
+def jacobi_preconditioner(A):
+    """M = diag(A)^-1 as a LinearOperator (BASELINE config 2)."""
+    dinv = 1.0 / A.diagonal()
+    N = A.shape[0]
+    return scipy.sparse.linalg.LinearOperator((N, N), matvec=lambda x: dinv * np.ravel(x),
+                                              dtype=np.complex128)
+
+
+def shifted_laplace_jacobi(b, const, eta, omega, h, n, c_mat, beta=0.5, sweeps=4,
+                           damping=0.7):
+    """Shifted-Laplace preconditioner M ~= A_beta^-1 (BASELINE config 3).
+
+    A_beta = build_A_matrix(..., c_mat / sqrt(1 + i*beta)) -- the reference's own
+    assembly with the complex-shifted mass term.  Its inverse
+    is approximated by ``sweeps`` damped-Jacobi sweeps from a zero guess:
+        z_0 = 0,  z_{k+1} = z_k + damping * D_beta^-1 (r - A_beta z_k).
+    The first sweep is just damping*D^-1 r.  Must match the device kernel
+    sequence in csrc/precond.hip (same recurrence, same order).
+    """
+    Ab = build_A_matrix(b, const, eta, omega, h, n, np.asarray(c_mat) / np.sqrt(1 + 1j * beta))
+    dinv = 1.0 / Ab.diagonal()
+    NN = n * n
+
+    def mv(r):
+        r = np.ravel(r)
+        z = damping * dinv * r
+        for _ in range(sweeps - 1):
+            z = z + damping * dinv * (r - Ab @ z)
+        return z
+
+    return scipy.sparse.linalg.LinearOperator((NN, NN), matvec=mv, dtype=np.complex128), Ab
+
+
+class _Counter:
+    """gmres_counter of code.py:413-420 (counts legacy callbacks)."""
+
+    def __init__(self):
+        self.niter = 0
+        self.history = []
+
+    def __call__(self, rk=None):
+        self.niter += 1
+        self.history.append(float(rk))
+
+
+def gmres_reference(A, b, M=None, rtol=1e-3, restart=20, maxiter=None, x0=None):
+    """scipy.sparse.linalg.gmres exactly as code.py:516 calls it (legacy callback).
+
+    Returns (x, info, presid_history, true_relres).  In legacy callback mode
+    ``maxiter`` caps inner iterations (scipy iterative.py:792,820).
+    """
+    cnt = _Counter()
+    x, info = scipy.sparse.linalg.gmres(A, b, x0=x0, rtol=rtol, restart=restart,
+                                        maxiter=maxiter, M=M, callback=cnt,
+                                        callback_type='legacy')
+    relres = np.linalg.norm(b - A @ x) / np.linalg.norm(b)
+    return x, info, np.array(cnt.history), relres
+
+
+# --------------------------------------------------------------------------
+# Row-slab decomposition emulator (test tier 4): P virtual slabs,
+# each owning layers [j0, j1) with an explicit one-layer halo copy.
+# --------------------------------------------------------------------------
+def slab_apply_emulated(const, eta, omega, h, n, c_mat, x, bounds):
+    """Apply A slab by slab with explicit halo copies; must equal A @ x."""
+    W, E, S, N, D = stencil_coefficients(const, eta, omega, h, n, c_mat)
+    X = np.asarray(x).reshape(n, n)
+    out = []
+    for (j0, j1) in bounds:                       # 0-based layer range
+        loc = X[j0:j1]
+        lo = X[j0 - 1] if j0 > 0 else np.zeros(n, X.dtype)      # halo from rank below
+        hi = X[j1] if j1 < n else np.zeros(n, X.dtype)          # halo from rank above
+        ext = np.vstack([lo[None], loc, hi[None]])
+        y = D[j0:j1] * loc
+        y[:, 1:] += W[j0:j1, 1:] * loc[:, :-1]
+        y[:, :-1] += E[j0:j1, :-1] * loc[:, 1:]
+        y += S[j0:j1] * ext[:-2] * (np.arange(j0, j1) > 0)[:, None]
+        y += N[j0:j1] * ext[2:] * (np.arange(j0, j1) < n - 1)[:, None]
+        out.append(y)
+    return np.vstack(out).ravel()

@@ -1,0 +1,26 @@
+#!/bin/bash
+# One GPU-box session: parity tests, a bench line, and a rocprofv3 kernel-trace profile.
+# Every GPU step has its own time limit; a fault/abort/timeout stops the session.
+# usage: tools/gpu_session.sh TAG [pytest-args...]
+set -u
+TAG=${1:-r01}; shift || true
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+fatal() { case $1 in 124|137|134|139|-6|-11) return 0;; *) return 1;; esac; }
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -5 "$OUT/$name.log"
+  if fatal $rc; then echo "FATAL rc=$rc in $name: stopping"; exit $rc; fi
+  return 0
+}
+rocm-smi --showproductname > "$OUT/smi.log" 2>&1 || true
+step pytest_gpu 900 python -m pytest tests -m gpu -q -x "$@"
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
+step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline --gmres-iters 40
+echo done
