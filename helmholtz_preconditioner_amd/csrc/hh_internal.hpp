@@ -26,6 +26,11 @@ enum Epi : int {
   EPI_SL_SWEEP = 6,  // z' = z + damp (r - Abeta z) / Dbeta   (u = z, in1 = r)
 };
 
+// W/E neighbour exchange of the stencil kernel (see stencil.hip).
+enum XMode : int { XM_LDS = 0, XM_DIRECT = 1, XM_SHFL = 2 };
+// Tuning variant = XM + 3 * (PF - 1) + 6 * NT + 12 * NTU  (0..23).
+constexpr int kNumVariants = 24;
+
 // Pointwise (no-neighbour) operations that need only the diagonal.
 enum PointOp : int {
   PT_DIAG = 0,       // out0 = D
@@ -47,6 +52,7 @@ struct StencilArgs {
   int row_begin, row_end;  // local rows computed by this launch
   int rows_per_block;      // strip height marched by one block
   int tiles_x, tiles_y, tiles_per_xcd;  // XCD-aware tile map
+  int grid_blocks;         // 0: one block per tile; >0: persistent grid of this many blocks
   double2 mshift;          // mass-term multiplier for the shifted operator (EPI_SL_*)
   double damping;          // damped-Jacobi weight (EPI_SL_*)
   const double* in_scale;  // lazily-normalised input: A (s u) = s (A u); nullptr -> 1
@@ -71,7 +77,11 @@ struct PointArgs {
 
 // Kernel launchers (kernels.hip).  All are asynchronous on `stream`.
 void launch_stencil(int epi, bool const_c, const StencilArgs& a, int nblocks_out[1],
-                    hipStream_t stream);
+                    hipStream_t stream, int variant = -1);
+int stencil_default_variant();
+// Streaming roofline probes (probe.hip); returns the probe's bytes per point (0: unknown kind).
+int launch_probe_kind(int kind, int blocks, const double2* u, const double* ic, double2* y,
+                      size_t len, hipStream_t s);
 int stencil_grid_blocks(int n, int rows, int rows_per_block);
 int stencil_rows_per_block(int n, int rows);
 void launch_point(int op, bool const_c, const PointArgs& a, int blocks, hipStream_t stream);

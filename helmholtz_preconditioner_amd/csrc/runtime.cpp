@@ -158,6 +158,10 @@ struct hh_op {
   double* status_h = nullptr;
   // timing hooks
   hipEvent_t tk0 = nullptr, tk1 = nullptr;
+  // tuning (hh_op_tune): stencil variant for the plain apply, rows per block override
+  int variant = -1;
+  int rpb_override = 0;
+  int grid_override = 0;
   hh_stats stats{};
 };
 
@@ -238,10 +242,11 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
     StencilArgs a = make_args(si);
     a.row_begin = r0;
     a.row_end = r1;
-    a.rows_per_block = rpb;
+    a.rows_per_block = (op->rpb_override > 0 && rpb > 1) ? std::min(op->rpb_override, r1 - r0) : rpb;
+    a.grid_blocks = op->grid_override;
     a.partials = op->partials + (size_t)nparts * kMaxNorms;
     int written = 0;
-    launch_stencil(epi, op->const_c, a, &written, c->stream);
+    launch_stencil(epi, op->const_c, a, &written, c->stream, op->variant);
     nparts += written;
   };
 
@@ -867,6 +872,44 @@ HH_API int hh_op_time_apply(hh_op* op, const hh_vec* x, hh_vec* y, int mode, int
     (void)hipEventDestroy(k1[i]);
   }
   *kernel_ms = ksum / iters;
+  (void)hipEventDestroy(t0);
+  (void)hipEventDestroy(t1);
+  GUARD_END
+}
+
+HH_API int hh_op_tune(hh_op* op, int variant, int rows_per_block, int grid_blocks) {
+  GUARD_BEGIN
+  REQUIRE(op, "null op");
+  REQUIRE(grid_blocks >= 0, "grid_blocks must be >= 0");
+  op->grid_override = grid_blocks;
+  REQUIRE(variant >= -1 && variant < kNumVariants, "variant must be in [-1, %d)", kNumVariants);
+  REQUIRE(rows_per_block >= 0 && rows_per_block <= 4096, "rows_per_block must be in [0, 4096]");
+  op->variant = variant;
+  op->rpb_override = rows_per_block;
+  GUARD_END
+}
+
+HH_API int hh_op_probe_stream(hh_op* op, int kind, int blocks, const hh_vec* x, hh_vec* y,
+                              int iters, double* kernel_ms, int* bytes_per_point) {
+  GUARD_BEGIN
+  REQUIRE(op && x && y && x != y && iters >= 1 && kernel_ms && bytes_per_point, "bad arguments");
+  REQUIRE(!op->const_c && op->slabs.size() == 1, "probe needs a heterogeneous single-slab operator");
+  REQUIRE(blocks >= 1 && blocks <= (1 << 20), "blocks out of range");
+  HIPC(hipSetDevice(op->ctx->device));
+  hipStream_t s = op->ctx->stream;
+  hipEvent_t t0, t1;
+  HIPC(hipEventCreate(&t0));
+  HIPC(hipEventCreate(&t1));
+  const int bpp = launch_probe_kind(kind, blocks, x->d, op->slabs[0].invc2, y->d, op->nloc, s);
+  REQUIRE(bpp > 0, "unknown probe kind %d", kind);
+  HIPC(hipEventRecord(t0, s));
+  for (int i = 0; i < iters; ++i) launch_probe_kind(kind, blocks, x->d, op->slabs[0].invc2, y->d, op->nloc, s);
+  HIPC(hipEventRecord(t1, s));
+  HIPC(hipEventSynchronize(t1));
+  float ms = 0.f;
+  HIPC(hipEventElapsedTime(&ms, t0, t1));
+  *kernel_ms = ms / iters;
+  *bytes_per_point = bpp;
   (void)hipEventDestroy(t0);
   (void)hipEventDestroy(t1);
   GUARD_END

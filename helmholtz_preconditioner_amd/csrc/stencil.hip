@@ -22,6 +22,8 @@
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
 
+#include <type_traits>
+
 namespace hh {
 namespace {
 
@@ -58,57 +60,167 @@ __device__ __forceinline__ void block_reduce_store(double (&acc)[kMaxNorms], dou
   }
 }
 
-template <int EPI, bool CONSTC>
-__global__ __launch_bounds__(kStencilThreads) void stencil_kernel(const StencilArgs a) {
-  using T = EpiTraits<EPI>;
-  __shared__ double2 lrow[2][kStencilThreads + 2];
+__device__ __forceinline__ void store2(double2* p, double2 v, bool nt) {
+  if (nt) {
+    __builtin_nontemporal_store(v.x, &p->x);
+    __builtin_nontemporal_store(v.y, &p->y);
+  } else {
+    *p = v;
+  }
+}
 
-  // XCD-aware tile map: consecutive blocks go round-robin over the 8 XCDs, so give each XCD
-  // a contiguous range of tiles (row-band major) -> vertically adjacent tiles share an L2.
+// Per-row operands a thread needs besides the centre column: 1/c^2 and its W/E inputs
+// (block-edge values for XM_LDS, wave-edge values for XM_SHFL, both neighbours for
+// XM_DIRECT).  Loaded unconditionally from clamped (always valid) addresses and masked
+// at use: an exec-masked load makes hipcc drain vmcnt at the join, which would serialise
+// the prefetch pipeline.
+struct RowIn {
+  double ic;
+  double2 eW, eE;
+};
+
+template <bool NTL>
+__device__ __forceinline__ double2 ld2(const double2* p) {
+  if constexpr (NTL) {
+    return make_double2(__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y));
+  } else {
+    return *p;
+  }
+}
+template <bool NTL>
+__device__ __forceinline__ double ld1(const double* p) {
+  if constexpr (NTL) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
+template <int K, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (K < N) {
+    f(std::integral_constant<int, K>{});
+    static_for<K + 1, N>(f);
+  }
+}
+
+// Per-row PML factors (wave-uniform): read through the constant address space so hipcc
+// issues scalar loads into SGPRs (the generic pointer would force vector loads because the
+// kernel also stores through generic pointers).
+using cdouble_p = const __attribute__((address_space(4))) double*;
+
+// XM  : how W/E neighbours are exchanged -- XM_LDS (double-buffered LDS row, one barrier
+//       per row), XM_DIRECT (each lane loads u[i-1], u[i+1]; the lines are L1/L2 hits of
+//       the neighbouring lanes' loads), XM_SHFL (ds_bpermute within the wave, wave-edge
+//       lanes load one extra value).
+// PF  : rows of prefetch distance (1 or 2) for u, 1/c^2 and the edge values.
+// NT  : non-temporal loads of the once-read 1/c^2 stream and stores of the outputs.
+//
+// The row loop is unrolled by the register-ring length: ring slot m always holds row
+// rb-1+m (mod ring), so no value is copied between registers -- a copy of a register with
+// a load still in flight would make hipcc drain vmcnt and serialise the prefetch.
+template <int EPI, bool CONSTC, int XM, int PF, bool NT, bool NTU>
+__device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t);
+
+// Grid: either one block per tile, or a persistent grid of `gridDim.x` blocks (a multiple
+// of 8) in which block L works through the tiles of XCD L % 8 in order, so at any moment
+// each XCD streams one contiguous band window (L2 reuse of band-edge rows).
+template <int EPI, bool CONSTC, int XM, int PF, bool NT, bool NTU>
+__global__ __launch_bounds__(kStencilThreads) void stencil_kernel(const StencilArgs a) {
   const int L = blockIdx.x;
-  const int t = (L & 7) * a.tiles_per_xcd + (L >> 3);
-  if (t >= a.tiles_x * a.tiles_y) return;  // uniform per block, before any barrier
+  const int q = L >> 3, Q = gridDim.x >> 3;
+  const int ntiles = a.tiles_x * a.tiles_y;
+  for (int tt = q; tt < a.tiles_per_xcd; tt += Q) {
+    const int t = (L & 7) * a.tiles_per_xcd + tt;
+    if (t >= ntiles) break;  // uniform per block
+    stencil_tile<EPI, CONSTC, XM, PF, NT, NTU>(a, t);
+  }
+}
+
+template <int EPI, bool CONSTC, int XM, int PF, bool NT, bool NTU>
+__device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) {
+  using T = EpiTraits<EPI>;
+  constexpr int UR = (PF == 1) ? 4 : 6;  // u ring: u_{r-1} .. u_{r+1+PF}
+  constexpr int IR = PF + 1;             // per-row input ring
+  constexpr int UNR = UR;                // unroll (multiple of UR, IR and 2)
+  static_assert(UNR % IR == 0 && UNR % 2 == 0, "ring sizes");
+  __shared__ double2 lrow[2][XM == XM_LDS ? kStencilThreads + 2 : 1];
+
+  // XCD-aware tile map (see stencil_kernel): tile t is a 256-wide strip x one row band.
   const int tx = t % a.tiles_x;
   const int ty = t / a.tiles_x;
   const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
   const int n = a.n;
   const int i0 = tx * kStencilThreads;
   const int i = i0 + tid;
   const bool act = i < n;
-  const int rb = a.row_begin + ty * a.rows_per_block;
-  const int re = min(rb + a.rows_per_block, a.row_end);
+  const int ic_ = min(i, n - 1);  // clamped column for loads
+  // row band (wave-uniform; readfirstlane keeps the row loop and its prefetch branches on
+  // the scalar unit)
+  const int rb = __builtin_amdgcn_readfirstlane(a.row_begin + ty * a.rows_per_block);
+  const int re = __builtin_amdgcn_readfirstlane(min(rb + a.rows_per_block, a.row_end));
 
   auto rowp = [&](int r) -> const double2* {
     return r < 0 ? a.halo_lo : (r >= a.nl ? a.halo_hi : a.u + (size_t)r * n);
   };
+  // which column each lane reads for its W / E inputs, and whether that value is real
+  int iw, ie;
+  bool lw, le;
+  if constexpr (XM == XM_LDS) {
+    iw = i0 - 1; ie = i0 + kStencilThreads; lw = tid == 0; le = tid == kStencilThreads - 1;
+  } else if constexpr (XM == XM_SHFL) {
+    iw = i - lane - 1; ie = i - lane + kWave; lw = lane == 0; le = lane == kWave - 1;
+  } else {
+    iw = i - 1; ie = i + 1; lw = act; le = act;
+  }
+  lw = lw && iw >= 0;
+  le = le && ie < n;
+  iw = max(iw, 0);
+  ie = min(ie, n - 1);
+  if constexpr (XM != XM_DIRECT) {
+    // lanes without an edge duty re-read their own column (an L1 hit) so that the load
+    // stays unconditional
+    iw = lw ? iw : ic_;
+    ie = le ? ie : ic_;
+  }
 
   const double2 z2 = make_double2(0.0, 0.0);
-  double2 AW = z2, AE = z2, R1 = z2;
-  if (act) {
-    AW = a.tab_i[i];
-    AE = a.tab_i[n + i];
-    R1 = a.tab_i[2 * n + i];
-  }
-  const bool west_lane = tid == 0;
-  const bool east_lane = tid == kStencilThreads - 1;
-  const int iw = i0 - 1;
-  const int ie = i0 + kStencilThreads;
-  const bool has_w = iw >= 0;
-  const bool has_e = ie < n;
+  auto load_row_in = [&](int r, RowIn& v) {
+    if constexpr (!CONSTC) v.ic = ld1<NT>(a.invc2 + (size_t)r * n + ic_);
+    else v.ic = a.invc2_const;
+    const double2* rp = rowp(r);
+    v.eW = rp[iw];
+    v.eE = rp[ie];
+  };
+  auto load_u = [&](int r) { return ld2<NTU>(rowp(r) + ic_); };
+  const cdouble_p tabj = (cdouble_p)(a.tab_j);
+  struct Tab {
+    double2 R2, BS, BN, OM;
+  };
+  auto load_tab = [&](int r, Tab& tb) {
+    const int ru = __builtin_amdgcn_readfirstlane(r);
+    const cdouble_p q = tabj + 8 * ru;
+    tb.R2 = make_double2(q[0], q[1]);
+    tb.BS = make_double2(q[2], q[3]);
+    tb.BN = make_double2(q[4], q[5]);
+    tb.OM = make_double2(q[6], q[7]);
+  };
 
-  double2 uS = z2, uC = z2, uN = z2;
-  double icC = a.invc2_const, icN = a.invc2_const;
-  double2 eWc = z2, eEc = z2, eWn = z2, eEn = z2;
-  if (act) {
-    uS = rowp(rb - 1)[i];
-    uC = rowp(rb)[i];
-    uN = rowp(rb + 1)[i];
-    if constexpr (!CONSTC) icC = a.invc2[(size_t)rb * n + i];
+  const double2 AW = a.tab_i[ic_], AE = a.tab_i[n + ic_], R1 = a.tab_i[2 * n + ic_];
+
+  double2 U[UR];
+  RowIn IN[IR];
+  Tab TB[2];
+  // Every load below is unconditional, with its row clamped into rows this band needs
+  // anyway: hipcc's vmcnt bookkeeping takes the minimum over control-flow paths, so a
+  // load under a (even uniform) branch would turn the next wait into vmcnt(0).
+  U[0] = load_u(rb - 1);
+  U[1] = load_u(rb);
+  U[2] = load_u(rb + 1);
+  load_row_in(rb, IN[0]);
+  if constexpr (PF == 2) {
+    U[3] = load_u(min(rb + 2, re));
+    load_row_in(min(rb + 1, re - 1), IN[1]);
   }
-  if (west_lane && has_w) eWc = rowp(rb)[iw];
-  if (east_lane && has_e) eEc = rowp(rb)[ie];
-  const double2* tj = a.tab_j + 4 * rb;
-  double2 R2 = tj[0], BS = tj[1], BN = tj[2], OM = tj[3];
+  load_tab(rb, TB[0]);
 
   double sin = 1.0;
   if constexpr (T::scaled_in) {
@@ -116,99 +228,95 @@ __global__ __launch_bounds__(kStencilThreads) void stencil_kernel(const StencilA
   }
   double acc[kMaxNorms] = {0.0, 0.0};
 
-  for (int r = rb; r < re; ++r) {
-    // ---- prefetch row r+1's operands (used next iteration) ----
-    double2 uNN = z2;
-    double2 R2n = R2, BSn = BS, BNn = BN, OMn = OM;
-    const bool more = (r + 1) < re;
-    if (more) {
-      if (act) {
-        uNN = rowp(r + 2)[i];
-        if constexpr (!CONSTC) icN = a.invc2[(size_t)(r + 1) * n + i];
+  for (int r0 = rb; r0 < re; r0 += UNR) {
+    static_for<0, UNR>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      const int r = r0 + k;
+      const bool live = r < re;  // uniform; steps past the band end only keep the ring going
+      // ---- prefetch (distance PF rows) into ring slots that are dead by now ----
+      U[(k + 2 + PF) % UR] = load_u(min(r + 1 + PF, re));
+      load_row_in(min(r + PF, re - 1), IN[(k + PF) % IR]);
+      load_tab(min(r + 1, re - 1), TB[(k + 1) % 2]);
+      const double2 uS = U[k % UR], uC = U[(k + 1) % UR], uN = U[(k + 2) % UR];
+      const RowIn& in = IN[k % IR];
+      const Tab& tb = TB[k % 2];
+      double2 bin = z2;
+      const size_t p = (size_t)min(r, re - 1) * n + ic_;
+      if constexpr (T::reads_in1) bin = a.in1[p];
+
+      // ---- W/E neighbours ----
+      const double2 uCm = act ? uC : z2;  // columns past n contribute zero (Dirichlet)
+      const double2 eW = lw ? in.eW : z2;
+      const double2 eE = le ? in.eE : z2;
+      double2 uW, uE;
+      if constexpr (XM == XM_LDS) {
+        double2* buf = lrow[k & 1];
+        buf[tid + 1] = uCm;
+        if (tid == 0) buf[0] = eW;
+        if (tid == kStencilThreads - 1) buf[kStencilThreads + 1] = eE;
+        __syncthreads();
+        uW = buf[tid];
+        uE = buf[tid + 2];
+      } else if constexpr (XM == XM_SHFL) {
+        const double2 sw = make_double2(__shfl_up(uCm.x, 1), __shfl_up(uCm.y, 1));
+        const double2 se = make_double2(__shfl_down(uCm.x, 1), __shfl_down(uCm.y, 1));
+        uW = lane == 0 ? eW : sw;
+        uE = lane == kWave - 1 ? eE : se;
+      } else {
+        uW = eW;
+        uE = eE;
       }
-      if (west_lane && has_w) eWn = rowp(r + 1)[iw];
-      if (east_lane && has_e) eEn = rowp(r + 1)[ie];
-      const double2* tn = a.tab_j + 4 * (r + 1);
-      R2n = tn[0];
-      BSn = tn[1];
-      BNn = tn[2];
-      OMn = tn[3];
-    }
-    double2 bin = z2;
-    const size_t p = (size_t)r * n + i;
-    if constexpr (T::reads_in1) {
-      if (act) bin = a.in1[p];
-    }
 
-    // ---- W/E neighbours through LDS (double-buffered: one barrier per row) ----
-    double2* buf = lrow[(r - rb) & 1];
-    buf[tid + 1] = uC;
-    if (west_lane) buf[0] = eWc;
-    if (east_lane) buf[kStencilThreads + 1] = eEc;
-    __syncthreads();
-    const double2 uW = buf[tid];
-    const double2 uE = buf[tid + 2];
+      // ---- coefficients (code.py:83-109) and the five-point product ----
+      const double2 W = cmul(AW, tb.R2);
+      const double2 E = cmul(AE, tb.R2);
+      const double2 S = cmul(tb.BS, R1);
+      const double2 N = cmul(tb.BN, R1);
+      const double2 M = cscale(cmul(tb.OM, R1), in.ic);
+      const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
+      const double2 D = csub(M, sum4);
+      double2 Db = D;
+      if constexpr (T::shifted) Db = csub(cmul(M, a.mshift), sum4);
+      const double2 Dc = (EPI == EPI_SL_SWEEP) ? Db : D;
 
-    // ---- coefficients (code.py:83-109) and the five-point product ----
-    const double2 W = cmul(AW, R2);
-    const double2 E = cmul(AE, R2);
-    const double2 S = cmul(BS, R1);
-    const double2 N = cmul(BN, R1);
-    const double2 M = cscale(cmul(OM, R1), icC);
-    const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
-    const double2 D = csub(M, sum4);
-    double2 Db = D;
-    if constexpr (T::shifted) Db = csub(cmul(M, a.mshift), sum4);
-    const double2 Dc = (EPI == EPI_SL_SWEEP) ? Db : D;
+      double2 Au = cmul(S, uS);
+      Au = cfma(W, uW, Au);
+      Au = cfma(Dc, uC, Au);
+      Au = cfma(E, uE, Au);
+      Au = cfma(N, uN, Au);
 
-    double2 Au = cmul(S, uS);
-    Au = cfma(W, uW, Au);
-    Au = cfma(Dc, uC, Au);
-    Au = cfma(E, uE, Au);
-    Au = cfma(N, uN, Au);
-
-    if (act) {
-      if constexpr (EPI == EPI_AX) {
-        a.out0[p] = cscale(Au, sin);
-      } else if constexpr (EPI == EPI_JAC) {
-        a.out0[p] = cscale(cdiv(Au, D), sin);
-      } else if constexpr (EPI == EPI_RES) {
-        const double2 rr = csub(bin, Au);
-        a.out0[p] = rr;
-        acc[0] += cabs2(rr);
-      } else if constexpr (EPI == EPI_RES_JAC) {
-        const double2 rr = csub(bin, Au);
-        const double2 zz = cdiv(rr, D);
-        a.out0[p] = zz;
-        acc[0] += cabs2(rr);
-        acc[1] += cabs2(zz);
-      } else if constexpr (EPI == EPI_RES_SL) {
-        const double2 rr = csub(bin, Au);
-        a.out0[p] = rr;
-        a.out1[p] = cscale(cdiv(rr, Db), a.damping);
-        acc[0] += cabs2(rr);
-      } else if constexpr (EPI == EPI_SL_FIRST) {
-        const double2 tt = cscale(Au, sin);
-        a.out0[p] = tt;
-        a.out1[p] = cscale(cdiv(tt, Db), a.damping);
-      } else if constexpr (EPI == EPI_SL_SWEEP) {
-        a.out0[p] = cadd(uC, cscale(cdiv(csub(bin, Au), Db), a.damping));
+      if (act && live) {
+        if constexpr (EPI == EPI_AX) {
+          store2(a.out0 + p, cscale(Au, sin), NT);
+        } else if constexpr (EPI == EPI_JAC) {
+          store2(a.out0 + p, cscale(cdiv(Au, D), sin), NT);
+        } else if constexpr (EPI == EPI_RES) {
+          const double2 rr = csub(bin, Au);
+          store2(a.out0 + p, rr, NT);
+          acc[0] += cabs2(rr);
+        } else if constexpr (EPI == EPI_RES_JAC) {
+          const double2 rr = csub(bin, Au);
+          const double2 zz = cdiv(rr, D);
+          store2(a.out0 + p, zz, NT);
+          acc[0] += cabs2(rr);
+          acc[1] += cabs2(zz);
+        } else if constexpr (EPI == EPI_RES_SL) {
+          const double2 rr = csub(bin, Au);
+          store2(a.out0 + p, rr, NT);
+          store2(a.out1 + p, cscale(cdiv(rr, Db), a.damping), NT);
+          acc[0] += cabs2(rr);
+        } else if constexpr (EPI == EPI_SL_FIRST) {
+          const double2 tt = cscale(Au, sin);
+          store2(a.out0 + p, tt, NT);
+          store2(a.out1 + p, cscale(cdiv(tt, Db), a.damping), NT);
+        } else if constexpr (EPI == EPI_SL_SWEEP) {
+          store2(a.out0 + p, cadd(uC, cscale(cdiv(csub(bin, Au), Db), a.damping)), NT);
+        }
       }
-    }
-
-    // ---- rotate the register window ----
-    uS = uC;
-    uC = uN;
-    uN = uNN;
-    icC = icN;
-    eWc = eWn;
-    eEc = eEn;
-    R2 = R2n;
-    BS = BSn;
-    BN = BNn;
-    OM = OMn;
+    });
   }
   block_reduce_store<T::nacc>(acc, a.partials, t);
+  if constexpr (T::nacc > 0 || XM == XM_LDS) __syncthreads();  // LDS reuse by the next tile
 }
 
 // Pointwise operations needing only the diagonal D (or D_beta) of a point.
@@ -256,12 +364,43 @@ __global__ __launch_bounds__(kStencilThreads) void point_kernel(const PointArgs 
   }
 }
 
+// Default exchange/prefetch/store variant for every epilogue (tuned on MI355X, see
+// DESIGN.md "stencil variants"); the benchmark kernel (EPI_AX) can run all 12 variants.
+constexpr int kDefaultVariant = 6;  // XM_LDS, PF 1, NT stores + NT 1/c^2 loads
+
+// Variant table: V = XM + 3 (PF - 1) + 6 NT + 12 NTU  (0..23).
+template <int EPI, bool C, int V>
+struct VariantLaunch {
+  static void go(const StencilArgs& a, int blocks, hipStream_t s) {
+    constexpr int XM = V % 3, PF = (V / 3) % 2 + 1;
+    constexpr bool NT = (V / 6) % 2 == 1, NTU = V >= 12;
+    hipLaunchKernelGGL((stencil_kernel<EPI, C, XM, PF, NT, NTU>), dim3(blocks),
+                       dim3(kStencilThreads), 0, s, a);
+  }
+};
+
+template <int EPI, int V>
+void launch_v(bool const_c, const StencilArgs& a, int blocks, hipStream_t s) {
+  if (const_c) VariantLaunch<EPI, true, V>::go(a, blocks, s);
+  else VariantLaunch<EPI, false, V>::go(a, blocks, s);
+}
+
+template <int EPI, int... Vs>
+void launch_any(int v, bool const_c, const StencilArgs& a, int blocks, hipStream_t s) {
+  bool done = false;
+  ((v == Vs ? (launch_v<EPI, Vs>(const_c, a, blocks, s), done = true) : false), ...);
+  if (!done) launch_v<EPI, kDefaultVariant>(const_c, a, blocks, s);
+}
+
 template <int EPI>
-void launch_stencil_t(bool const_c, const StencilArgs& a, int blocks, hipStream_t s) {
-  if (const_c)
-    hipLaunchKernelGGL((stencil_kernel<EPI, true>), dim3(blocks), dim3(kStencilThreads), 0, s, a);
-  else
-    hipLaunchKernelGGL((stencil_kernel<EPI, false>), dim3(blocks), dim3(kStencilThreads), 0, s, a);
+void launch_stencil_t(bool const_c, const StencilArgs& a, int blocks, hipStream_t s, int v) {
+  if constexpr (EPI == EPI_AX) {
+    launch_any<EPI, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21,
+               22, 23>(v, const_c, a, blocks, s);
+  } else {
+    (void)v;
+    launch_v<EPI, kDefaultVariant>(const_c, a, blocks, s);
+  }
 }
 
 template <int OP>
@@ -275,12 +414,13 @@ void launch_point_t(bool const_c, const PointArgs& a, int blocks, hipStream_t s)
 }  // namespace
 
 int stencil_rows_per_block(int n, int rows) {
-  // Aim for ~4096 tiles (16 blocks per CU over 256 CUs) so the chip stays full while each
-  // block marches a band long enough to amortise its two halo rows.
+  // ~2048 tiles (8 per CU): measured best at 4096^2 (32-row bands, tools/tune_stencil.py);
+  // bands long enough to amortise their two halo rows, a multiple of the 4-row unroll.
   const int tiles_x = (n + kStencilThreads - 1) / kStencilThreads;
-  long want_y = 4096 / tiles_x;
+  long want_y = 2048 / tiles_x;
   if (want_y < 1) want_y = 1;
   int rpb = (int)((rows + want_y - 1) / want_y);
+  rpb = (rpb + 3) / 4 * 4;
   if (rpb < 16) rpb = 16;
   if (rpb > 256) rpb = 256;
   if (rpb > rows) rpb = rows > 0 ? rows : 1;
@@ -295,23 +435,27 @@ int stencil_grid_blocks(int n, int rows, int rows_per_block) {
   return per_xcd * 8;
 }
 
+
+int stencil_default_variant() { return kDefaultVariant; }
+
 void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_out[1],
-                    hipStream_t stream) {
+                    hipStream_t stream, int variant) {
   StencilArgs a = a_in;
   const int rows = a.row_end - a.row_begin;
   a.tiles_x = (a.n + kStencilThreads - 1) / kStencilThreads;
   a.tiles_y = (rows + a.rows_per_block - 1) / a.rows_per_block;
   a.tiles_per_xcd = (a.tiles_x * a.tiles_y + 7) / 8;
-  const int blocks = a.tiles_per_xcd * 8;
+  int blocks = a.tiles_per_xcd * 8;
+  if (a.grid_blocks > 0 && a.grid_blocks < blocks) blocks = (a.grid_blocks + 7) / 8 * 8;
   nblocks_out[0] = a.tiles_x * a.tiles_y;  // partial slots written (one per tile)
   switch (epi) {
-    case EPI_AX: launch_stencil_t<EPI_AX>(const_c, a, blocks, stream); break;
-    case EPI_JAC: launch_stencil_t<EPI_JAC>(const_c, a, blocks, stream); break;
-    case EPI_RES: launch_stencil_t<EPI_RES>(const_c, a, blocks, stream); break;
-    case EPI_RES_JAC: launch_stencil_t<EPI_RES_JAC>(const_c, a, blocks, stream); break;
-    case EPI_RES_SL: launch_stencil_t<EPI_RES_SL>(const_c, a, blocks, stream); break;
-    case EPI_SL_FIRST: launch_stencil_t<EPI_SL_FIRST>(const_c, a, blocks, stream); break;
-    case EPI_SL_SWEEP: launch_stencil_t<EPI_SL_SWEEP>(const_c, a, blocks, stream); break;
+    case EPI_AX: launch_stencil_t<EPI_AX>(const_c, a, blocks, stream, variant); break;
+    case EPI_JAC: launch_stencil_t<EPI_JAC>(const_c, a, blocks, stream, variant); break;
+    case EPI_RES: launch_stencil_t<EPI_RES>(const_c, a, blocks, stream, variant); break;
+    case EPI_RES_JAC: launch_stencil_t<EPI_RES_JAC>(const_c, a, blocks, stream, variant); break;
+    case EPI_RES_SL: launch_stencil_t<EPI_RES_SL>(const_c, a, blocks, stream, variant); break;
+    case EPI_SL_FIRST: launch_stencil_t<EPI_SL_FIRST>(const_c, a, blocks, stream, variant); break;
+    case EPI_SL_SWEEP: launch_stencil_t<EPI_SL_SWEEP>(const_c, a, blocks, stream, variant); break;
     default: break;
   }
 }

@@ -180,6 +180,11 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
                                    ctypes.byref(t), ctypes.byref(k)))
         return t.value, k.value
 
+    def tune(self, variant: int = -1, rows_per_block: int = 0, grid_blocks: int = 0):
+        """Select a stencil kernel variant / band height / persistent grid size (speed only;
+        results are identical)."""
+        check(lib.hh_op_tune(self.handle, int(variant), int(rows_per_block), int(grid_blocks)))
+
     def stats(self):
         s = _ffi.HHStats()
         check(lib.hh_op_last_stats(self.handle, ctypes.byref(s)))

@@ -149,6 +149,19 @@ int hh_gmres(hh_op* op, const hh_vec* b, hh_vec* x, double rtol, double atol,
              double* hist, long hist_cap, hh_gmres_callback cb, void* user,
              long* iters_out, int* info_out, double* rnorm_out, double* bnorm_out);
 
+/* Performance tuning of the stencil kernel used by HH_APPLY_A: variant in [0, 24)
+ * selects the W/E exchange (LDS row / direct cached loads / wave shuffle), prefetch
+ * depth and load/store cache policy (-1 = built-in default); rows_per_block overrides
+ * the band height one workgroup marches (0 = automatic); grid_blocks > 0 runs a
+ * persistent grid of that many workgroups (0 = one per tile).  Results are identical
+ * for every setting; only speed changes. */
+int hh_op_tune(hh_op* op, int variant, int rows_per_block, int grid_blocks);
+/* Streaming roofline probes (diagnostic only): the stencil's byte mix without neighbour
+ * traffic in different access shapes (`kind`, see csrc/probe.hip), `blocks` workgroups,
+ * `iters` launches; outputs the average kernel ms and the probe's bytes per point. */
+int hh_op_probe_stream(hh_op* op, int kind, int blocks, const hh_vec* x, hh_vec* y, int iters,
+                       double* kernel_ms, int* bytes_per_point);
+
 /* Optional per-call counters of the last hh_gmres / hh_op_time_apply. */
 typedef struct {
   double solve_ms;        /* wall ms inside hh_gmres                      */

@@ -19,8 +19,10 @@ step() {  # step NAME SECONDS CMD...
   return 0
 }
 rocm-smi --showproductname > "$OUT/smi.log" 2>&1 || true
-step pytest_gpu 900 python -m pytest tests -m gpu -q -x "$@"
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py
-step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline --gmres-iters 40
+step pytest_gpu 480 python -m pytest tests -m gpu -q -x "$@"
+step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 300 python bench.py
+step rocprof 240 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline --gmres-iters 40
+step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 tools/prof_stencil.py --iters 20
+step pmc_write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 tools/prof_stencil.py --iters 20
 echo done

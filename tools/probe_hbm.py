@@ -1,0 +1,27 @@
+"""Streaming roofline probes for the stencil's byte mix (see csrc/probe.hip)."""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import helmholtz_preconditioner_amd as H  # noqa: E402
+from helmholtz_preconditioner_amd import _ffi  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+om, h, eta = H.problem_params(n, 12, 100.0, 2.0)
+A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.marmousi_like_c_mat(n))
+x, y = A.vector(), A.vector()
+x.fill_hash(1)
+names = ["1pt/lane u16 ic8 y16", "2pt/lane adjacent (ic16, u/y 32B stride)",
+         "2pt/lane wave-strided (ic8)", "copy y=u", "read-only u+ic", "1pt/lane nontemporal",
+         "copy 2pt/lane adjacent"]
+km, bpp = ctypes.c_double(), ctypes.c_int()
+for blocks in (2048, 8192, 32768):
+    for kind in range(7):
+        best = 1e9
+        for _ in range(3):
+            _ffi.check(_ffi.lib.hh_op_probe_stream(A.handle, kind, blocks, x.handle, y.handle, 20,
+                                                   ctypes.byref(km), ctypes.byref(bpp)))
+            best = min(best, km.value)
+        print(f"blocks {blocks:6d} kind {kind} {names[kind]:42s} {best*1e3:8.1f} us "
+              f"{bpp.value*n*n/(best*1e-3)/1e9:7.0f} GB/s", flush=True)
