@@ -38,11 +38,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200, help="timed operator applies")
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--n", type=int, default=0, help="global grid size (default 4096*sqrt(N))")
+    p.add_argument("--grid", type=int, default=0, help="global grid size n (default 4096*sqrt(N))")
     p.add_argument("--medium", default="marmousi", choices=["marmousi", "const", "c1"])
     p.add_argument("--wave-num", type=float, default=100.0)
-    p.add_argument("--b", type=int, default=12)
-    p.add_argument("--C", type=float, default=81.0)
+    p.add_argument("--pml-b", dest="b", type=int, default=12)
+    p.add_argument("--pml-C", dest="C", type=float, default=81.0)
     p.add_argument("--alpha", type=float, default=2.0)
     p.add_argument("--precond", default="sl", choices=["sl", "jacobi", "none"])
     p.add_argument("--sl-sweeps", type=int, default=2)
@@ -142,7 +142,7 @@ def main():
     ctx = dist.init_from_env(virtual_slabs=args.virtual_slabs)
     H.set_default_context(ctx)
 
-    n = args.n or int(round(4096 * math.sqrt(world) / 32) * 32)
+    n = args.grid or int(round(4096 * math.sqrt(world) / 32) * 32)
     omega, h, eta = H.problem_params(n, args.b, args.wave_num, args.alpha)
     j0, j1 = dist.slab_bounds(n, world, rank)
     t0 = time.perf_counter()

@@ -29,6 +29,7 @@ PP = ctypes.POINTER(ctypes.c_void_p)
 
 HH_PREC_NONE, HH_PREC_JACOBI, HH_PREC_SHIFTED_LAPLACE = 0, 1, 2
 HH_APPLY_A, HH_APPLY_JACOBI_A, HH_APPLY_PREC, HH_APPLY_PREC_A = 0, 1, 2, 3
+HH_TRANSPORT_RCCL, HH_TRANSPORT_SHM = 0, 1
 
 GMRES_CALLBACK = ctypes.CFUNCTYPE(None, c_void_p, c_long, c_double)
 
@@ -45,6 +46,7 @@ SIGNATURES = [
     ("hh_device_count", c_int, [c_ip]),
     ("hh_comm_unique_id", c_int, [c_ubp]),
     ("hh_ctx_create", c_int, [c_int, c_int, c_int, c_ubp, c_int, PP]),
+    ("hh_ctx_create_ex", c_int, [c_int, c_int, c_int, c_ubp, c_int, c_int, PP]),
     ("hh_ctx_destroy", c_int, [c_void_p]),
     ("hh_ctx_allreduce_max", c_int, [c_void_p, c_dp, c_int]),
     ("hh_ctx_allreduce_sum", c_int, [c_void_p, c_dp, c_int]),

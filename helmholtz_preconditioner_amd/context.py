@@ -20,15 +20,22 @@ class Context:
     that many slabs on the same device (tests the decomposition on one GPU)."""
 
     def __init__(self, device: int = 0, rank: int = 0, world: int = 1, nccl_id: bytes | None = None,
-                 virtual_slabs: int = 1):
+                 virtual_slabs: int = 1, transport: str = "rccl"):
+        """transport: "rccl" (production: one GPU per rank, RCCL over xGMI) or "shm"
+        (host-staged shared memory; ranks may share one GPU -- test rehearsal)."""
         self.device, self.rank, self.world, self.virtual_slabs = device, rank, world, virtual_slabs
+        self.transport = transport
+        kinds = {"rccl": _ffi.HH_TRANSPORT_RCCL, "shm": _ffi.HH_TRANSPORT_SHM}
+        if transport not in kinds:
+            raise ValueError(f"unknown transport {transport!r}")
         h = ctypes.c_void_p()
         idbuf = None
         if world > 1:
             if nccl_id is None or len(nccl_id) != 128:
-                raise ValueError("world > 1 needs the 128-byte RCCL unique id from rank 0")
+                raise ValueError("world > 1 needs the 128-byte communicator id from rank 0")
             idbuf = (ctypes.c_ubyte * 128).from_buffer_copy(nccl_id)
-        check(lib.hh_ctx_create(device, rank, world, idbuf, virtual_slabs, ctypes.byref(h)))
+        check(lib.hh_ctx_create_ex(device, rank, world, idbuf, virtual_slabs, kinds[transport],
+                                   ctypes.byref(h)))
         self._h = h
 
     @property

@@ -1,0 +1,205 @@
+// Inter-rank transports (see comm.hpp).
+#include "comm.hpp"
+
+#include <fcntl.h>
+#include <rccl/rccl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <new>
+#include <thread>
+
+#include "hh_error.hpp"
+
+namespace hh {
+
+// ------------------------------------------------------------------------- RCCL
+namespace {
+class RcclComm final : public Comm {
+ public:
+  RcclComm(int r, int w, const unsigned char id[128]) {
+    rank = r;
+    world = w;
+    ncclUniqueId uid;
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    std::memcpy(&uid, id, 128);
+    NCCLC(ncclCommInitRank(&comm_, w, uid, r));
+  }
+  ~RcclComm() override {
+    if (comm_) ncclCommDestroy(comm_);
+  }
+  void allreduce(double* d, int count, bool max, hipStream_t s) override {
+    NCCLC(ncclAllReduce(d, d, count, ncclFloat64, max ? ncclMax : ncclSum, comm_, s));
+  }
+  void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi, size_t bytes,
+            hipStream_t compute, hipStream_t hs, hipEvent_t ready) override {
+    // the halo stream starts once the input vector is complete on the compute stream
+    HIPC(hipEventRecord(ready, compute));
+    HIPC(hipStreamWaitEvent(hs, ready, 0));
+    const size_t cnt = bytes / sizeof(double);
+    NCCLC(ncclGroupStart());
+    if (recv_lo) NCCLC(ncclRecv(recv_lo, cnt, ncclFloat64, rank - 1, comm_, hs));
+    if (send_lo) NCCLC(ncclSend(send_lo, cnt, ncclFloat64, rank - 1, comm_, hs));
+    if (recv_hi) NCCLC(ncclRecv(recv_hi, cnt, ncclFloat64, rank + 1, comm_, hs));
+    if (send_hi) NCCLC(ncclSend(send_hi, cnt, ncclFloat64, rank + 1, comm_, hs));
+    NCCLC(ncclGroupEnd());
+  }
+
+ private:
+  ncclComm_t comm_ = nullptr;
+};
+
+// -------------------------------------------------------------------------- SHM
+constexpr size_t kShmSlotDoubles = 256;          // allreduce slot per rank
+constexpr size_t kShmHaloBytes = 65536 * 16;     // one row of up to n = 65536 complex
+constexpr uint64_t kShmMagic = 0x48484d5348574d31ull;
+constexpr double kShmTimeoutS = 300.0;
+
+struct ShmHeader {
+  std::atomic<uint64_t> magic;
+  std::atomic<int> arrive;
+  std::atomic<int> generation;
+  std::atomic<int> detached;
+  int world;
+};
+
+class ShmComm final : public Comm {
+ public:
+  ShmComm(int r, int w, const unsigned char id[128]) {
+    rank = r;
+    world = w;
+    char hex[33];
+    for (int k = 0; k < 16; ++k) snprintf(hex + 2 * k, 3, "%02x", id[k]);
+    name_ = std::string("/hh_shm_") + hex;
+    size_ = 4096 + (size_t)w * kShmSlotDoubles * sizeof(double) + (size_t)w * 2 * kShmHaloBytes;
+    int fd = -1;
+    if (r == 0) {
+      fd = shm_open(name_.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+      if (fd < 0) fail(HH_ERR_STATE, "shm_open(%s) create failed", name_.c_str());
+      if (ftruncate(fd, (off_t)size_) != 0) fail(HH_ERR_ALLOC, "ftruncate shm failed");
+    } else {
+      const auto t0 = std::chrono::steady_clock::now();
+      while ((fd = shm_open(name_.c_str(), O_RDWR, 0600)) < 0) {
+        if (elapsed(t0) > kShmTimeoutS) fail(HH_ERR_STATE, "rank %d: shm %s never appeared", r, name_.c_str());
+        std::this_thread::sleep_for(std::chrono::milliseconds(2));
+      }
+      struct stat st;
+      const auto t1 = std::chrono::steady_clock::now();
+      while (fstat(fd, &st) == 0 && (size_t)st.st_size < size_) {
+        if (elapsed(t1) > kShmTimeoutS) fail(HH_ERR_STATE, "shm segment never sized");
+        std::this_thread::sleep_for(std::chrono::milliseconds(2));
+      }
+    }
+    void* p = mmap(nullptr, size_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) fail(HH_ERR_ALLOC, "mmap shm failed");
+    base_ = static_cast<char*>(p);
+    hdr_ = reinterpret_cast<ShmHeader*>(base_);
+    if (r == 0) {
+      new (&hdr_->arrive) std::atomic<int>(0);
+      new (&hdr_->generation) std::atomic<int>(0);
+      new (&hdr_->detached) std::atomic<int>(0);
+      hdr_->world = w;
+      hdr_->magic.store(kShmMagic, std::memory_order_release);
+    } else {
+      const auto t0 = std::chrono::steady_clock::now();
+      while (hdr_->magic.load(std::memory_order_acquire) != kShmMagic) {
+        if (elapsed(t0) > kShmTimeoutS) fail(HH_ERR_STATE, "shm header never initialised");
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      }
+      if (hdr_->world != w) fail(HH_ERR_STATE, "shm world mismatch");
+    }
+    slots_ = reinterpret_cast<double*>(base_ + 4096);
+    halo_ = base_ + 4096 + (size_t)w * kShmSlotDoubles * sizeof(double);
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&pin_), kShmSlotDoubles * sizeof(double)));
+    barrier();
+    // every rank has mapped the segment: drop its name now so nothing can leak in /dev/shm
+    // (the mappings stay valid until each rank unmaps)
+    if (r == 0) shm_unlink(name_.c_str());
+  }
+  ~ShmComm() override {
+    // no barrier here: a peer may already have exited
+    if (pin_) (void)hipHostFree(pin_);
+    if (base_) munmap(base_, size_);
+  }
+  void allreduce(double* d, int count, bool max, hipStream_t s) override {
+    REQUIRE(count <= (int)kShmSlotDoubles, "shm allreduce too large");
+    HIPC(hipMemcpyAsync(pin_, d, count * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    std::memcpy(slots_ + (size_t)rank * kShmSlotDoubles, pin_, count * sizeof(double));
+    barrier();
+    for (int k = 0; k < count; ++k) {  // fixed rank order: identical result on every rank
+      double acc = slots_[k];
+      for (int q = 1; q < world; ++q) {
+        const double v = slots_[(size_t)q * kShmSlotDoubles + k];
+        acc = max ? std::max(acc, v) : acc + v;
+      }
+      pin_[k] = acc;
+    }
+    barrier();
+    HIPC(hipMemcpyAsync(d, pin_, count * sizeof(double), hipMemcpyHostToDevice, s));
+    HIPC(hipStreamSynchronize(s));
+  }
+  void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi, size_t bytes,
+            hipStream_t compute, hipStream_t, hipEvent_t) override {
+    REQUIRE(bytes <= kShmHaloBytes, "shm halo row too large (n > 65536)");
+    HIPC(hipStreamSynchronize(compute));
+    if (send_lo) HIPC(hipMemcpy(slot(rank, 0), send_lo, bytes, hipMemcpyDeviceToHost));
+    if (send_hi) HIPC(hipMemcpy(slot(rank, 1), send_hi, bytes, hipMemcpyDeviceToHost));
+    barrier();
+    if (recv_lo) HIPC(hipMemcpy(recv_lo, slot(rank - 1, 1), bytes, hipMemcpyHostToDevice));
+    if (recv_hi) HIPC(hipMemcpy(recv_hi, slot(rank + 1, 0), bytes, hipMemcpyHostToDevice));
+    barrier();
+  }
+
+ private:
+  static double elapsed(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  char* slot(int r, int side) { return halo_ + ((size_t)r * 2 + side) * kShmHaloBytes; }
+  void barrier() {
+    const int gen = hdr_->generation.load(std::memory_order_acquire);
+    if (hdr_->arrive.fetch_add(1, std::memory_order_acq_rel) == world - 1) {
+      hdr_->arrive.store(0, std::memory_order_relaxed);
+      hdr_->generation.fetch_add(1, std::memory_order_acq_rel);
+      return;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    unsigned spins = 0;
+    while (hdr_->generation.load(std::memory_order_acquire) == gen) {
+      if (++spins > 1000) {
+        sched_yield();
+        if ((spins & 0xfff) == 0 && elapsed(t0) > kShmTimeoutS)
+          fail(HH_ERR_STATE, "rank %d: shm barrier timed out", rank);
+      }
+    }
+  }
+  std::string name_;
+  size_t size_ = 0;
+  char* base_ = nullptr;
+  ShmHeader* hdr_ = nullptr;
+  double* slots_ = nullptr;
+  char* halo_ = nullptr;
+  double* pin_ = nullptr;
+};
+}  // namespace
+
+std::unique_ptr<Comm> make_rccl_comm(int rank, int world, const unsigned char id[128]) {
+  return std::make_unique<RcclComm>(rank, world, id);
+}
+std::unique_ptr<Comm> make_shm_comm(int rank, int world, const unsigned char id[128]) {
+  return std::make_unique<ShmComm>(rank, world, id);
+}
+void rccl_unique_id(unsigned char out[128]) {
+  ncclUniqueId id;
+  NCCLC(ncclGetUniqueId(&id));
+  std::memcpy(out, &id, 128);
+}
+
+}  // namespace hh

@@ -1,0 +1,38 @@
+// Inter-rank transport for the row-slab decomposition: the one-row halo exchange with the
+// neighbouring ranks and the small global reductions of GMRES.
+//   RcclComm : production -- ncclSend/ncclRecv pairs in one group on the halo stream and
+//              ncclAllReduce on the compute stream (RCCL over xGMI; one process per GPU).
+//   ShmComm  : test transport -- host-staged through a POSIX shared-memory segment with a
+//              process-shared barrier; lets N ranks share ONE GPU (RCCL refuses duplicate
+//              devices), so the N > 1 orchestration is exercised on a single-GPU box.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <memory>
+
+namespace hh {
+
+enum Transport : int { TRANSPORT_RCCL = 0, TRANSPORT_SHM = 1 };
+
+class Comm {
+ public:
+  virtual ~Comm() = default;
+  // In-place sum (or max) of `count` doubles in device memory, ordered on `s`.  The result
+  // is identical on every rank.
+  virtual void allreduce(double* d, int count, bool max, hipStream_t s) = 0;
+  // One-row halo exchange, ordered after the work already queued on `compute`:
+  // send_lo -> rank-1, send_hi -> rank+1; recv_lo <- rank-1, recv_hi <- rank+1 (nullptr
+  // where there is no neighbour).  Work for it is queued on `halo` (RCCL) or done
+  // synchronously (SHM); the caller records its completion event on `halo`.
+  virtual void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi,
+                    size_t bytes, hipStream_t compute, hipStream_t halo, hipEvent_t ready) = 0;
+  int rank = 0, world = 1;
+};
+
+std::unique_ptr<Comm> make_rccl_comm(int rank, int world, const unsigned char id[128]);
+std::unique_ptr<Comm> make_shm_comm(int rank, int world, const unsigned char id[128]);
+void rccl_unique_id(unsigned char out[128]);
+
+}  // namespace hh

@@ -70,13 +70,20 @@ def cleanup_rendezvous(key: str | None = None):
 
 def init_from_env(virtual_slabs: int = 1) -> Context:
     """Context for this process: its LOCAL_RANK's GPU, joined to the node-wide RCCL
-    communicator when WORLD_SIZE > 1."""
+    communicator when WORLD_SIZE > 1.
+
+    Test rehearsal knobs (single-GPU machine): HH_TRANSPORT=shm selects the host-staged
+    shared-memory transport and HH_FORCE_DEVICE=0 puts every rank on device 0.
+    """
     rank, world, local = env_rank_world()
+    device = int(os.environ.get("HH_FORCE_DEVICE", local if "LOCAL_RANK" in os.environ else 0))
+    transport = os.environ.get("HH_TRANSPORT", "rccl")
     if world == 1:
-        return Context(device=local if "LOCAL_RANK" in os.environ else 0,
-                       virtual_slabs=virtual_slabs)
-    uid = exchange_unique_id(rank, world)
-    ctx = Context(device=local, rank=rank, world=world, nccl_id=uid, virtual_slabs=virtual_slabs)
+        return Context(device=device, virtual_slabs=virtual_slabs)
+    make_id = unique_id if transport == "rccl" else (lambda: os.urandom(128))
+    uid = exchange_unique_id(rank, world, make_id=make_id)
+    ctx = Context(device=device, rank=rank, world=world, nccl_id=uid, virtual_slabs=virtual_slabs,
+                  transport=transport)
     ctx.barrier()
     if rank == 0:
         cleanup_rendezvous()

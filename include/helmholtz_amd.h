@@ -74,6 +74,14 @@ int hh_comm_unique_id(unsigned char id_out[128]);
  * production uses 1). */
 int hh_ctx_create(int device, int rank, int world, const unsigned char* nccl_id,
                   int virtual_slabs, hh_ctx** ctx);
+/* Same, choosing the inter-rank transport: HH_TRANSPORT_RCCL (production, one GPU per
+ * rank) or HH_TRANSPORT_SHM (host-staged POSIX shared memory; several ranks may share one
+ * GPU -- the test rehearsal of the N > 1 path on a single-GPU machine).  For SHM the 128
+ * id bytes are any random token shared by all ranks. */
+#define HH_TRANSPORT_RCCL 0
+#define HH_TRANSPORT_SHM 1
+int hh_ctx_create_ex(int device, int rank, int world, const unsigned char* id,
+                     int virtual_slabs, int transport, hh_ctx** ctx);
 int hh_ctx_destroy(hh_ctx* ctx);
 /* Host-side collectives for harness timing (RCCL allreduce; no-op at world 1). */
 int hh_ctx_allreduce_max(hh_ctx* ctx, double* values, int count);
@@ -123,10 +131,11 @@ int hh_vec_fill_hash(hh_vec* v, uint64_t seed);
 /* Device-resident apply: y = mode(A) x, including the halo exchange. */
 int hh_op_apply_dev(hh_op* op, const hh_vec* x, hh_vec* y, int mode);
 
-/* Timing harness: `iters` back-to-back device applies (x -> y), bracketed by
- * HIP events on the stream the stencil runs on.  Outputs total wall ms of the
- * timed region and the average stencil-kernel ms per apply (events around the
- * kernel launches only). */
+/* Timing harness: `iters` back-to-back device applies (x -> y) on the stream the
+ * stencil runs on.  total_ms: HIP events bracketing the whole timed region.
+ * kernel_ms: average stencil-kernel duration -- total / iters when one apply is one
+ * launch (single rank, single slab, HH_APPLY_A); otherwise the average of events
+ * recorded around the interior stencil launch of every apply. */
 int hh_op_time_apply(hh_op* op, const hh_vec* x, hh_vec* y, int mode, int iters,
                      double* total_ms, double* kernel_ms);
 

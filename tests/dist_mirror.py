@@ -1,0 +1,151 @@
+"""Distributed GMRES mirror over torch.distributed (gloo, CPU) -- test helper.
+
+Restates, in numpy, what the C runtime does at world > 1 (runtime.cpp run_stencil /
+hh_gmres with the RCCL transport): each rank owns the layer slab
+[floor(r n / P), floor((r+1) n / P)) (dist.slab_bounds), applies the stencil after a
+one-row halo exchange with its neighbours, and forms every inner product as local partial
+sums + an allreduce; the Hessenberg / Givens scalars are then identical on every rank and
+drive scipy's control flow (restart cycles, legacy counting, ptol, true-residual test).
+Classical Gram-Schmidt with lazily applied basis scales, like csrc/krylov.hip.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+from scipy.linalg import get_lapack_funcs
+
+from oracle import helmholtz_oracle as O
+
+
+class SlabOperator:
+    def __init__(self, const, eta, omega, h, n, c_mat, j0, j1, jacobi=False):
+        W, E, S, N, D = O.stencil_coefficients(const, eta, omega, h, n, c_mat)
+        self.W, self.E, self.S, self.N, self.D = (a[j0:j1] for a in (W, E, S, N, D))
+        self.n, self.j0, self.j1 = n, j0, j1
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.jacobi = jacobi
+
+    def _halo(self, X):
+        n = self.n
+        lo, hi = np.zeros(n, complex), np.zeros(n, complex)
+        reqs = []
+        buf_lo = torch.zeros(2 * n, dtype=torch.float64)
+        buf_hi = torch.zeros(2 * n, dtype=torch.float64)
+        if self.rank > 0:
+            reqs.append(dist.isend(torch.from_numpy(X[0].view(np.float64).copy()), self.rank - 1))
+            reqs.append(dist.irecv(buf_lo, self.rank - 1))
+        if self.rank < self.world - 1:
+            reqs.append(dist.isend(torch.from_numpy(X[-1].view(np.float64).copy()), self.rank + 1))
+            reqs.append(dist.irecv(buf_hi, self.rank + 1))
+        for r in reqs:
+            r.wait()
+        if self.rank > 0:
+            lo = buf_lo.numpy().view(np.complex128).copy()
+        if self.rank < self.world - 1:
+            hi = buf_hi.numpy().view(np.complex128).copy()
+        return lo, hi
+
+    def apply(self, x):
+        X = x.reshape(-1, self.n)
+        lo, hi = self._halo(X)
+        ext = np.vstack([lo[None], X, hi[None]])
+        y = self.S * ext[:-2]
+        y[:, 1:] += self.W[:, 1:] * X[:, :-1]
+        y += self.D * X
+        y[:, :-1] += self.E[:, :-1] * X[:, 1:]
+        y += self.N * ext[2:]
+        return y.ravel()
+
+    def psolve(self, r):
+        return r / self.D.ravel() if self.jacobi else r.copy()
+
+
+def allreduce(vals):
+    t = torch.from_numpy(np.ascontiguousarray(vals, dtype=np.float64).copy())
+    dist.all_reduce(t)
+    return t.numpy()
+
+
+def gdot(a, b):  # global vdot(a, b)
+    v = np.vdot(a, b)
+    s = allreduce([v.real, v.imag])
+    return s[0] + 1j * s[1]
+
+
+def gnorm(a):
+    return float(np.sqrt(allreduce([np.vdot(a, a).real])[0]))
+
+
+def gmres_dist(op, b, rtol, restart, maxiter):
+    """legacy-callback GMRES (maxiter = inner iterations); returns (x, info, history)."""
+    lartg = get_lapack_funcs('lartg', dtype=np.complex128)
+    eps = np.finfo(float).eps
+    x = np.zeros_like(b)
+    bn = gnorm(b)
+    atol = rtol * bn
+    Mb = gnorm(op.psolve(b))
+    ptol_f = 1.0
+    ptol = Mb * min(ptol_f, atol / bn)
+    V = np.empty((restart + 1, b.size), complex)
+    scale = np.zeros(restart + 1)
+    H = np.zeros((restart, restart + 1), complex)
+    G = np.zeros((restart, 2), complex)
+    hist, inner = [], 0
+    r = b.copy()
+    presid = 0.0
+    for _ in range(maxiter):
+        V[0] = op.psolve(r)
+        t = gnorm(V[0])
+        scale[0] = 1 / t
+        S = np.zeros(restart + 1, complex)
+        S[0] = t
+        brk = False
+        for col in range(restart):
+            w = scale[col] * op.psolve(op.apply(V[col]))
+            raw = allreduce(np.concatenate([[c.real, c.imag] for c in (V[:col + 1].conj() @ w)]
+                                           + [[np.vdot(w, w).real]]))
+            dots = raw[0:2 * (col + 1):2] + 1j * raw[1:2 * (col + 1):2]
+            h0 = np.sqrt(raw[-1])
+            hk = scale[:col + 1] * dots
+            w = w - (hk * scale[:col + 1]) @ V[:col + 1]
+            h1 = gnorm(w)
+            H[col, :col + 1] = hk
+            H[col, col + 1] = h1
+            V[col + 1] = w
+            if h1 <= eps * h0:
+                H[col, col + 1] = 0
+                brk = True
+            else:
+                scale[col + 1] = 1 / h1
+            for k in range(col):
+                c, s = G[k]
+                n0, n1 = H[col, [k, k + 1]]
+                H[col, [k, k + 1]] = [c * n0 + s * n1, -s.conj() * n0 + c * n1]
+            c, s, mag = lartg(H[col, col], H[col, col + 1])
+            G[col] = [c, s]
+            H[col, [col, col + 1]] = mag, 0
+            tmp = -np.conj(s) * S[col]
+            S[[col, col + 1]] = [c * S[col], tmp]
+            presid = abs(tmp)
+            inner += 1
+            hist.append(presid / bn)
+            if inner == maxiter or presid <= ptol or brk:
+                break
+        if H[col, col] == 0:
+            S[col] = 0
+        y = S[:col + 1].copy()
+        for k in range(col, 0, -1):
+            if y[k] != 0:
+                y[k] /= H[k, k]
+                y[:k] -= y[k] * H[k, :k]
+        if y[0] != 0:
+            y[0] /= H[0, 0]
+        x += (y * scale[:col + 1]) @ V[:col + 1]
+        r = b - op.apply(x)
+        rn = gnorm(r)
+        if inner == maxiter:
+            return x, (0 if rn <= atol else maxiter), np.array(hist)
+        if rn <= atol or brk:
+            break
+        ptol_f = max(eps, 0.25 * ptol_f) if presid <= ptol else min(1.0, 1.5 * ptol_f)
+        ptol = presid * min(ptol_f, atol / rn)
+    return x, (0 if rn <= atol else maxiter), np.array(hist)

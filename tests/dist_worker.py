@@ -1,0 +1,52 @@
+"""One rank of a multi-process row-slab run (used by tests/test_gpu_dist.py).
+
+Every rank runs on device 0 with the shared-memory transport, so the N > 1
+orchestration (slab ownership, halo exchange, global reductions inside GMRES, the
+preconditioners) is exercised on a single GPU.  Results go to an .npz for the parent.
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import helmholtz_preconditioner_amd as H  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rank", type=int)
+    p.add_argument("--world", type=int)
+    p.add_argument("--id")
+    p.add_argument("--out")
+    p.add_argument("--n", type=int, default=150)
+    p.add_argument("--slabs", type=int, default=1)
+    a = p.parse_args()
+    ctx = H.Context(device=0, rank=a.rank, world=a.world, nccl_id=bytes.fromhex(a.id),
+                    virtual_slabs=a.slabs, transport="shm")
+    n = a.n
+    om, h, eta = H.problem_params(n, 12, 6.0, 2.0)
+    cm = H.init_c1_mat(.5, .5, n)
+    A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, context=ctx)
+    j0, j1 = A.row_begin, A.row_end
+    rng = np.random.default_rng(5)
+    xg = (rng.standard_normal(n * n) + 1j * rng.standard_normal(n * n)).reshape(n, n)
+    y = A @ xg[j0:j1].ravel()
+    f = H.init_f1_mat(.5, .125, om, n)[j0:j1].ravel()
+    out = dict(j0=j0, j1=j1, y=y)
+    for name, M in (("none", None), ("jacobi", "jacobi"),
+                    ("sl", H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7))):
+        x, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=50, M=M,
+                                callback=lambda r: None, callback_type="legacy",
+                                return_history=True)
+        out[f"x_{name}"], out[f"info_{name}"], out[f"hist_{name}"] = x, info, hist
+    # a host collective the bench uses for its timing
+    out["maxrank"] = ctx.allreduce_max([float(a.rank)])[0]
+    np.savez(a.out, **out)
+    ctx.barrier()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,97 @@
+"""CPU tier, N > 1: the row-slab decomposition over torch.distributed gloo (world 2, 3).
+
+* slab ownership (dist.slab_bounds == the C runtime's formula) tiles [0, n);
+* the file rendezvous hands rank 0's 128-byte id to every rank;
+* a numpy restatement of the distributed algorithm (tests/dist_mirror.py: halo exchange +
+  allreduced inner products + scipy's control flow) reproduces the single-process
+  reference solve (scipy gmres on the oracle CSR, golden-pinned) to 1e-10.
+"""
+import multiprocessing as mp
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, load_golden, medium
+from helmholtz_preconditioner_amd import dist as hdist
+
+
+def test_slab_bounds_tile_the_grid():
+    for n in (1, 7, 100, 4096, 11584):
+        for world in range(1, 9):
+            if world > n:
+                continue
+            b = [hdist.slab_bounds(n, world, r) for r in range(world)]
+            assert b[0][0] == 0 and b[-1][1] == n
+            assert all(x[1] == y[0] for x, y in zip(b, b[1:]))
+            sizes = [e - s for s, e in b]
+            assert max(sizes) - min(sizes) <= 1 and min(sizes) >= 1
+
+
+def _rdzv_worker(rank, world, key, q):
+    uid = hdist.exchange_unique_id(rank, world, key=key, make_id=lambda: bytes(range(128)),
+                                   timeout=60)
+    q.put((rank, uid))
+
+
+def test_file_rendezvous_two_processes():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    key = f"test_{os.getpid()}_{np.random.default_rng().integers(1 << 30)}"
+    ps = [ctx.Process(target=_rdzv_worker, args=(r, 3, key, q)) for r in (1, 2, 0)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    hdist.cleanup_rendezvous(key)
+    assert all(v == bytes(range(128)) for v in got.values()) and len(got) == 3
+
+
+def _gloo_worker(rank, world, port, case, out):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    from oracle import helmholtz_oracle as O
+    import dist_mirror as DM
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    z = np.load(os.path.join(ROOT, "tests", "golden", case), allow_pickle=False)
+    n = int(z["n"])
+    j0, j1 = hdist.slab_bounds(n, world, rank)
+    om = complex(z["omega"])
+    op = DM.SlabOperator(float(z["C"]), float(z["eta"]), om, float(z["h"]), n,
+                         medium(str(z["medium"]), n), j0, j1,
+                         jacobi=str(z["precond"]) == "jacobi")
+    f = O.init_f1_mat(.5, .125, om, n)[j0:j1].ravel()
+    x, info, hist = DM.gmres_dist(op, f, 1e-3, 20, int(z["K"]))
+    np.savez(out, x=x, info=info, hist=hist, j0=j0, j1=j1)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,world", [("gmres_n64_c1_none.npz", 2), ("gmres_n128_jacobi.npz", 3)])
+def test_distributed_gmres_mirror_matches_reference(case, world):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    with tempfile.TemporaryDirectory() as td:
+        outs = [os.path.join(td, f"r{r}.npz") for r in range(world)]
+        ps = [ctx.Process(target=_gloo_worker, args=(r, world, port, case, outs[r]))
+              for r in range(world)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(timeout=300)
+            assert p.exitcode == 0
+        parts = [np.load(o) for o in outs]
+        z = load_golden(case)
+        x = np.concatenate([p["x"] for p in parts])
+        for p in parts:
+            assert int(p["info"]) == int(z["info"])
+            assert np.max(np.abs(p["hist"] - z["history"]) / z["history"]) < 1e-9
+        assert np.linalg.norm(x - z["x"]) / np.linalg.norm(z["x"]) < 1e-9

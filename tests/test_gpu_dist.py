@@ -1,0 +1,99 @@
+"""GPU tier, N > 1: row-slab decomposition across processes.
+
+RCCL refuses two ranks on one GPU, so these tests run W processes on device 0 with the
+host-staged shared-memory transport (csrc/comm.cpp ShmComm) -- the same orchestration as
+the RCCL production path (slab ownership, one-row halo exchange, rank-ordered global
+reductions), checked against the single-domain result on the same GPU:
+  * the operator apply: bit-identical slabs;
+  * GMRES (none / Jacobi / shifted-Laplace): residual history and field to 1e-8 (the
+    reductions sum partials in a different order; the contract is 1e-6).
+It also rehearses `bench.py --gpus 2` end to end under torch.distributed.run.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import helmholtz_preconditioner_amd as H
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+WORKER = os.path.join(ROOT, "tests", "dist_worker.py")
+
+
+def _single_domain(n):
+    ctx = H.Context(device=0)
+    om, h, eta = H.problem_params(n, 12, 6.0, 2.0)
+    A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.init_c1_mat(.5, .5, n), context=ctx)
+    rng = np.random.default_rng(5)
+    xg = rng.standard_normal(n * n) + 1j * rng.standard_normal(n * n)
+    res = dict(y=A @ xg)
+    f = H.init_f1_mat(.5, .125, om, n).ravel()
+    for name, M in (("none", None), ("jacobi", "jacobi"),
+                    ("sl", H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7))):
+        x, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=50, M=M,
+                                callback=lambda r: None, callback_type="legacy",
+                                return_history=True)
+        res[f"x_{name}"], res[f"info_{name}"], res[f"hist_{name}"] = x, info, hist
+    return res
+
+
+@pytest.mark.parametrize("world,slabs", [(2, 1), (3, 1), (2, 2)])
+def test_multiprocess_slabs_match_single_domain(tmp_path, world, slabs):
+    n = 150
+    ref = _single_domain(n)
+    tok = os.urandom(128).hex()
+    procs = []
+    for r in range(world):
+        out = tmp_path / f"r{r}.npz"
+        procs.append((subprocess.Popen([sys.executable, WORKER, "--rank", str(r), "--world",
+                                        str(world), "--id", tok, "--out", str(out), "--n", str(n),
+                                        "--slabs", str(slabs)],
+                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT), out))
+    for p, _ in procs:
+        try:
+            p.wait(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q, _ in procs:
+                q.kill()
+            raise
+    for p, _ in procs:
+        assert p.returncode == 0, p.stdout.read().decode()[-3000:]
+    parts = [np.load(o) for _, o in procs]
+    assert parts[0]["j0"] == 0 and parts[-1]["j1"] == n
+    for a, b in zip(parts, parts[1:]):
+        assert a["j1"] == b["j0"]
+    y = np.concatenate([p["y"] for p in parts])
+    np.testing.assert_array_equal(y, ref["y"])
+    for name in ("none", "jacobi", "sl"):
+        x = np.concatenate([p[f"x_{name}"] for p in parts])
+        for p in parts:
+            assert int(p[f"info_{name}"]) == int(ref[f"info_{name}"])
+            h = p[f"hist_{name}"]
+            assert len(h) == len(ref[f"hist_{name}"])
+            assert np.max(np.abs(h - ref[f"hist_{name}"]) / ref[f"hist_{name}"]) < 1e-8
+        assert np.linalg.norm(x - ref[f"x_{name}"]) / np.linalg.norm(ref[f"x_{name}"]) < 1e-8
+    assert all(float(p["maxrank"]) == world - 1 for p in parts)
+
+
+def test_bench_two_ranks_rehearsal(tmp_path):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, HH_TRANSPORT="shm", HH_FORCE_DEVICE="0", TMPDIR=str(tmp_path))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--grid", "768", "--steps", "10",
+           "--warmup", "2", "--gmres-iters", "6", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=400, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["n"] == 768 and res["value"] > 0
+    assert res["gmres"]["iterations"] == 6
