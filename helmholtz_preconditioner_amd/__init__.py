@@ -20,6 +20,7 @@ from .media import (constant_c_mat, init_c1_f1, init_c1_f2, init_c1_mat, init_c2
 from .operator import (DeviceOperator, DevicePreconditioner, DeviceVector, Jacobi,  # noqa: F401
                        ShiftedLaplace, build_A_matrix)
 from .solver import gmres  # noqa: F401
+from . import dist  # noqa: F401
 
 __all__ = [
     "build_A_matrix", "gmres", "DeviceOperator", "DeviceVector", "Jacobi", "ShiftedLaplace",
