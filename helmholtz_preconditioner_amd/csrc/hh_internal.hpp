@@ -14,6 +14,7 @@ constexpr int kStencilThreads = 256;   // one 256-wide strip of the fast axis i 
 constexpr int kReduceThreads = 256;
 constexpr int kMaxProj = 32;           // max basis vectors per multidot/update launch
 constexpr int kMaxNorms = 2;           // norm accumulators a stencil epilogue may produce
+constexpr int kMaxStreamBlocks = 8192; // upper bound of the Krylov streaming grid
 
 // Stencil epilogues (what the kernel writes after computing (A u) at a point).
 enum Epi : int {
@@ -60,6 +61,7 @@ struct StencilArgs {
   double2* out0;
   double2* out1;
   double* partials;        // [blocks][kMaxNorms] when the epilogue accumulates norms
+  const int* stop;         // GMRES cycle stop flag: the launch is a no-op once *stop != 0
 };
 
 struct PointArgs {
@@ -73,6 +75,7 @@ struct PointArgs {
   double2 mshift;
   double damping;
   double* partials;        // [blocks][kMaxNorms]
+  const int* stop;         // as StencilArgs::stop
 };
 
 // Kernel launchers (kernels.hip).  All are asynchronous on `stream`.
@@ -89,26 +92,30 @@ int point_blocks(size_t len);
 
 // Krylov kernels.
 //   multidot: partials[blk][2K+2] = sum conj(V_k) w (K vectors, stride ldv), |w|^2 at [2K]
+// `stop` (optional): device flag of a queued GMRES cycle; kernels return at once when set.
 void launch_multidot(const double2* V, size_t ldv, int K, const double2* w, size_t len,
-                     double* partials, int blocks, hipStream_t stream);
+                     double* partials, int blocks, hipStream_t stream, const int* stop = nullptr);
 //   update: w_out = w - sum_k coef_k V_k, coef_k = scale_k^2 * raw_k (raw from reduced dots);
 //   acc |w_out|^2 into partials[blk][0]
 void launch_update(const double2* V, size_t ldv, int K, const double* raw, const double* scale,
                    const double2* w, double2* w_out, size_t len, double* partials, int blocks,
-                   hipStream_t stream);
+                   hipStream_t stream, const int* stop = nullptr);
 //   xupdate: x += sum_k y_k V_k  (y complex, device, already including scales)
 void launch_xupdate(const double2* V, size_t ldv, int K, const double2* y, double2* x,
                     size_t len, int blocks, hipStream_t stream);
 int stream_blocks(size_t len);
+void tune_krylov(int nt, int blocks);  // global knobs (tuning studies only)
 // Deterministic reduction of `count` partial rows of width `width` (fixed order):
 // out[k] = sum_b partials[b*width + k] for k < cols.  One block per column.
 void launch_reduce(const double* partials, int count, int width, int cols, double* out,
-                   hipStream_t stream);
+                   hipStream_t stream, const int* stop = nullptr);
 // out[k] += in[k], k < count (tiny, one block).
-void launch_add_small(const double* in, double* out, int count, hipStream_t stream);
+void launch_add_small(const double* in, double* out, int count, hipStream_t stream,
+                      const int* stop = nullptr);
 // Hash fill of a slab vector (global element offset `goff`).
 void launch_fill_hash(double2* v, size_t len, size_t goff, uint64_t seed, hipStream_t stream);
-void launch_scale_copy(const double2* in, double2* out, size_t len, double s, hipStream_t stream);
+void launch_scale_copy(const double2* in, double2* out, size_t len, double s, hipStream_t stream,
+                       const int* stop = nullptr);
 
 // GMRES device state machine step (single wave, krylov.hip).
 struct GivensState {
@@ -119,12 +126,18 @@ struct GivensState {
   double* vscale;  // [restart+1] real scales of the stored basis vectors
   double2* ycoef;  // [restart] x-update coefficients y_k * vscale_k
   double* status;  // [8]: 0 presid, 1 breakdown, 2 h0, 3 h1, 4 rnorm, 5 mnorm
+  double* status_it;  // [restart][4]: presid, breakdown, h0, h1 of every inner iteration
+  int* ctrl;          // [0] stop flag of the queued cycle, [1] last column executed
   int restart;
 };
 // After multidot+update reductions: column `col` of H from raw dots (red_dots, 2*(col+1)
-// doubles + |w|^2 at [2*(col+1)]) and |w_new|^2 (red_norm[0]).
+// doubles + |w|^2 at [2*(col+1)]) and |w_new|^2 (red_norm[0]).  Then scipy's inner-loop
+// exit test (iterative.py:792-795) on the device: presid <= ptol, breakdown, or
+// col == stop_col (the legacy maxiter cap) raises ctrl[0], which turns every kernel queued
+// after it in this cycle into a no-op.
 void launch_gmres_column(const GivensState& g, int col, const double* red_dots,
-                         const double* red_norm, double eps, hipStream_t stream);
+                         const double* red_norm, double eps, double ptol, int stop_col,
+                         hipStream_t stream);
 // Start of a cycle: S[0] = ||Mr||, vscale[0] = 1/||Mr|| from red[idx_m]; status[4] = ||r||.
 void launch_gmres_start(const GivensState& g, const double* red, int idx_r, int idx_m,
                         hipStream_t stream);

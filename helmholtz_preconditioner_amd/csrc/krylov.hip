@@ -18,6 +18,15 @@ namespace {
 
 constexpr int kT = 256;  // threads per streaming block
 
+template <bool NT>
+__device__ __forceinline__ double2 ldnt(const double2* p) {
+  if constexpr (NT) {
+    return make_double2(__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y));
+  } else {
+    return *p;
+  }
+}
+
 // Block-reduce NV doubles held per thread; lane results land in partials[blk*width + k].
 template <int NV>
 __device__ __forceinline__ void block_reduce_vec(double (&v)[NV], double* partials, int width) {
@@ -41,10 +50,12 @@ __device__ __forceinline__ void block_reduce_vec(double (&v)[NV], double* partia
 }
 
 // partials[blk][2K+2]: [2k, 2k+1] = sum_p conj(V_k[p]) w[p];  [2K] = sum |w|^2.
-template <int K>
+template <int K, bool NT>
 __global__ __launch_bounds__(kT) void multidot_kernel(const double2* __restrict__ V, size_t ldv,
                                                       const double2* __restrict__ w, size_t len,
-                                                      double* __restrict__ partials) {
+                                                      double* __restrict__ partials,
+                                                      const int* stop) {
+  if (stop && *stop) return;
   double2 acc[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) acc[k] = make_double2(0.0, 0.0);
@@ -54,7 +65,7 @@ __global__ __launch_bounds__(kT) void multidot_kernel(const double2* __restrict_
     const double2 wv = w[p];
     nrm = fma(wv.x, wv.x, fma(wv.y, wv.y, nrm));
 #pragma unroll
-    for (int k = 0; k < K; ++k) acc[k] = cfma_conj(V[(size_t)k * ldv + p], wv, acc[k]);
+    for (int k = 0; k < K; ++k) acc[k] = cfma_conj(ldnt<NT>(V + (size_t)k * ldv + p), wv, acc[k]);
   }
   double v[2 * K + 1];
 #pragma unroll
@@ -67,12 +78,14 @@ __global__ __launch_bounds__(kT) void multidot_kernel(const double2* __restrict_
 }
 
 // w_out = w - sum_k (s_k * (s_k * raw_k)) V_k; partials[blk][kMaxNorms]: [0] = |w_out|^2.
-template <int K>
+template <int K, bool NT>
 __global__ __launch_bounds__(kT) void update_kernel(const double2* __restrict__ V, size_t ldv,
                                                     const double* __restrict__ raw,
                                                     const double* __restrict__ scale,
                                                     const double2* w, double2* w_out, size_t len,
-                                                    double* __restrict__ partials) {
+                                                    double* __restrict__ partials,
+                                                    const int* stop) {
+  if (stop && *stop) return;
   double2 coef[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -86,7 +99,7 @@ __global__ __launch_bounds__(kT) void update_kernel(const double2* __restrict__ 
     double2 wv = w[p];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const double2 vk = V[(size_t)k * ldv + p];
+      const double2 vk = ldnt<NT>(V + (size_t)k * ldv + p);
       wv = csub(wv, cmul(coef[k], vk));
     }
     w_out[p] = wv;
@@ -115,7 +128,9 @@ __global__ __launch_bounds__(kT) void xupdate_kernel(const double2* __restrict__
 
 // One block per output column: out[k] = sum_b partials[b*width + k] in fixed order.
 __global__ __launch_bounds__(kT) void reduce_kernel(const double* __restrict__ partials, int count,
-                                                    int width, double* __restrict__ out) {
+                                                    int width, double* __restrict__ out,
+                                                    const int* stop) {
+  if (stop && *stop) return;
   __shared__ double sh[kT];
   const int k = blockIdx.x;
   double s = 0.0;
@@ -129,7 +144,8 @@ __global__ __launch_bounds__(kT) void reduce_kernel(const double* __restrict__ p
   if (threadIdx.x == 0) out[k] = sh[0];
 }
 
-__global__ void add_small_kernel(const double* in, double* out, int count) {
+__global__ void add_small_kernel(const double* in, double* out, int count, const int* stop) {
+  if (stop && *stop) return;
   for (int k = threadIdx.x; k < count; k += blockDim.x) out[k] += in[k];
 }
 
@@ -155,7 +171,8 @@ __global__ __launch_bounds__(kT) void fill_hash_kernel(double2* v, size_t len, s
 }
 
 __global__ __launch_bounds__(kT) void scale_copy_kernel(const double2* in, double2* out,
-                                                        size_t len, double s) {
+                                                        size_t len, double s, const int* stop) {
+  if (stop && *stop) return;
   const size_t stride = (size_t)gridDim.x * kT;
   for (size_t p = (size_t)blockIdx.x * kT + threadIdx.x; p < len; p += stride)
     out[p] = cscale(in[p], s);
@@ -188,8 +205,8 @@ __device__ void zlartg(double2 f, double2 g, double* c, double2* s, double2* r) 
 }
 
 __global__ void gmres_column_kernel(GivensState g, int col, const double* rd, const double* rn,
-                                    double eps) {
-  if (threadIdx.x != 0) return;
+                                    double eps, double ptol, int stop_col) {
+  if (threadIdx.x != 0 || g.ctrl[0]) return;
   const int R1 = g.restart + 1;
   double2* h = g.H + (size_t)col * R1;
   for (int k = 0; k <= col; ++k) h[k] = cscale(make_double2(rd[2 * k], rd[2 * k + 1]), g.vscale[k]);
@@ -221,14 +238,24 @@ __global__ void gmres_column_kernel(GivensState g, int col, const double* rd, co
   const double2 tmp = cmul(make_double2(-s.x, s.y), Sc);  // -conj(s) * S[col]
   g.S[col] = cscale(Sc, c);
   g.S[col + 1] = tmp;
-  g.status[0] = hypot(tmp.x, tmp.y);
+  const double presid = hypot(tmp.x, tmp.y);
+  g.status[0] = presid;
   g.status[1] = brk;
   g.status[2] = h0;
   g.status[3] = h1;
+  double* st = g.status_it + 4 * col;
+  st[0] = presid;
+  st[1] = brk;
+  st[2] = h0;
+  st[3] = h1;
+  g.ctrl[1] = col;
+  if (presid <= ptol || brk != 0.0 || col >= stop_col) g.ctrl[0] = 1;
 }
 
 __global__ void gmres_start_kernel(GivensState g, const double* red, int idx_r, int idx_m) {
   if (threadIdx.x != 0) return;
+  g.ctrl[0] = 0;
+  g.ctrl[1] = -1;
   const double rn = sqrt(red[idx_r]);
   const double mn = sqrt(red[idx_m]);
   for (int k = 0; k <= g.restart; ++k) g.S[k] = make_double2(0.0, 0.0);
@@ -256,17 +283,30 @@ __global__ void gmres_solve_kernel(GivensState g, int col) {
   for (int k = 0; k <= col; ++k) g.ycoef[k] = cscale(y[k], g.vscale[k]);
 }
 
+// Krylov tuning knobs (hh_tune_krylov): non-temporal basis loads, streaming grid size.
+int g_krylov_nt = 1;  // measured +7.7% GMRES it/s at 4096^2 (profiles/r01_tune_krylov.log)
+int g_krylov_blocks = 1024;
+
 template <int K>
 void md_launch(const double2* V, size_t ldv, const double2* w, size_t len, double* part,
-               int blocks, hipStream_t s) {
-  hipLaunchKernelGGL((multidot_kernel<K>), dim3(blocks), dim3(kT), 0, s, V, ldv, w, len, part);
+               int blocks, hipStream_t s, const int* stop) {
+  if (g_krylov_nt)
+    hipLaunchKernelGGL((multidot_kernel<K, true>), dim3(blocks), dim3(kT), 0, s, V, ldv, w, len,
+                       part, stop);
+  else
+    hipLaunchKernelGGL((multidot_kernel<K, false>), dim3(blocks), dim3(kT), 0, s, V, ldv, w, len,
+                       part, stop);
 }
 template <int K>
 void up_launch(const double2* V, size_t ldv, const double* raw, const double* scale,
                const double2* w, double2* wo, size_t len, double* part, int blocks,
-               hipStream_t s) {
-  hipLaunchKernelGGL((update_kernel<K>), dim3(blocks), dim3(kT), 0, s, V, ldv, raw, scale, w, wo,
-                     len, part);
+               hipStream_t s, const int* stop) {
+  if (g_krylov_nt)
+    hipLaunchKernelGGL((update_kernel<K, true>), dim3(blocks), dim3(kT), 0, s, V, ldv, raw, scale,
+                       w, wo, len, part, stop);
+  else
+    hipLaunchKernelGGL((update_kernel<K, false>), dim3(blocks), dim3(kT), 0, s, V, ldv, raw, scale,
+                       w, wo, len, part, stop);
 }
 template <int K>
 void xu_launch(const double2* V, size_t ldv, const double2* y, double2* x, size_t len, int blocks,
@@ -276,9 +316,10 @@ void xu_launch(const double2* V, size_t ldv, const double2* y, double2* x, size_
 
 template <int... Ks>
 struct KTable {
-  using MD = void (*)(const double2*, size_t, const double2*, size_t, double*, int, hipStream_t);
+  using MD = void (*)(const double2*, size_t, const double2*, size_t, double*, int, hipStream_t,
+                      const int*);
   using UP = void (*)(const double2*, size_t, const double*, const double*, const double2*,
-                      double2*, size_t, double*, int, hipStream_t);
+                      double2*, size_t, double*, int, hipStream_t, const int*);
   using XU = void (*)(const double2*, size_t, const double2*, double2*, size_t, int, hipStream_t);
   static constexpr MD md[] = {md_launch<Ks>...};
   static constexpr UP up[] = {up_launch<Ks>...};
@@ -290,22 +331,27 @@ static_assert(kMaxProj == 32, "table covers 1..kMaxProj");
 
 }  // namespace
 
+void tune_krylov(int nt, int blocks) {
+  g_krylov_nt = nt;
+  g_krylov_blocks = blocks > 0 ? (blocks < kMaxStreamBlocks ? blocks : kMaxStreamBlocks) : 1024;
+}
+
 int stream_blocks(size_t len) {
   size_t b = (len + kT - 1) / kT;
-  if (b > 1024) b = 1024;
+  if (b > (size_t)g_krylov_blocks) b = g_krylov_blocks;
   if (b < 1) b = 1;
   return (int)b;
 }
 
 void launch_multidot(const double2* V, size_t ldv, int K, const double2* w, size_t len,
-                     double* partials, int blocks, hipStream_t stream) {
-  Table::md[K - 1](V, ldv, w, len, partials, blocks, stream);
+                     double* partials, int blocks, hipStream_t stream, const int* stop) {
+  Table::md[K - 1](V, ldv, w, len, partials, blocks, stream, stop);
 }
 
 void launch_update(const double2* V, size_t ldv, int K, const double* raw, const double* scale,
                    const double2* w, double2* w_out, size_t len, double* partials, int blocks,
-                   hipStream_t stream) {
-  Table::up[K - 1](V, ldv, raw, scale, w, w_out, len, partials, blocks, stream);
+                   hipStream_t stream, const int* stop) {
+  Table::up[K - 1](V, ldv, raw, scale, w, w_out, len, partials, blocks, stream, stop);
 }
 
 void launch_xupdate(const double2* V, size_t ldv, int K, const double2* y, double2* x,
@@ -314,12 +360,14 @@ void launch_xupdate(const double2* V, size_t ldv, int K, const double2* y, doubl
 }
 
 void launch_reduce(const double* partials, int count, int width, int cols, double* out,
-                   hipStream_t stream) {
-  hipLaunchKernelGGL(reduce_kernel, dim3(cols), dim3(kT), 0, stream, partials, count, width, out);
+                   hipStream_t stream, const int* stop) {
+  hipLaunchKernelGGL(reduce_kernel, dim3(cols), dim3(kT), 0, stream, partials, count, width, out,
+                     stop);
 }
 
-void launch_add_small(const double* in, double* out, int count, hipStream_t stream) {
-  hipLaunchKernelGGL(add_small_kernel, dim3(1), dim3(kT), 0, stream, in, out, count);
+void launch_add_small(const double* in, double* out, int count, hipStream_t stream,
+                      const int* stop) {
+  hipLaunchKernelGGL(add_small_kernel, dim3(1), dim3(kT), 0, stream, in, out, count, stop);
 }
 
 void launch_fill_hash(double2* v, size_t len, size_t goff, uint64_t seed, hipStream_t stream) {
@@ -328,15 +376,16 @@ void launch_fill_hash(double2* v, size_t len, size_t goff, uint64_t seed, hipStr
 }
 
 void launch_scale_copy(const double2* in, double2* out, size_t len, double s,
-                       hipStream_t stream) {
+                       hipStream_t stream, const int* stop) {
   hipLaunchKernelGGL(scale_copy_kernel, dim3(stream_blocks(len)), dim3(kT), 0, stream, in, out,
-                     len, s);
+                     len, s, stop);
 }
 
 void launch_gmres_column(const GivensState& g, int col, const double* red_dots,
-                         const double* red_norm, double eps, hipStream_t stream) {
+                         const double* red_norm, double eps, double ptol, int stop_col,
+                         hipStream_t stream) {
   hipLaunchKernelGGL(gmres_column_kernel, dim3(1), dim3(kWave), 0, stream, g, col, red_dots,
-                     red_norm, eps);
+                     red_norm, eps, ptol, stop_col);
 }
 
 void launch_gmres_start(const GivensState& g, const double* red, int idx_r, int idx_m,

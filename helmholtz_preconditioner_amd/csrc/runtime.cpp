@@ -122,6 +122,9 @@ struct hh_op {
   double* status_h = nullptr;
   // timing hooks
   hipEvent_t tk0 = nullptr, tk1 = nullptr;
+  // device stop flag of the GMRES cycle being queued (nullptr outside hh_gmres)
+  const int* stop_flag = nullptr;
+  int* gctrl = nullptr;
   // tuning (hh_op_tune): stencil variant for the plain apply, rows per block override
   int variant = -1;
   int rpb_override = 0;
@@ -187,6 +190,7 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
     a.in1 = in1 ? in1 + s.off : nullptr;
     a.out0 = out0 ? out0 + s.off : nullptr;
     a.out1 = out1 ? out1 + s.off : nullptr;
+    a.stop = op->stop_flag;
     return a;
   };
 
@@ -199,6 +203,9 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
     a.rows_per_block = (op->rpb_override > 0 && rpb > 1) ? std::min(op->rpb_override, r1 - r0) : rpb;
     a.grid_blocks = op->grid_override;
     a.partials = op->partials + (size_t)nparts * kMaxNorms;
+    REQUIRE((size_t)(nparts + stencil_grid_blocks(n, r1 - r0, a.rows_per_block)) * kMaxNorms <=
+                op->partials_cap,
+            "partials workspace too small for the stencil launch");
     int written = 0;
     launch_stencil(epi, op->const_c, a, &written, c->stream, op->variant);
     nparts += written;
@@ -248,7 +255,10 @@ int run_point(hh_op* op, int pt, const double2* in0, double2* out0, bool shifted
     a.mshift = shifted ? op->mshift : make_double2(1.0, 0.0);
     a.damping = op->damping;
     a.partials = op->partials + (size_t)nparts * kMaxNorms;
+    a.stop = op->stop_flag;
     const int blocks = point_blocks((size_t)s.nl * op->n);
+    REQUIRE((size_t)(nparts + blocks) * kMaxNorms <= op->partials_cap,
+            "partials workspace too small for the pointwise launch");
     launch_point(pt, op->const_c, a, blocks, c->stream);
     nparts += blocks;
   }
@@ -273,7 +283,7 @@ void sl_sweeps(hh_op* op, const double2* T, double2* z1dst, double2* out) {
     run_stencil(op, EPI_SL_SWEEP, cur, nullptr, T, dst, nullptr, true);
     cur = dst;
   }
-  if (cur != out) launch_scale_copy(cur, out, op->nloc, 1.0, op->ctx->stream);
+  if (cur != out) launch_scale_copy(cur, out, op->nloc, 1.0, op->ctx->stream, op->stop_flag);
 }
 double2* sl_first_dst(hh_op* op, double2* out) {
   return ((op->sweeps - 1) % 2 == 0) ? out : op->scrZ;
@@ -368,7 +378,7 @@ void ensure_gmres(hh_op* op, int restart) {
   op->V_cols = restart + 1;
   const int R1 = restart + 1;
   const size_t nH = (size_t)restart * R1, nG = 2 * (size_t)restart, nS = R1, nY = restart;
-  const size_t total2 = nH + nG + nS + nY + (R1 + 8 + 1) / 2 + 8;
+  const size_t total2 = nH + nG + nS + nY + (R1 + 8 + 1) / 2 + 8 + 2 * (size_t)restart + 8;
   op->gbuf = dalloc<double2>(total2);
   HIPC(hipMemset(op->gbuf, 0, total2 * sizeof(double2)));
   GivensState& g = op->gs;
@@ -378,6 +388,11 @@ void ensure_gmres(hh_op* op, int restart) {
   g.ycoef = g.S + nS;
   g.vscale = reinterpret_cast<double*>(g.ycoef + nY);
   g.status = g.vscale + R1 + 1;
+  g.status_it = g.status + 8;
+  dfree(op->gctrl);
+  op->gctrl = dalloc<int>(8);
+  HIPC(hipMemset(op->gctrl, 0, 8 * sizeof(int)));
+  g.ctrl = op->gctrl;
   g.restart = restart;
 }
 
@@ -611,10 +626,10 @@ HH_API int hh_op_create(hh_ctx* c, int n, int b, double cconst, double eta, doub
     // partial-sum workspace: stencil tiles (+ boundary rows) of every slab, or streaming blocks
     size_t tiles = 0;
     for (const Slab& sl : op->slabs) {
-      tiles += (size_t)stencil_grid_blocks(n, sl.nl, sl.rpb) +
+      tiles += (size_t)stencil_grid_blocks(n, sl.nl, std::min(sl.rpb, 4)) +
                2 * (size_t)((n + kStencilThreads - 1) / kStencilThreads) + 8;
     }
-    size_t cap = std::max(tiles * kMaxNorms, (size_t)1024 * (2 * kMaxProj + 2));
+    size_t cap = std::max(tiles * kMaxNorms, (size_t)kMaxStreamBlocks * (2 * kMaxProj + 2));
     cap = std::max(cap, (size_t)c->vslabs * 2048 * kMaxNorms);
     op->partials = dalloc<double>(cap);
     op->partials_cap = cap;
@@ -651,6 +666,7 @@ HH_API int hh_op_destroy(hh_op* op) {
   dfree(op->scrR);
   dfree(op->V);
   dfree(op->gbuf);
+  dfree(op->gctrl);
   if (op->status_h) (void)hipHostFree(op->status_h);
   delete op;
   GUARD_END
@@ -854,9 +870,17 @@ HH_API int hh_op_tune(hh_op* op, int variant, int rows_per_block, int grid_block
   REQUIRE(grid_blocks >= 0, "grid_blocks must be >= 0");
   op->grid_override = grid_blocks;
   REQUIRE(variant >= -1 && variant < kNumVariants, "variant must be in [-1, %d)", kNumVariants);
-  REQUIRE(rows_per_block >= 0 && rows_per_block <= 4096, "rows_per_block must be in [0, 4096]");
+  REQUIRE(rows_per_block == 0 || (rows_per_block >= 4 && rows_per_block <= 4096),
+          "rows_per_block must be 0 or in [4, 4096]");
   op->variant = variant;
   op->rpb_override = rows_per_block;
+  GUARD_END
+}
+
+HH_API int hh_tune_krylov(int nt_loads, int blocks) {
+  GUARD_BEGIN
+  REQUIRE(blocks >= 0 && blocks <= (1 << 20), "blocks out of range");
+  tune_krylov(nt_loads, blocks);
   GUARD_END
 }
 
@@ -918,6 +942,8 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
   GivensState& g = op->gs;
   const double eps = std::numeric_limits<double>::epsilon();
   const int blocks = stream_blocks(L);
+  REQUIRE((size_t)blocks * (2 * (restart + 1) + 2) <= op->partials_cap,
+          "partials workspace too small for %d streaming blocks", blocks);
   double st[8];
 
   // red[4] = |b|^2 (= |r|^2 while x0 == 0), red[2] = |x0|^2
@@ -962,45 +988,62 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         return HH_OK;
       }
     }
-    // v[0] = psolve(r) / ||psolve(r)||, S[0] = ||psolve(r)|| (lazy scale)
+    // v[0] = psolve(r) / ||psolve(r)||, S[0] = ||psolve(r)|| (lazy scale); clears the stop flag
     launch_gmres_start(g, op->red, 4, 5, s);
+    // The whole cycle is queued at once: the column kernel evaluates scipy's inner exit test
+    // (presid <= ptol, breakdown, legacy maxiter) and raises the stop flag, after which the
+    // kernels still queued in this cycle return immediately.  One host sync per cycle.
     bool breakdown = false;
     int col = 0;
-    for (col = 0; col < restart; ++col) {
-      double2* vcol = V + (size_t)col * ldv;
-      double2* w = V + (size_t)(col + 1) * ldv;
-      apply_MA(op, vcol, g.vscale + col, w);  // w = M A v_col
-      const int K = col + 1;
+    const long left = legacy ? maxiter - inner : (long)restart;
+    const int stop_col = (int)std::min<long>(restart - 1, left - 1);
+    op->stop_flag = g.ctrl;
+    for (int c2 = 0; c2 <= stop_col; ++c2) {
+      double2* vcol = V + (size_t)c2 * ldv;
+      double2* w = V + (size_t)(c2 + 1) * ldv;
+      const int* stp = g.ctrl;
+      apply_MA(op, vcol, g.vscale + c2, w);  // w = M A v_col
+      const int K = c2 + 1;
       // classical Gram-Schmidt: raw dots u_k^H w (+ |w|^2), then w -= sum h_k v_k, |w|^2
-      launch_multidot(V, ldv, K, w, L, op->partials, blocks, s);
-      launch_reduce(op->partials, blocks, 2 * K + 2, 2 * K + 1, op->red + 16, s);
+      launch_multidot(V, ldv, K, w, L, op->partials, blocks, s, stp);
+      launch_reduce(op->partials, blocks, 2 * K + 2, 2 * K + 1, op->red + 16, s, stp);
       allreduce_sum_dev(op, op->red + 16, 2 * K + 1);
-      launch_update(V, ldv, K, op->red + 16, g.vscale, w, w, L, op->partials, blocks, s);
-      launch_reduce(op->partials, blocks, kMaxNorms, 1, op->red + 8, s);
+      launch_update(V, ldv, K, op->red + 16, g.vscale, w, w, L, op->partials, blocks, s, stp);
+      launch_reduce(op->partials, blocks, kMaxNorms, 1, op->red + 8, s, stp);
       allreduce_sum_dev(op, op->red + 8, 1);
       if (reorth) {
         // CGS2: project once more; the H column is the sum of both passes' dots, h0 stays
         // the first pass's |w| (scipy's h0 is taken before orthogonalisation).
-        launch_multidot(V, ldv, K, w, L, op->partials, blocks, s);
-        launch_reduce(op->partials, blocks, 2 * K + 2, 2 * K, op->red + 96, s);
+        launch_multidot(V, ldv, K, w, L, op->partials, blocks, s, stp);
+        launch_reduce(op->partials, blocks, 2 * K + 2, 2 * K, op->red + 96, s, stp);
         allreduce_sum_dev(op, op->red + 96, 2 * K);
-        launch_update(V, ldv, K, op->red + 96, g.vscale, w, w, L, op->partials, blocks, s);
-        launch_reduce(op->partials, blocks, kMaxNorms, 1, op->red + 8, s);
+        launch_update(V, ldv, K, op->red + 96, g.vscale, w, w, L, op->partials, blocks, s, stp);
+        launch_reduce(op->partials, blocks, kMaxNorms, 1, op->red + 8, s, stp);
         allreduce_sum_dev(op, op->red + 8, 1);
-        launch_add_small(op->red + 96, op->red + 16, 2 * K, s);
+        launch_add_small(op->red + 96, op->red + 16, 2 * K, s, stp);
       }
-      launch_gmres_column(g, col, op->red + 16, op->red + 8, eps, s);
+      launch_gmres_column(g, c2, op->red + 16, op->red + 8, eps, ptol, stop_col, s);
       HIPC(hipGetLastError());
-      read_dev(op, g.status, st, 4);
-      presid = st[0];
-      breakdown = st[1] != 0.0;
-      inner += 1;
-      if (hist && inner - 1 < hist_cap) hist[inner - 1] = presid / bnrm2;
-      if (cb) cb(user, inner, presid / bnrm2);
-      if (legacy && inner == maxiter) break;
-      if (presid <= ptol || breakdown) break;
     }
-    if (col == restart) col = restart - 1;  // loop ran to completion
+    op->stop_flag = nullptr;
+    // one sync: per-iteration statuses + the last column executed
+    HIPC(hipMemcpyAsync(op->status_h, g.status_it, 4 * (size_t)restart * sizeof(double),
+                        hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(op->status_h + 4 * restart, g.ctrl, 2 * sizeof(int),
+                        hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    int ctl[2];
+    std::memcpy(ctl, op->status_h + 4 * restart, 2 * sizeof(int));
+    col = ctl[1];
+    REQUIRE(col >= 0 && col <= stop_col, "GMRES cycle state corrupt (last column %d)", col);
+    for (int k = 0; k <= col; ++k) {
+      const double pr = op->status_h[4 * k];
+      inner += 1;
+      if (hist && inner - 1 < hist_cap) hist[inner - 1] = pr / bnrm2;
+      if (cb) cb(user, inner, pr / bnrm2);
+    }
+    presid = op->status_h[4 * col];
+    breakdown = op->status_h[4 * col + 1] != 0.0;
     op->stats.restarts++;
     launch_gmres_solve(g, col, s);
     launch_xupdate(V, ldv, col + 1, g.ycoef, x, L, blocks, s);

@@ -124,6 +124,7 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t);
 // each XCD streams one contiguous band window (L2 reuse of band-edge rows).
 template <int EPI, bool CONSTC, int XM, int PF, bool NT, bool NTU>
 __global__ __launch_bounds__(kStencilThreads) void stencil_kernel(const StencilArgs a) {
+  if (a.stop && *a.stop) return;  // queued GMRES cycle already stopped
   const int L = blockIdx.x;
   const int q = L >> 3, Q = gridDim.x >> 3;
   const int ntiles = a.tiles_x * a.tiles_y;
@@ -322,6 +323,7 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
 // Pointwise operations needing only the diagonal D (or D_beta) of a point.
 template <int OP, bool CONSTC>
 __global__ __launch_bounds__(kStencilThreads) void point_kernel(const PointArgs a) {
+  if (a.stop && *a.stop) return;
   const int n = a.n;
   const int tiles_x = (n + kStencilThreads - 1) / kStencilThreads;
   const long ntiles = (long)tiles_x * a.nl;

@@ -165,6 +165,9 @@ int hh_gmres(hh_op* op, const hh_vec* b, hh_vec* x, double rtol, double atol,
  * persistent grid of that many workgroups (0 = one per tile).  Results are identical
  * for every setting; only speed changes. */
 int hh_op_tune(hh_op* op, int variant, int rows_per_block, int grid_blocks);
+/* Process-wide tuning of the Krylov streaming kernels (multidot / update): non-temporal
+ * basis loads on/off and the streaming grid size (0 = default 1024).  Speed only. */
+int hh_tune_krylov(int nt_loads, int blocks);
 /* Streaming roofline probes (diagnostic only): the stencil's byte mix without neighbour
  * traffic in different access shapes (`kind`, see csrc/probe.hip), `blocks` workgroups,
  * `iters` launches; outputs the average kernel ms and the probe's bytes per point. */

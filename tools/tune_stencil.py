@@ -40,7 +40,7 @@ A.tune(0, 0, 0)
 A.apply_device(x, y)
 ref = y.download()
 for v in variants:
-    for r, g in ((0, 0), (7, 0), (0, 64), (7, 24)):
+    for r, g in ((0, 0), (8, 0), (0, 64), (8, 24)):
         A.tune(v, r, g)
         A.apply_device(x, y)
         d = y.download()
