@@ -29,8 +29,9 @@ enum Epi : int {
 
 // W/E neighbour exchange of the stencil kernel (see stencil.hip).
 enum XMode : int { XM_LDS = 0, XM_DIRECT = 1, XM_SHFL = 2 };
-// Tuning variant = XM + 3 * (PF - 1) + 6 * NT + 12 * NTU  (0..23).
-constexpr int kNumVariants = 24;
+// Tuning variant = XM + 3 * (PF - 1) + 6 * NT + 12 * NTU + 24 * (512-wide strips)  (0..47;
+// the 512-wide set is instantiated for 24..27 and 30..33).
+constexpr int kNumVariants = 48;
 
 // Pointwise (no-neighbour) operations that need only the diagonal.
 enum PointOp : int {
@@ -82,6 +83,7 @@ struct PointArgs {
 void launch_stencil(int epi, bool const_c, const StencilArgs& a, int nblocks_out[1],
                     hipStream_t stream, int variant = -1);
 int stencil_default_variant();
+bool stencil_variant_valid(int v);  // instantiated for the plain apply
 // Streaming roofline probes (probe.hip); returns the probe's bytes per point (0: unknown kind).
 int launch_probe_kind(int kind, int blocks, const double2* u, const double* ic, double2* y,
                       size_t len, hipStream_t s);

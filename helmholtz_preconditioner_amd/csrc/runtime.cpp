@@ -869,7 +869,7 @@ HH_API int hh_op_tune(hh_op* op, int variant, int rows_per_block, int grid_block
   REQUIRE(op, "null op");
   REQUIRE(grid_blocks >= 0, "grid_blocks must be >= 0");
   op->grid_override = grid_blocks;
-  REQUIRE(variant >= -1 && variant < kNumVariants, "variant must be in [-1, %d)", kNumVariants);
+  REQUIRE(variant == -1 || stencil_variant_valid(variant), "variant %d not instantiated", variant);
   REQUIRE(rows_per_block == 0 || (rows_per_block >= 4 && rows_per_block <= 4096),
           "rows_per_block must be 0 or in [4, 4096]");
   op->variant = variant;

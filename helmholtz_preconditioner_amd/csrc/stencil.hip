@@ -36,11 +36,11 @@ struct EpiTraits {
   static constexpr bool shifted = (EPI == EPI_RES_SL || EPI == EPI_SL_FIRST || EPI == EPI_SL_SWEEP);
 };
 
-template <int NACC>
+template <int NACC, int TPB = kStencilThreads>
 __device__ __forceinline__ void block_reduce_store(double (&acc)[kMaxNorms], double* partials,
                                                    int slot) {
   if constexpr (NACC > 0) {
-    __shared__ double red[kMaxNorms][kStencilThreads / kWave];
+    __shared__ double red[kMaxNorms][TPB / kWave];
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = threadIdx.x / kWave;
 #pragma unroll
@@ -54,7 +54,7 @@ __device__ __forceinline__ void block_reduce_store(double (&acc)[kMaxNorms], dou
     if (threadIdx.x < NACC) {
       double s = 0.0;
 #pragma unroll
-      for (int w = 0; w < kStencilThreads / kWave; ++w) s += red[threadIdx.x][w];
+      for (int w = 0; w < TPB / kWave; ++w) s += red[threadIdx.x][w];
       partials[(size_t)slot * kMaxNorms + threadIdx.x] = s;
     }
   }
@@ -116,14 +116,14 @@ using cdouble_p = const __attribute__((address_space(4))) double*;
 // The row loop is unrolled by the register-ring length: ring slot m always holds row
 // rb-1+m (mod ring), so no value is copied between registers -- a copy of a register with
 // a load still in flight would make hipcc drain vmcnt and serialise the prefetch.
-template <int EPI, bool CONSTC, int XM, int PF, bool NT, bool NTU>
+template <int EPI, bool CONSTC, int XM, int PF, bool NT, bool NTU, int TPB>
 __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t);
 
 // Grid: either one block per tile, or a persistent grid of `gridDim.x` blocks (a multiple
 // of 8) in which block L works through the tiles of XCD L % 8 in order, so at any moment
 // each XCD streams one contiguous band window (L2 reuse of band-edge rows).
-template <int EPI, bool CONSTC, int XM, int PF, bool NT, bool NTU>
-__global__ __launch_bounds__(kStencilThreads) void stencil_kernel(const StencilArgs a) {
+template <int EPI, bool CONSTC, int XM, int PF, bool NT, bool NTU, int TPB>
+__global__ __launch_bounds__(TPB) void stencil_kernel(const StencilArgs a) {
   if (a.stop && *a.stop) return;  // queued GMRES cycle already stopped
   const int L = blockIdx.x;
   const int q = L >> 3, Q = gridDim.x >> 3;
@@ -131,18 +131,18 @@ __global__ __launch_bounds__(kStencilThreads) void stencil_kernel(const StencilA
   for (int tt = q; tt < a.tiles_per_xcd; tt += Q) {
     const int t = (L & 7) * a.tiles_per_xcd + tt;
     if (t >= ntiles) break;  // uniform per block
-    stencil_tile<EPI, CONSTC, XM, PF, NT, NTU>(a, t);
+    stencil_tile<EPI, CONSTC, XM, PF, NT, NTU, TPB>(a, t);
   }
 }
 
-template <int EPI, bool CONSTC, int XM, int PF, bool NT, bool NTU>
+template <int EPI, bool CONSTC, int XM, int PF, bool NT, bool NTU, int TPB>
 __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) {
   using T = EpiTraits<EPI>;
   constexpr int UR = (PF == 1) ? 4 : 6;  // u ring: u_{r-1} .. u_{r+1+PF}
   constexpr int IR = PF + 1;             // per-row input ring
   constexpr int UNR = UR;                // unroll (multiple of UR, IR and 2)
   static_assert(UNR % IR == 0 && UNR % 2 == 0, "ring sizes");
-  __shared__ double2 lrow[2][XM == XM_LDS ? kStencilThreads + 2 : 1];
+  __shared__ double2 lrow[2][XM == XM_LDS ? TPB + 2 : 1];
 
   // XCD-aware tile map (see stencil_kernel): tile t is a 256-wide strip x one row band.
   const int tx = t % a.tiles_x;
@@ -150,7 +150,7 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int n = a.n;
-  const int i0 = tx * kStencilThreads;
+  const int i0 = tx * TPB;
   const int i = i0 + tid;
   const bool act = i < n;
   const int ic_ = min(i, n - 1);  // clamped column for loads
@@ -166,7 +166,7 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
   int iw, ie;
   bool lw, le;
   if constexpr (XM == XM_LDS) {
-    iw = i0 - 1; ie = i0 + kStencilThreads; lw = tid == 0; le = tid == kStencilThreads - 1;
+    iw = i0 - 1; ie = i0 + TPB; lw = tid == 0; le = tid == TPB - 1;
   } else if constexpr (XM == XM_SHFL) {
     iw = i - lane - 1; ie = i - lane + kWave; lw = lane == 0; le = lane == kWave - 1;
   } else {
@@ -254,7 +254,7 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
         double2* buf = lrow[k & 1];
         buf[tid + 1] = uCm;
         if (tid == 0) buf[0] = eW;
-        if (tid == kStencilThreads - 1) buf[kStencilThreads + 1] = eE;
+        if (tid == TPB - 1) buf[TPB + 1] = eE;
         __syncthreads();
         uW = buf[tid];
         uE = buf[tid + 2];
@@ -316,7 +316,7 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
       }
     });
   }
-  block_reduce_store<T::nacc>(acc, a.partials, t);
+  block_reduce_store<T::nacc, TPB>(acc, a.partials, t);
   if constexpr (T::nacc > 0 || XM == XM_LDS) __syncthreads();  // LDS reuse by the next tile
 }
 
@@ -368,16 +368,20 @@ __global__ __launch_bounds__(kStencilThreads) void point_kernel(const PointArgs 
 
 // Default exchange/prefetch/store variant for every epilogue (tuned on MI355X, see
 // DESIGN.md "stencil variants"); the benchmark kernel (EPI_AX) can run all 12 variants.
-constexpr int kDefaultVariant = 6;  // XM_LDS, PF 1, NT stores + NT 1/c^2 loads
+constexpr int kDefaultVariant = 30;  // XM_LDS, PF 1, NT stores + NT 1/c^2 loads, 512-wide strips
 
-// Variant table: V = XM + 3 (PF - 1) + 6 NT + 12 NTU  (0..23).
+// Variant table: V = XM + 3 (PF - 1) + 6 NT + 12 NTU + 24 (512-wide strips)  (0..47).
+template <int V>
+constexpr int variant_tpb() { return V >= 24 ? 512 : 256; }
 template <int EPI, bool C, int V>
 struct VariantLaunch {
   static void go(const StencilArgs& a, int blocks, hipStream_t s) {
-    constexpr int XM = V % 3, PF = (V / 3) % 2 + 1;
-    constexpr bool NT = (V / 6) % 2 == 1, NTU = V >= 12;
-    hipLaunchKernelGGL((stencil_kernel<EPI, C, XM, PF, NT, NTU>), dim3(blocks),
-                       dim3(kStencilThreads), 0, s, a);
+    constexpr int W = V % 24;
+    constexpr int XM = W % 3, PF = (W / 3) % 2 + 1;
+    constexpr bool NT = (W / 6) % 2 == 1, NTU = W >= 12;
+    constexpr int TPB = variant_tpb<V>();
+    hipLaunchKernelGGL((stencil_kernel<EPI, C, XM, PF, NT, NTU, TPB>), dim3(blocks), dim3(TPB), 0,
+                       s, a);
   }
 };
 
@@ -398,7 +402,7 @@ template <int EPI>
 void launch_stencil_t(bool const_c, const StencilArgs& a, int blocks, hipStream_t s, int v) {
   if constexpr (EPI == EPI_AX) {
     launch_any<EPI, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21,
-               22, 23>(v, const_c, a, blocks, s);
+               22, 23, 24, 25, 26, 27, 30, 31, 32, 33>(v, const_c, a, blocks, s);
   } else {
     (void)v;
     launch_v<EPI, kDefaultVariant>(const_c, a, blocks, s);
@@ -439,12 +443,15 @@ int stencil_grid_blocks(int n, int rows, int rows_per_block) {
 
 
 int stencil_default_variant() { return kDefaultVariant; }
+bool stencil_variant_valid(int v) { return (v >= 0 && v <= 27) || (v >= 30 && v <= 33); }
 
 void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_out[1],
                     hipStream_t stream, int variant) {
   StencilArgs a = a_in;
   const int rows = a.row_end - a.row_begin;
-  a.tiles_x = (a.n + kStencilThreads - 1) / kStencilThreads;
+  const int v = (epi == EPI_AX && stencil_variant_valid(variant)) ? variant : kDefaultVariant;
+  const int tpb = v >= 24 ? 512 : 256;
+  a.tiles_x = (a.n + tpb - 1) / tpb;
   a.tiles_y = (rows + a.rows_per_block - 1) / a.rows_per_block;
   a.tiles_per_xcd = (a.tiles_x * a.tiles_y + 7) / 8;
   int blocks = a.tiles_per_xcd * 8;

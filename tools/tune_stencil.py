@@ -16,7 +16,7 @@ p = argparse.ArgumentParser()
 p.add_argument("--n", type=int, default=4096)
 p.add_argument("--rounds", type=int, default=3)
 p.add_argument("--iters", type=int, default=50)
-p.add_argument("--variants", default="0,6,7,8,9,18,19,20,21")
+p.add_argument("--variants", default="6,7,9,24,30,31,33")
 p.add_argument("--grids", default="0,1280")
 p.add_argument("--rpbs", default="16,32,64")
 p.add_argument("--medium", default="marmousi")
@@ -27,8 +27,9 @@ grids = [int(v) for v in a.grids.split(",")]
 
 
 def vname(v):
-    return f"{['lds', 'direct', 'shfl'][v % 3]} pf{(v // 3) % 2 + 1}{' nt' if (v // 6) % 2 else ''}" \
-           f"{' ntu' if v >= 12 else ''}"
+    w = v % 24
+    return f"{['lds', 'direct', 'shfl'][w % 3]} pf{(w // 3) % 2 + 1}{' nt' if (w // 6) % 2 else ''}" \
+           f"{' ntu' if w >= 12 else ''}{' w512' if v >= 24 else ''}"
 
 # correctness on a ragged grid: every variant bit-identical to variant 0
 n = 1000
