@@ -52,7 +52,20 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-gmres-iters", type=int, default=4)
     p.add_argument("--virtual-slabs", type=int, default=1)
-    return p.parse_args()
+    p.add_argument("--config", type=int, default=0, choices=[0, 1, 2, 3, 4, 5],
+                   help="BASELINE.json config preset (fixed grid => strong scaling); "
+                        "0 = config 3 workload with weak scaling (default)")
+    a = p.parse_args()
+    if a.config:  # SURVEY.md 8d concrete inputs
+        grid, medium, wn, pc, its = {1: (128, "const", 8.0, "none", 200),
+                                     2: (1024, "const", 64.0, "jacobi", 100),
+                                     3: (4096, "marmousi", 100.0, "sl", 20),
+                                     4: (8192, "const", 256.0, "jacobi", 20),
+                                     5: (16384, "const", 800.0, "jacobi", 20)}[a.config]
+        a.grid, a.medium, a.wave_num, a.precond = a.grid or grid, medium, wn, pc
+        if a.gmres_iters == 40:
+            a.gmres_iters = its
+    return a
 
 
 def relaunch_distributed(args):
@@ -195,12 +208,12 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.config and world > 1 else "weak",
         "vs_baseline": None,
         "dtype": "complex128",
         "data": f"synthetic: {args.medium}-like velocity (seeded), hash-filled complex input",
         "config": {
-            "workload": f"config3: {n}x{n} {args.medium} velocity, matrix-free PML stencil apply "
+            "workload": f"config{args.config or 3}: {n}x{n} {args.medium} velocity, matrix-free PML stencil apply "
                         f"(+ GMRES({args.restart}) {args.precond}-preconditioned)",
             "n": n, "unknowns": n * n, "wave_num": args.wave_num, "b": args.b, "C": args.C,
             "alpha": args.alpha, "bytes_per_unknown": bpp,
@@ -263,7 +276,7 @@ def main():
         del f, xs
 
     # ---------------- CPU baseline (rank 0, N=1) ----------------
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and n <= 4096:
         if args.medium == "marmousi":
             c_full = c_mat  # N=1: the full field was generated
         else:

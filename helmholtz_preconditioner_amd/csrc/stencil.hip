@@ -404,8 +404,9 @@ void launch_stencil_t(bool const_c, const StencilArgs& a, int blocks, hipStream_
     launch_any<EPI, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21,
                22, 23, 24, 25, 26, 27, 30, 31, 32, 33>(v, const_c, a, blocks, s);
   } else {
-    (void)v;
-    launch_v<EPI, kDefaultVariant>(const_c, a, blocks, s);
+    // every epilogue has the two default shapes: 256-wide (small grids) and 512-wide strips
+    if (v == 6) launch_v<EPI, 6>(const_c, a, blocks, s);
+    else launch_v<EPI, kDefaultVariant>(const_c, a, blocks, s);
   }
 }
 
@@ -420,17 +421,25 @@ void launch_point_t(bool const_c, const PointArgs& a, int blocks, hipStream_t s)
 }  // namespace
 
 int stencil_rows_per_block(int n, int rows) {
-  // ~2048 tiles (8 per CU): measured best at 4096^2 (32-row bands, tools/tune_stencil.py);
-  // bands long enough to amortise their two halo rows, a multiple of the 4-row unroll.
+  // ~2048 tiles (8 per CU) counted in 256-wide strips: 32-row bands at 4096^2 (measured
+  // best, tools/tune_stencil.py); short bands keep small grids busy; long bands amortise
+  // the two halo rows.  A multiple of the 4-row unroll.
   const int tiles_x = (n + kStencilThreads - 1) / kStencilThreads;
   long want_y = 2048 / tiles_x;
   if (want_y < 1) want_y = 1;
   int rpb = (int)((rows + want_y - 1) / want_y);
   rpb = (rpb + 3) / 4 * 4;
-  if (rpb < 16) rpb = 16;
+  if (rpb < 4) rpb = 4;
   if (rpb > 256) rpb = 256;
   if (rpb > rows) rpb = rows > 0 ? rows : 1;
   return rpb;
+}
+
+int stencil_resolve_variant(int epi, int requested, int n) {
+  const int autov = n < 2048 ? 6 : kDefaultVariant;  // 256-wide strips for small grids
+  if (requested < 0) return autov;
+  if (epi == EPI_AX) return stencil_variant_valid(requested) ? requested : autov;
+  return (requested == 6 || requested == kDefaultVariant) ? requested : autov;
 }
 
 int stencil_grid_blocks(int n, int rows, int rows_per_block) {
@@ -449,7 +458,7 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_
                     hipStream_t stream, int variant) {
   StencilArgs a = a_in;
   const int rows = a.row_end - a.row_begin;
-  const int v = (epi == EPI_AX && stencil_variant_valid(variant)) ? variant : kDefaultVariant;
+  const int v = stencil_resolve_variant(epi, variant, a.n);
   const int tpb = v >= 24 ? 512 : 256;
   a.tiles_x = (a.n + tpb - 1) / tpb;
   a.tiles_y = (rows + a.rows_per_block - 1) / a.rows_per_block;
@@ -458,13 +467,13 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_
   if (a.grid_blocks > 0 && a.grid_blocks < blocks) blocks = (a.grid_blocks + 7) / 8 * 8;
   nblocks_out[0] = a.tiles_x * a.tiles_y;  // partial slots written (one per tile)
   switch (epi) {
-    case EPI_AX: launch_stencil_t<EPI_AX>(const_c, a, blocks, stream, variant); break;
-    case EPI_JAC: launch_stencil_t<EPI_JAC>(const_c, a, blocks, stream, variant); break;
-    case EPI_RES: launch_stencil_t<EPI_RES>(const_c, a, blocks, stream, variant); break;
-    case EPI_RES_JAC: launch_stencil_t<EPI_RES_JAC>(const_c, a, blocks, stream, variant); break;
-    case EPI_RES_SL: launch_stencil_t<EPI_RES_SL>(const_c, a, blocks, stream, variant); break;
-    case EPI_SL_FIRST: launch_stencil_t<EPI_SL_FIRST>(const_c, a, blocks, stream, variant); break;
-    case EPI_SL_SWEEP: launch_stencil_t<EPI_SL_SWEEP>(const_c, a, blocks, stream, variant); break;
+    case EPI_AX: launch_stencil_t<EPI_AX>(const_c, a, blocks, stream, v); break;
+    case EPI_JAC: launch_stencil_t<EPI_JAC>(const_c, a, blocks, stream, v); break;
+    case EPI_RES: launch_stencil_t<EPI_RES>(const_c, a, blocks, stream, v); break;
+    case EPI_RES_JAC: launch_stencil_t<EPI_RES_JAC>(const_c, a, blocks, stream, v); break;
+    case EPI_RES_SL: launch_stencil_t<EPI_RES_SL>(const_c, a, blocks, stream, v); break;
+    case EPI_SL_FIRST: launch_stencil_t<EPI_SL_FIRST>(const_c, a, blocks, stream, v); break;
+    case EPI_SL_SWEEP: launch_stencil_t<EPI_SL_SWEEP>(const_c, a, blocks, stream, v); break;
     default: break;
   }
 }
