@@ -18,12 +18,13 @@ from .media import (constant_c_mat, init_c1_f1, init_c1_f2, init_c1_mat, init_c2
                     init_c2_f2, init_c2_mat, init_f1_mat, init_f2_mat, marmousi_like_c_mat,
                     problem_params)
 from .operator import (DeviceOperator, DevicePreconditioner, DeviceVector, Jacobi,  # noqa: F401
-                       ShiftedLaplace, build_A_matrix)
+                       ShiftedLaplace, Sweeping, build_A_matrix)
 from .solver import gmres  # noqa: F401
 from . import dist  # noqa: F401
 
 __all__ = [
     "build_A_matrix", "gmres", "DeviceOperator", "DeviceVector", "Jacobi", "ShiftedLaplace",
+    "Sweeping",
     "Context", "default_context", "set_default_context", "device_count", "unique_id",
     "init_c1_mat", "init_c2_mat", "init_f1_mat", "init_f2_mat", "init_c1_f1", "init_c1_f2",
     "init_c2_f1", "init_c2_f2", "constant_c_mat", "marmousi_like_c_mat", "problem_params",

@@ -27,7 +27,7 @@ c_lp = ctypes.POINTER(ctypes.c_long)
 c_ubp = ctypes.POINTER(ctypes.c_ubyte)
 PP = ctypes.POINTER(ctypes.c_void_p)
 
-HH_PREC_NONE, HH_PREC_JACOBI, HH_PREC_SHIFTED_LAPLACE = 0, 1, 2
+HH_PREC_NONE, HH_PREC_JACOBI, HH_PREC_SHIFTED_LAPLACE, HH_PREC_SWEEP, HH_PREC_SWEEP_REF = 0, 1, 2, 3, 4
 HH_APPLY_A, HH_APPLY_JACOBI_A, HH_APPLY_PREC, HH_APPLY_PREC_A = 0, 1, 2, 3
 HH_TRANSPORT_RCCL, HH_TRANSPORT_SHM = 0, 1
 

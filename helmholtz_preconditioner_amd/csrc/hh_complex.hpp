@@ -10,6 +10,7 @@ __device__ __forceinline__ double2 cadd(double2 a, double2 b) {
 __device__ __forceinline__ double2 csub(double2 a, double2 b) {
   return make_double2(a.x - b.x, a.y - b.y);
 }
+__device__ __forceinline__ double2 cneg(double2 a) { return make_double2(-a.x, -a.y); }
 __device__ __forceinline__ double2 cscale(double2 a, double s) {
   return make_double2(a.x * s, a.y * s);
 }

@@ -21,6 +21,7 @@
 #include "comm.hpp"
 #include "hh_error.hpp"
 #include "hh_internal.hpp"
+#include "sweep.hpp"
 
 using cd = std::complex<double>;
 
@@ -125,6 +126,12 @@ struct hh_op {
   // device stop flag of the GMRES cycle being queued (nullptr outside hh_gmres)
   const int* stop_flag = nullptr;
   int* gctrl = nullptr;
+  // sweeping preconditioner (HH_PREC_SWEEP / HH_PREC_SWEEP_REF)
+  SweepArgs sweep{};
+  double2* sw_P = nullptr;
+  double2* sw_y = nullptr;
+  double2* sw_uF = nullptr;
+  double2* sw_const = nullptr;  // as-is (quirk Q1): M x = algo2_4(b) for every x
   // tuning (hh_op_tune): stencil variant for the plain apply, rows per block override
   int variant = -1;
   int rpb_override = 0;
@@ -289,6 +296,21 @@ double2* sl_first_dst(hh_op* op, double2* out) {
   return ((op->sweeps - 1) % 2 == 0) ? out : op->scrZ;
 }
 
+bool is_sweep(int kind) { return kind == HH_PREC_SWEEP || kind == HH_PREC_SWEEP_REF; }
+
+// algo2_4 (code.py:356-385) on r -> out: forward, middle (as-is: u -= T u, quirk Q2;
+// corrected: u = T u), backward sweeps.  r and out must differ.
+void sweep_apply(hh_op* op, const double2* r, double2* out, bool asis) {
+  hipStream_t s = op->ctx->stream;
+  launch_scale_copy(r, out, op->nloc, 1.0, s, op->stop_flag);
+  SweepArgs a = op->sweep;
+  a.stop = op->stop_flag;
+  launch_sweep(a, 1, out, op->sw_uF, 0, s);
+  launch_sweep(a, 2, out, op->sw_uF, asis ? 1 : 0, s);
+  launch_sweep(a, 3, out, op->sw_uF, 0, s);
+  HIPC(hipGetLastError());
+}
+
 // out = M A (s * v)
 void apply_MA(hh_op* op, const double2* v, const double* vs, double2* out) {
   switch (op->pkind) {
@@ -305,6 +327,16 @@ void apply_MA(hh_op* op, const double2* v, const double* vs, double2* out) {
       sl_sweeps(op, op->scrT, z1, out);
       break;
     }
+    case HH_PREC_SWEEP:
+      ensure_scratch(op);
+      run_stencil(op, EPI_AX, v, vs, nullptr, op->scrT, nullptr, false);
+      sweep_apply(op, op->scrT, out, false);
+      break;
+    case HH_PREC_SWEEP_REF:
+      // code.py:510-511 (quirk Q1): the preconditioner ignores its argument
+      REQUIRE(op->sw_const, "as-is sweeping preconditioner needs its right-hand side (hh_gmres)");
+      launch_scale_copy(op->sw_const, out, op->nloc, 1.0, op->ctx->stream, op->stop_flag);
+      break;
   }
 }
 
@@ -324,6 +356,15 @@ void apply_M(hh_op* op, const double2* r, double2* out) {
       sl_sweeps(op, r, z1, out);
       break;
     }
+    case HH_PREC_SWEEP:
+      sweep_apply(op, r, out, false);
+      break;
+    case HH_PREC_SWEEP_REF:
+      if (op->sw_const)  // inside hh_gmres: constant map (quirk Q1)
+        launch_scale_copy(op->sw_const, out, op->nloc, 1.0, op->ctx->stream, op->stop_flag);
+      else               // plain apply: algo2_4 as-is (quirk Q2) on the given vector
+        sweep_apply(op, r, out, true);
+      break;
   }
 }
 
@@ -356,6 +397,15 @@ void residual(hh_op* op, const double2* b, const double2* x, double2* v0, int ds
       const int np = run_stencil(op, EPI_RES_SL, x, nullptr, b, op->scrR, z1, true);
       reduce_norms(op, np, dst, 1);  // red[dst] = |r|^2
       sl_sweeps(op, op->scrR, z1, v0);
+      norm2(op, v0, dst + 1);
+      break;
+    }
+    case HH_PREC_SWEEP:
+    case HH_PREC_SWEEP_REF: {
+      if (!op->scrR) op->scrR = dalloc<double2>(op->nloc);
+      const int np = run_stencil(op, EPI_RES, x, nullptr, b, op->scrR, nullptr, false);
+      reduce_norms(op, np, dst, 1);  // red[dst] = |r|^2
+      apply_M(op, op->scrR, v0);
       norm2(op, v0, dst + 1);
       break;
     }
@@ -667,6 +717,10 @@ HH_API int hh_op_destroy(hh_op* op) {
   dfree(op->V);
   dfree(op->gbuf);
   dfree(op->gctrl);
+  dfree(op->sw_P);
+  dfree(op->sw_y);
+  dfree(op->sw_uF);
+  dfree(op->sw_const);
   if (op->status_h) (void)hipHostFree(op->status_h);
   delete op;
   GUARD_END
@@ -683,11 +737,44 @@ HH_API int hh_op_local_rows(hh_op* op, int* j_begin, int* j_end) {
 HH_API int hh_op_set_precond(hh_op* op, int kind, double beta, int sweeps, double damping) {
   GUARD_BEGIN
   REQUIRE(op, "null op");
-  REQUIRE(kind == HH_PREC_NONE || kind == HH_PREC_JACOBI || kind == HH_PREC_SHIFTED_LAPLACE,
+  REQUIRE(kind == HH_PREC_NONE || kind == HH_PREC_JACOBI || kind == HH_PREC_SHIFTED_LAPLACE ||
+              is_sweep(kind),
           "unknown preconditioner kind %d", kind);
   if (kind == HH_PREC_SHIFTED_LAPLACE) {
     REQUIRE(sweeps >= 1 && sweeps <= 64, "sweeps must be in [1, 64]");
     REQUIRE(damping > 0, "damping must be positive");
+  }
+  if (is_sweep(kind)) {
+    // sequential in the layer index: no row-slab sharding (SURVEY 8e -> replicas only)
+    REQUIRE(op->ctx->world == 1 && op->slabs.size() == 1,
+            "the sweeping preconditioner needs the whole grid on one rank and one slab");
+    REQUIRE(op->b >= 1 && op->b < op->n, "sweeping needs 1 <= b < n (b = %d, n = %d)", op->b,
+            op->n);
+    REQUIRE(sweep_block(op->b) > 0, "sweeping supports b <= 16 (b = %d)", op->b);
+    if (!op->sw_P) {
+      HIPC(hipSetDevice(op->ctx->device));
+      const int n = op->n, b = op->b, B = sweep_block(b);
+      SweepArgs& a = op->sweep;
+      a.n = n;
+      a.b = b;
+      a.nsys = 1 + (n - b);
+      op->sw_P = dalloc<double2>((size_t)a.nsys * n * B * B);
+      a.ystride = sweep_scratch_per_wave(n);
+      op->sw_y = dalloc<double2>((size_t)std::max(1, a.nsys - 1) * a.ystride);
+      op->sw_uF = dalloc<double2>((size_t)b * n);
+      a.P = op->sw_P;
+      a.yscr = op->sw_y;
+      a.tab_i = op->tab_i;
+      a.tab_k = op->slabs[0].tab_j;      // layers 0..b-1: the local PML of every H_m
+      a.tab_glob = op->slabs[0].tab_j;
+      a.invc2 = op->const_c ? nullptr : op->slabs[0].invc2;
+      a.invc2_const = op->invc2_const;
+      a.stop = nullptr;
+      // algo2_3 (code.py:345-353): factor H_F and every H_m, all in parallel
+      launch_sweep(a, 0, nullptr, nullptr, 0, op->ctx->stream);
+      HIPC(hipGetLastError());
+      HIPC(hipStreamSynchronize(op->ctx->stream));
+    }
   }
   op->pkind = kind;
   op->beta = beta;
@@ -968,6 +1055,15 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     finish(0, 0, 0.0);
     return HH_OK;
   }
+  if (op->pkind == HH_PREC_SWEEP_REF) {
+    // run_solver's M (code.py:510-511, quirk Q1) is algo2_4 of the right-hand side f_vec,
+    // whatever GMRES passes it: compute that constant once
+    dfree(op->sw_const);
+    op->sw_const = nullptr;
+    double2* c = dalloc<double2>(L);
+    sweep_apply(op, b, c, true);
+    op->sw_const = c;
+  }
   // Mb_nrm2 = ||psolve(b)||; V[0] = M b, red[5] = |M b|^2 (= |M r|^2 while x0 == 0)
   apply_M(op, b, V);
   norm2(op, V, 5);
@@ -1052,6 +1148,8 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     rnorm = std::sqrt(st[0]);
     if (legacy && inner == maxiter) {
       finish(inner, rnorm <= atol ? 0 : (int)std::min<long>(maxiter, 0x7fffffff), rnorm);
+      dfree(op->sw_const);
+      op->sw_const = nullptr;
       return HH_OK;
     }
     if (rnorm <= atol) break;
@@ -1061,5 +1159,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     ptol = presid * std::min(ptol_max_factor, atol / rnorm);
   }
   finish(inner, rnorm <= atol ? 0 : (int)std::min<long>(maxiter, 0x7fffffff), rnorm);
+  dfree(op->sw_const);
+  op->sw_const = nullptr;
   GUARD_END
 }

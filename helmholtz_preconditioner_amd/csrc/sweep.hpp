@@ -1,0 +1,29 @@
+// Sweeping moving-PML preconditioner (sweep.hip) -- shared declarations.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+namespace hh {
+
+struct SweepArgs {
+  int n, b;            // grid size, PML width in layers (= sub-problem height)
+  int nsys;            // 1 (H_F) + (n - b) sub-problems H_m, m = b+1..n (1-based)
+  double2* P;          // [nsys][n][B][B] block-Thomas inverses Lambda_i^-1
+  const double2* tab_i;     // operator's per-column PML table [3][n]
+  const double2* tab_k;     // per-layer PML table of layers 0..b-1 (local PML of every H_m)
+  const double2* tab_glob;  // operator's per-layer table [n][4] (S/N couplings of the sweep)
+  const double* invc2;      // 1/c^2 [n][n] (row = layer) or nullptr
+  double invc2_const;
+  double2* yscr;       // per-wave solve scratch, ystride double2 each (sweep_scratch_per_wave)
+  size_t ystride;
+  const int* stop;     // GMRES cycle stop flag (kernels return at once when set)
+};
+
+int sweep_block(int b);
+size_t sweep_scratch_per_wave(int n);  // padded block size B (4, 8, 12, 16) or 0 if b > 16
+// what: 0 factor (one wave per system), 1 forward sweep, 2 middle sweep, 3 backward sweep
+void launch_sweep(const SweepArgs& a, int what, double2* u, double2* uF, int asis,
+                  hipStream_t st);
+
+}  // namespace hh

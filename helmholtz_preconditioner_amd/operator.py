@@ -248,3 +248,22 @@ class ShiftedLaplace(DevicePreconditioner):
 
     def __init__(self, A: DeviceOperator, beta=0.5, sweeps=4, damping=0.7):
         super().__init__(A, beta, sweeps, damping)
+
+
+class Sweeping(DevicePreconditioner):
+    """The reference's own preconditioner: the sweeping moving-PML preconditioner
+    (Engquist-Ying; algo2_3 / algo2_4, code.py:345-385), on the GPU.
+
+    * ``reference=False`` (default): Algorithm 2.4 with the reference's bugs fixed --
+      M x = sweep(x) (quirk Q1) and the middle sweep u_m = T_m u_m (quirk Q2).
+    * ``reference=True``: exactly what run_solver runs (code.py:510-511): inside ``gmres``
+      M x = algo2_4(b) for every x, middle sweep u_m -= T_m u_m.
+
+    Setup factors H_F and all n - b moving-PML sub-problems H_m (b = the PML width passed
+    to build_A_matrix) by block Thomas on the device.  Single rank, single slab only (the
+    sweep is sequential in the layer index).
+    """
+
+    def __init__(self, A: DeviceOperator, reference: bool = False):
+        self.kind = _ffi.HH_PREC_SWEEP_REF if reference else _ffi.HH_PREC_SWEEP
+        super().__init__(A)

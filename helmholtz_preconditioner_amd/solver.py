@@ -35,9 +35,9 @@ def _resolve_precond(A: DeviceOperator, M):
         M.configure()
         return
     raise TypeError(
-        "device gmres accepts M=None, 'jacobi', Jacobi(A) or ShiftedLaplace(A); an arbitrary "
-        "LinearOperator M (e.g. the reference's sweeping preconditioner) cannot run on the "
-        "device -- use scipy.sparse.linalg.gmres(A, b, M=M) with this DeviceOperator instead")
+        "device gmres accepts M=None, 'jacobi', Jacobi(A), ShiftedLaplace(A) or Sweeping(A); an "
+        "arbitrary host LinearOperator M cannot run on the device -- use "
+        "scipy.sparse.linalg.gmres(A, b, M=M) with this DeviceOperator instead")
 
 
 def gmres(A, b, x0=None, *, rtol=1e-5, atol=0., restart=None, maxiter=None, M=None,

@@ -43,8 +43,14 @@ typedef enum {
 typedef enum {
   HH_PREC_NONE = 0,            /* M = I                                          */
   HH_PREC_JACOBI = 1,          /* M = diag(A)^-1, fused into the stencil          */
-  HH_PREC_SHIFTED_LAPLACE = 2  /* M ~= A_beta^-1 by damped-Jacobi sweeps on the   */
+  HH_PREC_SHIFTED_LAPLACE = 2, /* M ~= A_beta^-1 by damped-Jacobi sweeps on the   */
                                /* shifted operator build_A_matrix(c/sqrt(1+i*b))  */
+  HH_PREC_SWEEP = 3,           /* sweeping moving-PML preconditioner, Engquist-Ying */
+                               /* Alg. 2.4 (algo2_3/algo2_4, code.py:345-385) with  */
+                               /* quirks Q1/Q2 corrected: M x = sweep(x)             */
+  HH_PREC_SWEEP_REF = 4        /* the reference as run_solver runs it: inside        */
+                               /* hh_gmres M x = algo2_4(b) for every x (Q1), middle  */
+                               /* sweep u -= T u (Q2); plain applies use algo2_4(x)   */
 } hh_precond_kind;
 
 /* Operator-apply modes for hh_op_apply*. */
@@ -110,7 +116,9 @@ int hh_op_destroy(hh_op* op);
 /* Layers owned by this rank: global 0-based [j_begin, j_end); local length =
  * (j_end - j_begin) * n complex values. */
 int hh_op_local_rows(hh_op* op, int* j_begin, int* j_end);
-/* Configure the preconditioner used by HH_APPLY_PREC* and hh_gmres. */
+/* Configure the preconditioner used by HH_APPLY_PREC* and hh_gmres.  The sweeping kinds
+ * factor every moving-PML sub-problem on the first call (algo2_3, code.py:345-353; b is the
+ * PML width given to hh_op_create) and need a single-rank, single-slab operator. */
 int hh_op_set_precond(hh_op* op, int kind, double beta, int sweeps, double damping);
 
 /* Host-buffer apply, the LinearOperator.matvec path (scipy _interface.py:227):

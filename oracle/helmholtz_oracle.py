@@ -242,3 +242,90 @@ def slab_apply_emulated(const, eta, omega, h, n, c_mat, x, bounds):
         y += N[j0:j1] * ext[2:] * (np.arange(j0, j1) < n - 1)[:, None]
         out.append(y)
     return np.vstack(out).ravel()
+
+
+# --------------------------------------------------------------------------
+# Sweeping moving-PML preconditioner: get_Hm_coeffs code.py:222-279,
+# get_Hm code.py:283-290, get_A_FF/Fb1/b1F code.py:177-199, algo2_3 code.py:345-353,
+# algo2_4 code.py:356-385.  SuperLU via scipy.sparse.linalg.splu as the reference.
+# --------------------------------------------------------------------------
+def s2m(x, m, b, const, eta, omega, h):
+    """Moving-PML stretch s2 shifted to the bottom of sub-domain m, code.py:35-37."""
+    return 1.0 / (1 + 1j * sigma2(np.asarray(x) - (m - b) * h, const, eta) / omega)
+
+
+def hm_matrix(m, b, const, eta, omega, h, n, c_mat):
+    """H_m (b n x b n) for 1-based m: layers j = m-b+1..m with the moving PML, code.py:222-290."""
+    I = np.arange(1, n + 1, dtype=np.float64)[None, :]
+    J = np.arange(m - b + 1, m + 1, dtype=np.float64)[:, None]
+    inv_h2 = 1 / h ** 2
+    sm = lambda x: s2m(x, m, b, const, eta, omega, h)  # noqa: E731
+    W = inv_h2 * (s1((I - .5) * h, const, eta, omega) / sm(J * h))
+    E = inv_h2 * (s1((I + .5) * h, const, eta, omega) / sm(J * h))
+    S = inv_h2 * (sm((J - .5) * h) / s1(I * h, const, eta, omega))
+    N = inv_h2 * (sm((J + .5) * h) / s1(I * h, const, eta, omega))
+    cc = np.asarray(c_mat)[:n, m - b:m].T           # c_mat[i-1, j-1], rows j
+    D = omega ** 2 / (s1(I * h, const, eta, omega) * sm(J * h) * cc ** 2) - (W + E + S + N)
+    bn = b * n
+    c1 = W.ravel()[1:].copy()
+    c2 = E.ravel()[:-1].copy()
+    c1[n - 1::n] = 0
+    c2[n - 1::n] = 0
+    A = scipy.sparse.diags([D.ravel(), c1, c2, S.ravel()[n:], N.ravel()[:-n]],
+                           [0, -1, 1, -n, n], shape=(bn, bn), format='csc')
+    return A
+
+
+class SweepState:
+    """algo2_3 setup + the coupling blocks run_solver prepares (code.py:496-507)."""
+
+    def __init__(self, b, const, eta, omega, h, n, c_mat):
+        self.b, self.n = b, n
+        W, E, S, N, D = stencil_coefficients(const, eta, omega, h, n, c_mat)
+        # A_FF = block_diag(A_11 .. A_bb): per-layer tridiagonals, no inter-layer blocks
+        blocks = []
+        for k in range(b):
+            blocks.append(scipy.sparse.diags([D[k], W[k, 1:], E[k, :-1]], [0, -1, 1]))
+        self.lu_HF = scipy.sparse.linalg.splu(scipy.sparse.block_diag(blocks, format='csc'))
+        self.lu_Hm = [scipy.sparse.linalg.splu(hm_matrix(m, b, const, eta, omega, h, n, c_mat))
+                      for m in range(b + 1, n + 1)]
+        self.S, self.N = S, N          # S[k]: A_{k+1,k} (0-based layers), N[k]: A_{k,k+1}
+
+    def T(self, m, v):
+        """lu_Hm.solve([0 .. 0, v])[-n:] for 1-based m."""
+        tmp = np.zeros(self.b * self.n, complex)
+        tmp[-self.n:] = v
+        return self.lu_Hm[m - self.b - 1].solve(tmp)[-self.n:]
+
+    def apply(self, f, corrected=False):
+        """algo2_4 applied to f (as-is: quirk Q2 in the middle sweep; corrected: u_m = T_m u_m)."""
+        b, n = self.b, self.n
+        u = np.array(np.asarray(f).reshape(n, n), dtype=complex)
+        TFuF = self.lu_HF.solve(u[:b].ravel())
+        u[b] = u[b] - self.S[b] * TFuF[-n:]
+        for m in range(b + 1, n):
+            u[m] = u[m] - self.S[m] * self.T(m, u[m - 1])
+        uF = TFuF
+        for m in range(b + 1, n + 1):
+            t = self.T(m, u[m - 1])
+            u[m - 1] = t if corrected else u[m - 1] - t
+        for m in range(n - 1, b, -1):
+            u[m - 1] = u[m - 1] - self.T(m, self.N[m - 1] * u[m])
+        Au = np.zeros(b * n, complex)
+        Au[-n:] = self.N[b - 1] * u[b]
+        uF = uF - self.lu_HF.solve(Au)
+        u[:b] = uF.reshape(b, n)
+        return u.ravel()
+
+
+def sweeping_preconditioner(b, const, eta, omega, h, n, c_mat, f=None, corrected=False):
+    """M for the gmres slot: as-is (code.py:510-511, quirk Q1) M x = algo2_4(f) for every x;
+    corrected: M x = algo2_4(x) with the Alg. 2.4 middle sweep."""
+    st = SweepState(b, const, eta, omega, h, n, c_mat)
+    NN = n * n
+    if corrected:
+        mv = lambda x: st.apply(np.ravel(x), corrected=True)  # noqa: E731
+    else:
+        fixed = st.apply(np.ravel(f))
+        mv = lambda x: fixed.copy()  # noqa: E731
+    return scipy.sparse.linalg.LinearOperator((NN, NN), matvec=mv, dtype=np.complex128), st

@@ -14,6 +14,11 @@ records the outputs of the reference's own functions:
                       callback_type='legacy') on the reference A (code.py:516;
                       ``tol=`` -> ``rtol=`` because scipy >= 1.14 removed it)
   shift_n64.npz       build_A_matrix with c_mat / sqrt(1 + 0.5i)  (shifted Laplace operator)
+  sweep_<case>.npz    the sweeping moving-PML preconditioner as the reference runs it:
+                      algo2_3 + algo2_4 (code.py:345-385) applied to f and to a random x
+                      (quirks Q1/Q2 included), two T_m = lu_Hm.solve([0..0, v])[-n:]
+                      probes, the CSR of one H_m (get_Hm, code.py:283-290), and scipy gmres
+                      with the reference's M (code.py:510-516)
 
 Only data is committed (inputs and expected outputs); no reference source.
 """
@@ -144,6 +149,45 @@ def main():
     A = ref.build_A_matrix(b, C, eta, om, h, n, cm)
     np.savez_compressed(os.path.join(HERE, 'shift_n64.npz'), n=n, b=b, C=C, omega=om, h=h,
                         eta=eta, beta=0.5, medium='c1', **csr_arrays(A))
+    # F1: the sweeping moving-PML preconditioner (algo2_3 / algo2_4, code.py:345-385), as-is
+    # (including quirks Q1/Q2), on the reference's own blocks (run_solver code.py:496-511)
+    for name, n, med, b, C, wn, al in (('n48_c1', 48, 'c1', 12, 81.0, 4.0, 2.0),
+                                       ('n37_c2', 37, 'c2', 6, 61.0, 3.0, 2.0)):
+        om, h, eta = params(n, b, wn, al)
+        cm = medium(ref, med, n)
+        A = ref.build_A_matrix(b, C, eta, om, h, n, cm).tocsr()
+        f = ref.init_f1_mat(.5, .125, om, n).flatten()
+        lu_HF, lu_Hm_ra = ref.algo2_3(b, C, eta, om, h, n, cm)
+        A_b1F = ref.get_A_b1F_block(b, C, eta, om, h, n, cm)
+        A_Fb1 = ref.get_A_Fb1_block(b, C, eta, om, h, n, cm)
+        up, lo = [], []
+        for i in range(1, n):
+            up.append(ref.get_A_block(i, i + 1, b, C, eta, om, h, n, cm))
+            lo.append(ref.get_A_block(i + 1, i, b, C, eta, om, h, n, cm))
+        u_f = ref.algo2_4(f, b, n, lu_HF, A_b1F, A_Fb1, up, lo, lu_Hm_ra)
+        x = rand_complex(n * n, 3)
+        u_x = ref.algo2_4(x, b, n, lu_HF, A_b1F, A_Fb1, up, lo, lu_Hm_ra)
+        # T_m blocks for two m (1-based): last-layer block of Hm^-1 applied to unit-ish v
+        v = rand_complex(n, 4)
+        T = {}
+        for m in (b + 1, n):
+            tmp = np.zeros(b * n, complex)
+            tmp[-n:] = v
+            T[f'T_{m}'] = lu_Hm_ra[m - b - 1].solve(tmp)[-n:]
+        Hm = ref.get_Hm(b + 3, b, C, eta, om, h, n, cm).tocsr()
+        Hm.sort_indices()
+        M = scipy.sparse.linalg.LinearOperator(A.shape, matvec=lambda xx: ref.algo2_4(
+            f, b, n, lu_HF, A_b1F, A_Fb1, up, lo, lu_Hm_ra), dtype=np.complex128)
+        hist = []
+        xs, info = scipy.sparse.linalg.gmres(A, f, M=M, rtol=1e-3, callback=hist.append,
+                                             callback_type='legacy')
+        np.savez_compressed(os.path.join(HERE, f'sweep_{name}.npz'), n=n, b=b, C=C, omega=om,
+                            h=h, eta=eta, medium=med, u_f=u_f.ravel(), u_x=u_x.ravel(), v=v,
+                            Hm_m=b + 3, Hm_data=Hm.data, Hm_indices=Hm.indices.astype(np.int32),
+                            Hm_indptr=Hm.indptr.astype(np.int64), gmres_hist=np.array(hist),
+                            gmres_info=info, gmres_x=xs, **T)
+        print('sweep', name, 'gmres callbacks', len(hist), 'info', info,
+              'max|u|', np.abs(u_f).max())
     with open(os.path.join(HERE, 'VERSIONS.txt'), 'w') as fh:
         fh.write(f"generated from /root/reference/code.py with scipy {meta['scipy']} "
                  f"numpy {meta['numpy']} (numba absent: identity jit stub)\n")

@@ -1,0 +1,101 @@
+"""GPU tier, SURVEY row F1: the sweeping moving-PML preconditioner (algo2_3 / algo2_4,
+code.py:345-385) on the device (csrc/sweep.hip, block Thomas instead of SuperLU).
+
+* as-is (the reference's run, quirks Q1/Q2) against golden vectors produced by the
+  reference's own algo2_4 (tests/golden/sweep_*.npz): 1e-10 relative;
+* corrected (Alg. 2.4) against the oracle's SuperLU restatement: apply 1e-10, GMRES
+  history / field 1e-6 (contract).
+"""
+import numpy as np
+import pytest
+
+import helmholtz_preconditioner_amd as H
+from conftest import load_golden, medium, rand_complex
+from oracle import helmholtz_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = H.Context(device=0)
+    H.set_default_context(c)
+    yield c
+    H.set_default_context(None)
+
+
+def relerr(a, b):
+    return np.linalg.norm(a - b) / np.linalg.norm(b)
+
+
+def _case(z, ctx):
+    n, b = int(z["n"]), int(z["b"])
+    om, C, h, eta = complex(z["omega"]), float(z["C"]), float(z["h"]), float(z["eta"])
+    cm = medium(str(z["medium"]), n)
+    A = H.build_A_matrix(b, C, eta, om, h, n, cm, context=ctx)
+    return A, (b, C, eta, om, h, n, cm)
+
+
+@pytest.mark.parametrize("name", ["sweep_n48_c1.npz", "sweep_n37_c2.npz"])
+def test_sweep_as_is_matches_reference(ctx, name):
+    z = load_golden(name)
+    A, (b, C, eta, om, h, n, cm) = _case(z, ctx)
+    M = H.Sweeping(A, reference=True)
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    assert relerr(M @ f, z["u_f"]) < 1e-10
+    assert relerr(M @ rand_complex(n * n, 3), z["u_x"]) < 1e-10
+
+
+@pytest.mark.parametrize("name", ["sweep_n48_c1.npz", "sweep_n37_c2.npz"])
+def test_sweep_corrected_matches_oracle(ctx, name):
+    z = load_golden(name)
+    A, (b, C, eta, om, h, n, cm) = _case(z, ctx)
+    st = O.SweepState(b, C, eta, om, h, n, cm)
+    M = H.Sweeping(A)
+    for seed in (0, 1):
+        x = rand_complex(n * n, seed)
+        assert relerr(M @ x, st.apply(x, corrected=True)) < 1e-10
+
+
+@pytest.mark.parametrize("n,b,kind", [(96, 12, "c1"), (130, 8, "const"), (200, 16, "c2"),
+                                      (61, 5, "c1")])
+def test_sweep_sizes_vs_oracle(ctx, n, b, kind):
+    om, h, eta = O.problem_params(n, b, 5.0, 2.0)
+    cm = medium(kind, n)
+    A = H.build_A_matrix(b, 81.0, eta, om, h, n, cm, context=ctx)
+    st = O.SweepState(b, 81.0, eta, om, h, n, cm)
+    x = rand_complex(n * n, n)
+    assert relerr(H.Sweeping(A) @ x, st.apply(x, corrected=True)) < 1e-10
+    assert relerr(H.Sweeping(A, reference=True) @ x, st.apply(x)) < 1e-10
+
+
+@pytest.mark.parametrize("name", ["sweep_n48_c1.npz", "sweep_n37_c2.npz"])
+def test_gmres_corrected_sweeping_vs_oracle(ctx, name):
+    z = load_golden(name)
+    A, (b, C, eta, om, h, n, cm) = _case(z, ctx)
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    Aref = O.build_A_matrix(b, C, eta, om, h, n, cm)
+    Mref, _ = O.sweeping_preconditioner(b, C, eta, om, h, n, cm, corrected=True)
+    xr, infor, histr, relr = O.gmres_reference(Aref, f, M=Mref, rtol=1e-3, restart=20, maxiter=200)
+    x, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=200, M=H.Sweeping(A),
+                            callback=lambda r: None, callback_type="legacy", return_history=True)
+    assert info == infor == 0 and len(hist) == len(histr)
+    assert np.max(np.abs(hist - histr) / histr) < 1e-6
+    assert relerr(x, xr) < 1e-6
+
+
+@pytest.mark.parametrize("name", ["sweep_n48_c1.npz", "sweep_n37_c2.npz"])
+def test_gmres_reference_run_as_is(ctx, name):
+    """the reference's own solve (code.py:516 with M of code.py:510): M is a constant map, so
+    every cycle's Krylov space is one-dimensional and GMRES sits ON scipy's breakdown test
+    h1 <= eps*h0 (iterative.py:767) -- h1 is the rounding residue of c - <v0,c> v0, so how
+    many cycles run before the test fires (1..3 here) is decided by rounding noise, not by
+    the algorithm.  What is reproducible: info == maxiter (not converged) and a ~0 history."""
+    z = load_golden(name)
+    A, (b, C, eta, om, h, n, cm) = _case(z, ctx)
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    x, info, hist = H.gmres(A, f, rtol=1e-3, M=H.Sweeping(A, reference=True),
+                            callback=lambda r: None, callback_type="legacy", return_history=True)
+    assert info == int(z["gmres_info"])
+    assert 1 <= len(hist) <= 3 and 1 <= len(z["gmres_hist"]) <= 3
+    assert np.all(np.abs(hist) < 1e-12)  # the reference's presid history is ~0 (breakdown)
