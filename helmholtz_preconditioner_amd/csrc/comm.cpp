@@ -149,12 +149,17 @@ class ShmComm final : public Comm {
   void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi, size_t bytes,
             hipStream_t compute, hipStream_t, hipEvent_t) override {
     REQUIRE(bytes <= kShmHaloBytes, "shm halo row too large (n > 65536)");
+    // Every copy is ordered on `compute` and completed before the barrier that releases the
+    // peers: a plain hipMemcpy from pageable (shm) memory may return before its DMA has
+    // landed, and the boundary-row kernels on the non-blocking compute stream would not
+    // wait for it; a peer may also refill its slot as soon as the second barrier passes.
+    if (send_lo) HIPC(hipMemcpyAsync(slot(rank, 0), send_lo, bytes, hipMemcpyDeviceToHost, compute));
+    if (send_hi) HIPC(hipMemcpyAsync(slot(rank, 1), send_hi, bytes, hipMemcpyDeviceToHost, compute));
     HIPC(hipStreamSynchronize(compute));
-    if (send_lo) HIPC(hipMemcpy(slot(rank, 0), send_lo, bytes, hipMemcpyDeviceToHost));
-    if (send_hi) HIPC(hipMemcpy(slot(rank, 1), send_hi, bytes, hipMemcpyDeviceToHost));
     barrier();
-    if (recv_lo) HIPC(hipMemcpy(recv_lo, slot(rank - 1, 1), bytes, hipMemcpyHostToDevice));
-    if (recv_hi) HIPC(hipMemcpy(recv_hi, slot(rank + 1, 0), bytes, hipMemcpyHostToDevice));
+    if (recv_lo) HIPC(hipMemcpyAsync(recv_lo, slot(rank - 1, 1), bytes, hipMemcpyHostToDevice, compute));
+    if (recv_hi) HIPC(hipMemcpyAsync(recv_hi, slot(rank + 1, 0), bytes, hipMemcpyHostToDevice, compute));
+    HIPC(hipStreamSynchronize(compute));
     barrier();
   }
 
