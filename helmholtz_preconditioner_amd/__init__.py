@@ -20,6 +20,9 @@ from .media import (constant_c_mat, init_c1_f1, init_c1_f2, init_c1_mat, init_c2
 from .operator import (DeviceOperator, DevicePreconditioner, DeviceVector, Jacobi,  # noqa: F401
                        ShiftedLaplace, Sweeping, build_A_matrix)
 from .solver import gmres  # noqa: F401
+from .driver import gmres_counter, run_solver, true_relative_residual  # noqa: F401
+from .io import (load_c_mat, load_solution, load_velocity_model, plot_solution,  # noqa: F401
+                 resample_velocity, save_c_mat, save_solution, solution_image)
 from . import dist  # noqa: F401
 
 __all__ = [
@@ -28,5 +31,7 @@ __all__ = [
     "Context", "default_context", "set_default_context", "device_count", "unique_id",
     "init_c1_mat", "init_c2_mat", "init_f1_mat", "init_f2_mat", "init_c1_f1", "init_c1_f2",
     "init_c2_f1", "init_c2_f2", "constant_c_mat", "marmousi_like_c_mat", "problem_params",
-    "HHError",
+    "HHError", "run_solver", "gmres_counter", "true_relative_residual",
+    "load_c_mat", "save_c_mat", "load_velocity_model", "resample_velocity", "save_solution",
+    "load_solution", "solution_image", "plot_solution",
 ]

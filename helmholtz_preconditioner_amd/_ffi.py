@@ -59,6 +59,8 @@ SIGNATURES = [
     ("hh_op_set_precond", c_int, [c_void_p, c_int, c_double, c_int, c_double]),
     ("hh_op_apply", c_int, [c_void_p, c_dp, c_dp, c_int]),
     ("hh_op_diagonal", c_int, [c_void_p, c_dp]),
+    ("hh_op_csr_nnz", c_int, [c_void_p, ctypes.POINTER(ctypes.c_int64)]),
+    ("hh_op_export_csr", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_dp, c_dp]),
     ("hh_vec_create", c_int, [c_void_p, PP]),
     ("hh_vec_destroy", c_int, [c_void_p]),
     ("hh_vec_upload", c_int, [c_void_p, c_dp]),

@@ -79,6 +79,24 @@ struct PointArgs {
   const int* stop;         // as StencilArgs::stop
 };
 
+// CSR export of one slab (assemble.hip).
+struct CsrArgs {
+  const double2* tab_i;    // as StencilArgs
+  const double2* tab_j;    // this slab's [nl][4]
+  const double* invc2;     // this slab's [nl][n], or nullptr
+  double invc2_const;
+  int n, nl;
+  int j0;                  // global first layer of the slab
+  int rank_j0;             // global first layer of the rank (indptr origin)
+  size_t row_off;          // local row offset of the slab inside the rank
+  int last;                // 1: also write indptr[row_off + nl n]
+  long long* indptr;       // [local rows + 1], relative to the rank's first entry
+  void* indices;           // int32 or int64 global column indices
+  double2* data;
+};
+long long csr_rank_nnz(int n, int j0, int j1);
+void launch_csr_export(const CsrArgs& a, int index_bytes, hipStream_t stream);
+
 // Kernel launchers (kernels.hip).  All are asynchronous on `stream`.
 void launch_stencil(int epi, bool const_c, const StencilArgs& a, int nblocks_out[1],
                     hipStream_t stream, int variant = -1);

@@ -826,6 +826,78 @@ HH_API int hh_op_diagonal(hh_op* op, double* d) {
   GUARD_END
 }
 
+// ------------------------------------------------------------- CSR export (F2)
+HH_API int hh_op_csr_nnz(hh_op* op, int64_t* nnz) {
+  GUARD_BEGIN
+  REQUIRE(op && nnz, "null argument");
+  *nnz = csr_rank_nnz(op->n, op->jb, op->je);
+  GUARD_END
+}
+
+HH_API int hh_op_export_csr(hh_op* op, int64_t* indptr, void* indices, int index_bytes,
+                            double* data, double* kernel_ms) {
+  GUARD_BEGIN
+  REQUIRE(op && indptr && indices && data, "null argument");
+  REQUIRE(index_bytes == 4 || index_bytes == 8, "index_bytes must be 4 or 8");
+  REQUIRE(index_bytes == 8 || (long long)op->n * op->n < (1LL << 31),
+          "n^2 >= 2^31: int32 column indices overflow (use index_bytes = 8)");
+  HIPC(hipSetDevice(op->ctx->device));
+  hipStream_t s = op->ctx->stream;
+  const long long nnz = csr_rank_nnz(op->n, op->jb, op->je);
+  const size_t rows = op->nloc;
+  long long* d_ptr = dalloc<long long>(rows + 1);
+  void* d_idx = nullptr;
+  double2* d_val = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  try {
+    d_idx = dalloc<char>((size_t)nnz * index_bytes);
+    d_val = dalloc<double2>((size_t)nnz);
+    HIPC(hipEventCreate(&e0));
+    HIPC(hipEventCreate(&e1));
+    HIPC(hipEventRecord(e0, s));
+    for (size_t si = 0; si < op->slabs.size(); ++si) {
+      const Slab& sl = op->slabs[si];
+      CsrArgs a{};
+      a.tab_i = op->tab_i;
+      a.tab_j = sl.tab_j;
+      a.invc2 = op->const_c ? nullptr : sl.invc2;
+      a.invc2_const = op->invc2_const;
+      a.n = op->n;
+      a.nl = sl.nl;
+      a.j0 = sl.j0;
+      a.rank_j0 = op->jb;
+      a.row_off = sl.off;
+      a.last = si + 1 == op->slabs.size();
+      a.indptr = d_ptr;
+      a.indices = d_idx;
+      a.data = d_val;
+      if (sl.nl > 0) launch_csr_export(a, index_bytes, s);
+    }
+    HIPC(hipGetLastError());
+    HIPC(hipEventRecord(e1, s));
+    HIPC(hipMemcpyAsync(indptr, d_ptr, (rows + 1) * sizeof(long long), hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(indices, d_idx, (size_t)nnz * index_bytes, hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(data, d_val, (size_t)nnz * sizeof(double2), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, e0, e1));
+    if (kernel_ms) *kernel_ms = ms;
+  } catch (...) {
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    dfree(d_ptr);
+    dfree(d_idx);
+    dfree(d_val);
+    throw;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  dfree(d_ptr);
+  dfree(d_idx);
+  dfree(d_val);
+  GUARD_END
+}
+
 // ------------------------------------------------------------------ vectors
 HH_API int hh_vec_create(hh_op* op, hh_vec** v) {
   GUARD_BEGIN

@@ -170,6 +170,43 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
         check(lib.hh_op_diagonal(self.handle, _ffi.dptr(d)))
         return d
 
+    @property
+    def csr_nnz(self) -> int:
+        """Entries of this rank's rows in the assembled matrix (5 n^2 - 4 n on one rank)."""
+        v = ctypes.c_int64()
+        check(lib.hh_op_csr_nnz(self.handle, ctypes.byref(v)))
+        return v.value
+
+    def to_csr(self, index_dtype=None, return_kernel_ms: bool = False):
+        """The scipy CSR matrix ``build_A_matrix`` returns (code.py:202-219), assembled on the
+        device from the coefficients the stencil applies.
+
+        One rank: the full N x N matrix, structurally identical to the reference's (canonical
+        CSR, sorted columns S, W, D, E, N per row).  Several ranks: this rank's rows with
+        global column indices, shape (local, N).  ``index_dtype`` defaults to int32 when
+        N < 2^31 (scipy's choice), else int64.
+        """
+        import scipy.sparse
+        N = self.n * self.n
+        if index_dtype is None:
+            index_dtype = np.int32 if N < 2 ** 31 else np.int64
+        index_dtype = np.dtype(index_dtype)
+        if index_dtype not in (np.dtype(np.int32), np.dtype(np.int64)):
+            raise ValueError("index_dtype must be int32 or int64")
+        nnz = self.csr_nnz
+        indptr = np.empty(self.local_size + 1, dtype=np.int64)
+        indices = np.empty(nnz, dtype=index_dtype)
+        data = np.empty(nnz, dtype=np.complex128)
+        ms = ctypes.c_double()
+        check(lib.hh_op_export_csr(self.handle, indptr.ctypes.data_as(ctypes.c_void_p),
+                                   indices.ctypes.data_as(ctypes.c_void_p), index_dtype.itemsize,
+                                   _ffi.dptr(data), ctypes.byref(ms)))
+        if index_dtype == np.dtype(np.int32):
+            indptr = indptr.astype(np.int32)
+        A = scipy.sparse.csr_matrix((data, indices, indptr), shape=(self.local_size, N))
+        A.has_sorted_indices = True
+        return (A, ms.value) if return_kernel_ms else A
+
     def apply_device(self, x: DeviceVector, y: DeviceVector, mode: int = _ffi.HH_APPLY_A):
         check(lib.hh_op_apply_dev(self.handle, x.handle, y.handle, int(mode)))
 

@@ -128,6 +128,20 @@ int hh_op_apply(hh_op* op, const double* x, double* y, int mode);
 /* diag(A) of the local slab (A.diagonal()), 2*len doubles. */
 int hh_op_diagonal(hh_op* op, double* d);
 
+/* Operator export: the CSR matrix build_A_matrix returns (code.py:202-219,
+ * canonical scipy CSR: per row S, W, D, E, N in column order, nnz = 5n^2 - 4n), restricted
+ * to this rank's rows, with global column indices.  Written on the device from the same
+ * tables the stencil applies (the exported values are the applied operator, bit for bit),
+ * then copied to the caller's host arrays.
+ *   nnz:      entries in this rank's rows (hh_op_csr_nnz).
+ *   indptr:   local rows + 1 int64 offsets (indptr[0] = 0).
+ *   indices:  nnz column indices, int32 (index_bytes 4; needs n^2 < 2^31) or int64 (8).
+ *   data:     2*nnz doubles (interleaved complex).
+ *   kernel_ms (optional): duration of the device export kernels. */
+int hh_op_csr_nnz(hh_op* op, int64_t* nnz);
+int hh_op_export_csr(hh_op* op, int64_t* indptr, void* indices, int index_bytes, double* data,
+                     double* kernel_ms);
+
 /* ------------------------------------------------------------ device vecs */
 int hh_vec_create(hh_op* op, hh_vec** v);
 int hh_vec_destroy(hh_vec* v);
