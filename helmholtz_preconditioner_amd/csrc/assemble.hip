@@ -8,7 +8,7 @@
 // a neighbour outside the grid has no entry (its coefficient still enters D).
 // nnz(A) = 5 n^2 - 4 n.
 //
-// One thread per row.  The row start is closed-form (no scan): with
+// One thread per row (staged through LDS, see the kernel).  The row start is closed-form (no scan): with
 //   rownnz(i, j) = 1 + [i>0] + [i<n-1] + [j>0] + [j<n-1],
 // the entries before global layer j are j (3n-2) + n (max(j-1, 0) + min(j, n-1)) and the
 // entries before column i inside layer j are i (1 + [j>0] + [j<n-1]) + max(i-1, 0) + min(i, n-1).
@@ -26,38 +26,66 @@ __device__ __forceinline__ long long layer_start(long long n, long long j) {
   return j * (3 * n - 2) + n * ((j > 0 ? j - 1 : 0) + (j < n - 1 ? j : n - 1));
 }
 
+// A block owns 256 consecutive rows, whose entries are one contiguous range of the output:
+// every thread stages its row's <= 5 entries in LDS at (row start - block start), then the
+// block writes the range out with consecutive lanes on consecutive entries (coalesced
+// 16-B value / 4- or 8-B index stores; a thread's own entries would be 80 B apart per lane).
+constexpr int kCsrRows = 256;
+constexpr int kCsrMax = 5 * kCsrRows;
+
 template <class IDX>
-__global__ __launch_bounds__(256) void csr_export_kernel(const CsrArgs a, IDX* indices) {
+__global__ __launch_bounds__(kCsrRows) void csr_export_kernel(const CsrArgs a, IDX* indices) {
+  __shared__ double2 sval[kCsrMax];
+  __shared__ IDX sidx[kCsrMax];
+  __shared__ long long sfirst, send;
   const long long n = a.n;
   const long long base = layer_start(n, a.rank_j0);  // first entry of this rank's rows
   const size_t len = (size_t)a.nl * a.n;
-  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < len;
-       t += (size_t)gridDim.x * blockDim.x) {
-    const int jl = (int)(t / a.n);
-    const int i = (int)(t % a.n);
+  const size_t nblk = (len + kCsrRows - 1) / kCsrRows;
+  for (size_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {  // uniform per block
+    const size_t t = blk * kCsrRows + threadIdx.x;
+    const bool live = t < len;
+    const size_t tc = live ? t : len - 1;
+    const int jl = (int)(tc / a.n);
+    const int i = (int)(tc % a.n);
     const long long j = a.j0 + jl;  // global layer
     const int up = j > 0, dn = j < n - 1;
     const long long start = layer_start(n, j) + (long long)i * (1 + up + dn) +
                             (i > 0 ? i - 1 : 0) + (i < n - 1 ? i : n - 1) - base;
+    const int cnt = 1 + up + dn + (i > 0) + (i < n - 1);
+    if (threadIdx.x == 0) sfirst = start;
+    if (live && (threadIdx.x == kCsrRows - 1 || t == len - 1)) send = start + cnt;
+    __syncthreads();
     const double2* tj = a.tab_j + 4 * jl;
     const double2 R2 = tj[0], BS = tj[1], BN = tj[2], OM = tj[3];
     const double2 AW = a.tab_i[i], AE = a.tab_i[n + i], R1 = a.tab_i[2 * n + i];
-    const double ic = a.invc2 ? a.invc2[t] : a.invc2_const;
+    const double ic = a.invc2 ? a.invc2[tc] : a.invc2_const;
     const double2 W = cmul(AW, R2);
     const double2 E = cmul(AE, R2);
     const double2 S = cmul(BS, R1);
     const double2 N = cmul(BN, R1);
     const double2 M = cscale(cmul(OM, R1), ic);
     const double2 D = csub(M, cadd(cadd(cadd(W, E), S), N));
-    const long long p = j * n + i;  // global row = global diagonal column
-    long long q = start;
-    if (up) { a.data[q] = S; indices[q] = (IDX)(p - n); ++q; }
-    if (i > 0) { a.data[q] = W; indices[q] = (IDX)(p - 1); ++q; }
-    a.data[q] = D; indices[q] = (IDX)p; ++q;
-    if (i < n - 1) { a.data[q] = E; indices[q] = (IDX)(p + 1); ++q; }
-    if (dn) { a.data[q] = N; indices[q] = (IDX)(p + n); ++q; }
-    a.indptr[a.row_off + t] = start;
-    if (a.last && t == len - 1) a.indptr[a.row_off + len] = q;
+    if (live) {
+      const long long p = j * n + i;  // global row = global diagonal column
+      int q = (int)(start - sfirst);
+      if (up) { sval[q] = S; sidx[q] = (IDX)(p - n); ++q; }
+      if (i > 0) { sval[q] = W; sidx[q] = (IDX)(p - 1); ++q; }
+      sval[q] = D; sidx[q] = (IDX)p; ++q;
+      if (i < n - 1) { sval[q] = E; sidx[q] = (IDX)(p + 1); ++q; }
+      if (dn) { sval[q] = N; sidx[q] = (IDX)(p + n); }
+      a.indptr[a.row_off + t] = start;
+      if (a.last && t == len - 1) a.indptr[a.row_off + len] = start + cnt;
+    }
+    __syncthreads();
+    const long long first = sfirst;
+    const int total = (int)(send - first);
+    for (int k = threadIdx.x; k < total; k += kCsrRows) {
+      __builtin_nontemporal_store(sval[k].x, &a.data[first + k].x);
+      __builtin_nontemporal_store(sval[k].y, &a.data[first + k].y);
+      indices[first + k] = sidx[k];
+    }
+    __syncthreads();  // LDS reuse by the next row block
   }
 }
 
@@ -73,7 +101,7 @@ long long csr_rank_nnz(int n, int j0, int j1) {
 
 void launch_csr_export(const CsrArgs& a, int index_bytes, hipStream_t stream) {
   const size_t len = (size_t)a.nl * a.n;
-  const int blocks = (int)std::min<size_t>((len + 255) / 256, 8192);
+  const int blocks = (int)std::min<size_t>((len + kCsrRows - 1) / kCsrRows, 16384);
   if (index_bytes == 8)
     hipLaunchKernelGGL(csr_export_kernel<long long>, dim3(blocks), dim3(256), 0, stream, a,
                        static_cast<long long*>(a.indices));

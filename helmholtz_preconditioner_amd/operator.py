@@ -203,7 +203,10 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
                                    _ffi.dptr(data), ctypes.byref(ms)))
         if index_dtype == np.dtype(np.int32):
             indptr = indptr.astype(np.int32)
-        A = scipy.sparse.csr_matrix((data, indices, indptr), shape=(self.local_size, N))
+        A = scipy.sparse.csr_matrix((data, indices, indptr), shape=(self.local_size, N),
+                                    copy=False)
+        if A.indices.dtype != index_dtype:  # scipy downcasts small matrices: keep the request
+            A.indices, A.indptr = indices, indptr
         A.has_sorted_indices = True
         return (A, ms.value) if return_kernel_ms else A
 
