@@ -67,6 +67,7 @@ static double2 d2(cd z) { return make_double2(z.real(), z.imag()); }
 using namespace hh;
 
 struct hh_ctx {
+  int refs = 1;  // the caller's handle + one per live operator (freed at zero)
   int device = 0, rank = 0, world = 1, vslabs = 1, transport = 0;
   std::unique_ptr<hh::Comm> comm;  // null at world == 1
   hipStream_t stream = nullptr;   // compute
@@ -89,6 +90,7 @@ struct Slab {
 }  // namespace
 
 struct hh_op {
+  int refs = 1;  // the caller's handle + one per live vector (freed at zero)
   hh_ctx* ctx = nullptr;
   int n = 0, b = 0;
   double C = 0, eta = 0, h = 0;
@@ -132,6 +134,9 @@ struct hh_op {
   double2* sw_y = nullptr;
   double2* sw_uF = nullptr;
   double2* sw_const = nullptr;  // as-is (quirk Q1): M x = algo2_4(b) for every x
+  double2* sw_T = nullptr;      // dense transfer matrices (sweep_dense.hip), or null
+  double2* sw_u = nullptr;      // dense apply scratch (n^2)
+  int sw_mode = -1;             // -1 auto, 0 block-Thomas solves, 1 dense transfer matrices
   // tuning (hh_op_tune): stencil variant for the plain apply, rows per block override
   int variant = -1;
   int rpb_override = 0;
@@ -302,6 +307,13 @@ bool is_sweep(int kind) { return kind == HH_PREC_SWEEP || kind == HH_PREC_SWEEP_
 // corrected: u = T u), backward sweeps.  r and out must differ.
 void sweep_apply(hh_op* op, const double2* r, double2* out, bool asis) {
   hipStream_t s = op->ctx->stream;
+  if (op->sw_T) {
+    SweepArgs a = op->sweep;
+    a.stop = op->stop_flag;
+    launch_sweep_dense_apply(a, op->sw_T, r, out, op->sw_u, asis ? 1 : 0, s);
+    HIPC(hipGetLastError());
+    return;
+  }
   launch_scale_copy(r, out, op->nloc, 1.0, s, op->stop_flag);
   SweepArgs a = op->sweep;
   a.stop = op->stop_flag;
@@ -522,9 +534,11 @@ HH_API int hh_ctx_create(int device, int rank, int world, const unsigned char* n
   return hh_ctx_create_ex(device, rank, world, nccl_id, virtual_slabs, TRANSPORT_RCCL, out);
 }
 
-HH_API int hh_ctx_destroy(hh_ctx* c) {
-  GUARD_BEGIN
-  if (!c) return HH_OK;
+// Lifetimes: hh_*_destroy releases the caller's handle; an object is freed when its last
+// dependent is gone too (a context outlives its operators, an operator its vectors), so no
+// destroy order -- e.g. a garbage collector's -- can leave a dangling context or operator.
+static void ctx_release(hh_ctx* c) {
+  if (--c->refs > 0) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   c->comm.reset();
@@ -534,7 +548,14 @@ HH_API int hh_ctx_destroy(hh_ctx* c) {
   (void)hipStreamDestroy(c->cstream);
   dfree(c->dscratch);
   if (c->hpinned) (void)hipHostFree(c->hpinned);
+  (void)hipGetLastError();  // teardown errors are not reported to a later call
   delete c;
+}
+
+HH_API int hh_ctx_destroy(hh_ctx* c) {
+  GUARD_BEGIN
+  if (!c) return HH_OK;
+  ctx_release(c);
   GUARD_END
 }
 
@@ -690,13 +711,14 @@ HH_API int hh_op_create(hh_ctx* c, int n, int b, double cconst, double eta, doub
     delete op;  // device memory of a failed create is reclaimed at process exit
     throw;
   }
+  c->refs++;  // the operator keeps its context alive
   *out = op;
   GUARD_END
 }
 
-HH_API int hh_op_destroy(hh_op* op) {
-  GUARD_BEGIN
-  if (!op) return HH_OK;
+static void op_release(hh_op* op) {
+  if (--op->refs > 0) return;
+  hh_ctx* c = op->ctx;
   (void)hipSetDevice(op->ctx->device);
   (void)hipStreamSynchronize(op->ctx->stream);
   for (Slab& s : op->slabs) {
@@ -721,8 +743,18 @@ HH_API int hh_op_destroy(hh_op* op) {
   dfree(op->sw_y);
   dfree(op->sw_uF);
   dfree(op->sw_const);
+  dfree(op->sw_T);
+  dfree(op->sw_u);
   if (op->status_h) (void)hipHostFree(op->status_h);
+  (void)hipGetLastError();
   delete op;
+  ctx_release(c);
+}
+
+HH_API int hh_op_destroy(hh_op* op) {
+  GUARD_BEGIN
+  if (!op) return HH_OK;
+  op_release(op);
   GUARD_END
 }
 
@@ -732,6 +764,53 @@ HH_API int hh_op_local_rows(hh_op* op, int* j_begin, int* j_end) {
   *j_begin = op->jb;
   *j_end = op->je;
   GUARD_END
+}
+
+// Dense-transfer form of the sweeping preconditioner (sweep_dense.hip): decide, allocate, form.
+static void sweep_dense_configure(hh_op* op) {
+  const int n = op->n, b = op->b;
+  if (op->sw_mode == 0) {
+    dfree(op->sw_T);
+    dfree(op->sw_u);
+    op->sw_T = op->sw_u = nullptr;
+    return;
+  }
+  if (op->sw_T) return;
+  size_t free_b = 0, total_b = 0;
+  HIPC(hipMemGetInfo(&free_b, &total_b));
+  const size_t tbytes = sweep_dense_bytes(n);
+  const size_t blk = sweep_dense_scratch_per_block(n, b) * sizeof(double2);
+  const int chunks = sweep_dense_chunks(n);
+  const bool fits = tbytes + (size_t)chunks * blk + (size_t)n * n * 16 < free_b / 10 * 7;
+  if (op->sw_mode < 0 && (n > 2048 || !fits)) return;  // auto: keep the block-Thomas solves
+  REQUIRE(fits, "dense sweeping needs %.1f GB for n = %d (%.1f GB free)", tbytes / 1e9, n,
+          free_b / 1e9);
+  REQUIRE(n <= 2048, "dense sweeping supports n <= 2048 (n = %d)", n);
+  hipStream_t s = op->ctx->stream;
+  op->sw_T = dalloc<double2>(tbytes / sizeof(double2));
+  double2* scr = nullptr;
+  try {
+    op->sw_u = dalloc<double2>((size_t)n * n);
+    HIPC(hipMemset(op->sw_u, 0, (size_t)n * n * sizeof(double2)));
+    // concurrency: ~1024 setup blocks, within a scratch budget of the remaining memory
+    const size_t left = free_b - tbytes - (size_t)n * n * 16;
+    const size_t budget = std::min(left / 4, (size_t)32 << 30);
+    const int nsys = op->sweep.nsys;
+    int batch = std::max(1, std::min(nsys, 1024 / chunks));
+    while (batch > 1 && (size_t)batch * chunks * blk > budget) batch /= 2;
+    scr = dalloc<double2>((size_t)batch * chunks * blk / sizeof(double2));
+    for (int s0 = 0; s0 < nsys; s0 += batch)
+      launch_sweep_dense_setup(op->sweep, s0, std::min(batch, nsys - s0), scr, op->sw_T, s);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(s));
+  } catch (...) {
+    dfree(scr);
+    dfree(op->sw_T);
+    dfree(op->sw_u);
+    op->sw_T = op->sw_u = nullptr;
+    throw;
+  }
+  dfree(scr);
 }
 
 HH_API int hh_op_set_precond(hh_op* op, int kind, double beta, int sweeps, double damping) {
@@ -775,6 +854,7 @@ HH_API int hh_op_set_precond(hh_op* op, int kind, double beta, int sweeps, doubl
       HIPC(hipGetLastError());
       HIPC(hipStreamSynchronize(op->ctx->stream));
     }
+    sweep_dense_configure(op);
   }
   op->pkind = kind;
   op->beta = beta;
@@ -912,6 +992,7 @@ HH_API int hh_vec_create(hh_op* op, hh_vec** v) {
     delete x;
     throw;
   }
+  op->refs++;  // the vector keeps its operator alive
   *v = x;
   GUARD_END
 }
@@ -919,10 +1000,12 @@ HH_API int hh_vec_create(hh_op* op, hh_vec** v) {
 HH_API int hh_vec_destroy(hh_vec* v) {
   GUARD_BEGIN
   if (!v) return HH_OK;
-  (void)hipSetDevice(v->op->ctx->device);
-  (void)hipStreamSynchronize(v->op->ctx->stream);
+  hh_op* op = v->op;
+  (void)hipSetDevice(op->ctx->device);
+  (void)hipStreamSynchronize(op->ctx->stream);
   dfree(v->d);
   delete v;
+  op_release(op);
   GUARD_END
 }
 
@@ -1036,6 +1119,17 @@ HH_API int hh_op_tune(hh_op* op, int variant, int rows_per_block, int grid_block
   GUARD_END
 }
 
+HH_API int hh_op_sweep_mode(hh_op* op, int mode, int* active) {
+  GUARD_BEGIN
+  REQUIRE(op, "null op");
+  REQUIRE(mode >= -1 && mode <= 1, "mode must be -1, 0 or 1");
+  HIPC(hipSetDevice(op->ctx->device));
+  op->sw_mode = mode;
+  if (op->sw_P) sweep_dense_configure(op);  // already factored: switch now
+  if (active) *active = op->sw_T ? 1 : 0;
+  GUARD_END
+}
+
 HH_API int hh_tune_krylov(int nt_loads, int blocks) {
   GUARD_BEGIN
   REQUIRE(blocks >= 0 && blocks <= (1 << 20), "blocks out of range");
@@ -1128,6 +1222,12 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     return HH_OK;
   }
   if (op->pkind == HH_PREC_SWEEP_REF) {
+    // The constant map makes M A rank one: every w = M A v is the same vector c as v_0, and the
+    // whole cycle hinges on scipy's breakdown test h1 <= eps h0 (iterative.py:767) applied to
+    // the ~1-ulp residue of c - <v_0, c> v_0 -- rounding decides whether it fires (scipy: after
+    // 1-3 cycles).  A second Gram-Schmidt pass takes the residue to the exact-arithmetic
+    // answer (h1 ~ eps^2 h0): breakdown in the first cycle, never a 10 N-iteration crawl.
+    reorth = 1;
     // run_solver's M (code.py:510-511, quirk Q1) is algo2_4 of the right-hand side f_vec,
     // whatever GMRES passes it: compute that constant once
     dfree(op->sw_const);

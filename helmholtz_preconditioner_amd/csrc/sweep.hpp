@@ -26,4 +26,15 @@ size_t sweep_scratch_per_wave(int n);  // padded block size B (4, 8, 12, 16) or 
 void launch_sweep(const SweepArgs& a, int what, double2* u, double2* uF, int asis,
                   hipStream_t st);
 
+// Dense-transfer form (sweep_dense.hip): n matrices of n x n -- A_ll^-1 (l < b) of H_F, then
+// T_m (m = b+1 .. n) -- formed at setup from the block-Thomas factors; the apply is a GEMV chain.
+size_t sweep_dense_bytes(int n);                       // bytes of the n matrices
+size_t sweep_dense_scratch_per_block(int n, int b);    // setup scratch (double2) per block
+int sweep_dense_chunks(int n);                          // setup blocks per system
+void launch_sweep_dense_setup(const SweepArgs& a, int s_base, int batch, double2* yscr,
+                              double2* T, hipStream_t st);
+// out = M r (r and out distinct, u: n^2 scratch); asis: middle sweep u -= T u (quirk Q2)
+void launch_sweep_dense_apply(const SweepArgs& a, const double2* T, const double2* r,
+                              double2* out, double2* u, int asis, hipStream_t st);
+
 }  // namespace hh

@@ -87,7 +87,9 @@ class DeviceVector:
         check(lib.hh_vec_fill_hash(self._h, ctypes.c_uint64(seed)))
 
     def close(self):
-        if getattr(self, "_h", None) is not None and self.op._h is not None:
+        # the library keeps the operator (and its context) alive until its vectors are gone,
+        # so a vector can always be released, whatever order a garbage collector picks
+        if getattr(self, "_h", None) is not None:
             lib.hh_vec_destroy(self._h)
         self._h = None
 
@@ -304,6 +306,23 @@ class Sweeping(DevicePreconditioner):
     sweep is sequential in the layer index).
     """
 
-    def __init__(self, A: DeviceOperator, reference: bool = False):
+    FORMS = {"auto": -1, "thomas": 0, "dense": 1}
+
+    def __init__(self, A: DeviceOperator, reference: bool = False, form: str = "auto"):
+        """``form``: ``"dense"`` forms the n matrices T_m (n^3 x 16 B of HBM) at setup and
+        applies M as a chain of GEMVs; ``"thomas"`` keeps O(n^2 b^2) block-Thomas factors
+        and solves; ``"auto"`` picks dense when n <= 2048 and it fits.  Same results to
+        rounding."""
         self.kind = _ffi.HH_PREC_SWEEP_REF if reference else _ffi.HH_PREC_SWEEP
+        if form not in self.FORMS:
+            raise ValueError(f"form must be one of {sorted(self.FORMS)}")
+        self.form = form
         super().__init__(A)
+
+    def configure(self):
+        A = self.A
+        active = ctypes.c_int()
+        check(lib.hh_op_sweep_mode(A.handle, self.FORMS[self.form], ctypes.byref(active)))
+        super().configure()
+        check(lib.hh_op_sweep_mode(A.handle, self.FORMS[self.form], ctypes.byref(active)))
+        self.dense = bool(active.value)

@@ -187,6 +187,13 @@ int hh_gmres(hh_op* op, const hh_vec* b, hh_vec* x, double rtol, double atol,
  * persistent grid of that many workgroups (0 = one per tile).  Results are identical
  * for every setting; only speed changes. */
 int hh_op_tune(hh_op* op, int variant, int rows_per_block, int grid_blocks);
+/* Sweeping preconditioner form (speed / memory only; results agree to rounding):
+ *   mode -1 (default) dense transfer matrices when n <= 2048 and the n^3 x 16 B fit in HBM,
+ *           else block-Thomas solves;  0 block-Thomas solves (O(n^2 b^2) memory, every solve
+ *           2n dependent steps);  1 dense transfer matrices (error if they do not fit).
+ * Applies at the next sweeping setup, or at once if the operator is already factored.
+ * active (optional) receives 1 when the dense form is in use. */
+int hh_op_sweep_mode(hh_op* op, int mode, int* active);
 /* Process-wide tuning of the Krylov streaming kernels (multidot / update): non-temporal
  * basis loads on/off and the streaming grid size (0 = default 1024).  Speed only. */
 int hh_tune_krylov(int nt_loads, int blocks);

@@ -99,3 +99,60 @@ def test_gmres_reference_run_as_is(ctx, name):
     assert info == int(z["gmres_info"])
     assert 1 <= len(hist) <= 3 and 1 <= len(z["gmres_hist"]) <= 3
     assert np.all(np.abs(hist) < 1e-12)  # the reference's presid history is ~0 (breakdown)
+
+
+# ---------------------------------------------------------------- dense-transfer form
+@pytest.mark.parametrize("n,b,kind", [(96, 12, "c1"), (130, 8, "const"), (61, 5, "c1"),
+                                      (13, 12, "c2"), (200, 16, "c2"), (300, 12, "c1")])
+def test_sweep_dense_matches_thomas_and_oracle(ctx, n, b, kind):
+    om, h, eta = O.problem_params(n, b, 5.0, 2.0)
+    cm = medium(kind, n)
+    A = H.build_A_matrix(b, 81.0, eta, om, h, n, cm, context=ctx)
+    x = rand_complex(n * n, n + 1)
+    st = O.SweepState(b, 81.0, eta, om, h, n, cm) if n <= 200 else None
+    for reference in (False, True):
+        Md = H.Sweeping(A, reference=reference, form="dense")
+        yd = Md @ x
+        assert Md.dense
+        Mt = H.Sweeping(A, reference=reference, form="thomas")
+        yt = Mt @ x
+        assert not Mt.dense
+        assert relerr(yd, yt) < 1e-10
+        if st is not None:
+            assert relerr(yd, st.apply(x, corrected=not reference)) < 1e-10
+
+
+def test_sweep_dense_large_rows(ctx):
+    """n > 1024: the 32-chunk GEMV rows and several setup chunks per system."""
+    n, b = 1100, 12
+    om, h, eta = O.problem_params(n, b, 40.0, 2.0)
+    A = H.build_A_matrix(b, 81.0, eta, om, h, n, O.init_c1_mat(.5, .5, n), context=ctx)
+    x = rand_complex(n * n, 11)
+    yd = H.Sweeping(A, form="dense") @ x
+    yt = H.Sweeping(A, form="thomas") @ x
+    assert relerr(yd, yt) < 1e-9
+
+
+@pytest.mark.parametrize("name", ["sweep_n48_c1.npz", "sweep_n37_c2.npz"])
+def test_sweep_dense_as_is_matches_reference_golden(ctx, name):
+    z = load_golden(name)
+    A, (b, C, eta, om, h, n, cm) = _case(z, ctx)
+    M = H.Sweeping(A, reference=True, form="dense")
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    assert relerr(M @ f, z["u_f"]) < 1e-10
+    assert relerr(M @ rand_complex(n * n, 3), z["u_x"]) < 1e-10
+
+
+def test_gmres_dense_sweeping_vs_oracle(ctx):
+    z = load_golden("sweep_n48_c1.npz")
+    A, (b, C, eta, om, h, n, cm) = _case(z, ctx)
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    Aref = O.build_A_matrix(b, C, eta, om, h, n, cm)
+    Mref, _ = O.sweeping_preconditioner(b, C, eta, om, h, n, cm, corrected=True)
+    xr, infor, histr, _ = O.gmres_reference(Aref, f, M=Mref, rtol=1e-3, restart=20, maxiter=200)
+    x, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=200,
+                            M=H.Sweeping(A, form="dense"), callback=lambda r: None,
+                            callback_type="legacy", return_history=True)
+    assert info == infor == 0 and len(hist) == len(histr)
+    assert np.max(np.abs(hist - histr) / histr) < 1e-6
+    assert relerr(x, xr) < 1e-6

@@ -1,6 +1,10 @@
 """Sweeping preconditioner (row F1) timings on the device vs the reference's SuperLU path
 (oracle restatement of algo2_3 / algo2_4 on this host's CPU).
-usage: python tools/bench_sweep.py [n ...]"""
+usage: python tools/bench_sweep.py [--form dense|thomas|auto] [n ...]
+
+Dense-form apply algorithmic bytes: every transfer matrix read once by the fused
+forward+middle pass and once by the backward pass: 2 (n - b) n^2 16 B + b n^2 16 B (F0)
++ n^2 16 B (FC), i.e. the GEMV chain's matrix stream (vectors ignored)."""
 import os
 import sys
 import time
@@ -12,7 +16,11 @@ sys.path.insert(0, ROOT)
 import helmholtz_preconditioner_amd as H  # noqa: E402
 from helmholtz_preconditioner_amd import _ffi  # noqa: E402
 
-ns = [int(v) for v in sys.argv[1:]] or [127, 255, 511, 1023]
+args = sys.argv[1:]
+form = "auto"
+if args and args[0] == "--form":
+    form, args = args[1], args[2:]
+ns = [int(v) for v in args] or [127, 255, 511, 1023]
 for n in ns:
     b, C, wn = 12, {127: 81.0, 255: 62.0, 511: 81.0, 1023: 100.0}.get(n, 81.0), n // 8 + 1
     om, h, eta = H.problem_params(n, b, float(wn), 2.0)
@@ -20,19 +28,27 @@ for n in ns:
     A = H.build_A_matrix(b, C, eta, om, h, n, cm)
     A.ctx.synchronize()
     t0 = time.perf_counter()
-    A.set_preconditioner(_ffi.HH_PREC_SWEEP)
+    Msw = H.Sweeping(A, form=form)
+    Msw.configure()
+    A.ctx.synchronize()
     t_setup = time.perf_counter() - t0
     x, y = A.vector(f.ravel()), A.vector()
     A.apply_device(x, y, _ffi.HH_APPLY_PREC)
     t0 = time.perf_counter()
-    for _ in range(2):
+    reps = 10 if Msw.dense else 2
+    for _ in range(reps):
         A.apply_device(x, y, _ffi.HH_APPLY_PREC)
-    t_apply = (time.perf_counter() - t0) / 2
+    A.ctx.synchronize()
+    t_apply = (time.perf_counter() - t0) / reps
     t0 = time.perf_counter()
-    u, info, hist = H.gmres(A, f.ravel(), rtol=1e-3, restart=20, maxiter=300, M=H.Sweeping(A),
+    u, info, hist = H.gmres(A, f.ravel(), rtol=1e-3, restart=20, maxiter=300, M=Msw,
                             callback=lambda r: None, callback_type="legacy", return_history=True)
     t_solve = time.perf_counter() - t0
-    line = (f"n={n} b={b} wn={wn}: setup {t_setup*1e3:.1f} ms, apply {t_apply*1e3:.1f} ms, "
+    gbs = ""
+    if Msw.dense:
+        alg = (2 * (n - b) + b + 1) * n * n * 16
+        gbs = f" ({alg / t_apply / 1e9:.0f} GB/s algorithmic, dense)"
+    line = (f"n={n} b={b} wn={wn} form={form}: setup {t_setup*1e3:.1f} ms, apply {t_apply*1e3:.2f} ms{gbs}, "
             f"corrected-sweep GMRES {len(hist)} its info={info} in {t_solve:.3f} s")
     if n <= 255 and os.path.isdir(os.path.join(ROOT, "oracle")):
         from oracle import helmholtz_oracle as O
