@@ -136,6 +136,14 @@ struct hh_op {
   double2* sw_const = nullptr;  // as-is (quirk Q1): M x = algo2_4(b) for every x
   double2* sw_T = nullptr;      // dense transfer matrices (sweep_dense.hip), or null
   double2* sw_u = nullptr;      // dense apply scratch (n^2)
+  double2* sw_in = nullptr;     // dense apply: fixed input / output the captured graphs use
+  double2* sw_out = nullptr;
+  struct SweepGraph {
+    int asis;
+    const int* stop;
+    hipGraphExec_t exec;
+  };
+  std::vector<SweepGraph> sw_graphs;  // the 2 (n - b) + 1 GEMV launches, captured once
   int sw_mode = -1;             // -1 auto, 0 block-Thomas solves, 1 dense transfer matrices
   // tuning (hh_op_tune): stencil variant for the plain apply, rows per block override
   int variant = -1;
@@ -303,15 +311,52 @@ double2* sl_first_dst(hh_op* op, double2* out) {
 
 bool is_sweep(int kind) { return kind == HH_PREC_SWEEP || kind == HH_PREC_SWEEP_REF; }
 
+void sweep_dense_release(hh_op* op) {
+  for (auto& g : op->sw_graphs) (void)hipGraphExecDestroy(g.exec);
+  op->sw_graphs.clear();
+  dfree(op->sw_T);
+  dfree(op->sw_u);
+  dfree(op->sw_in);
+  dfree(op->sw_out);
+  op->sw_T = op->sw_u = op->sw_in = op->sw_out = nullptr;
+}
+
 // algo2_4 (code.py:356-385) on r -> out: forward, middle (as-is: u -= T u, quirk Q2;
 // corrected: u = T u), backward sweeps.  r and out must differ.
 void sweep_apply(hh_op* op, const double2* r, double2* out, bool asis) {
   hipStream_t s = op->ctx->stream;
   if (op->sw_T) {
-    SweepArgs a = op->sweep;
-    a.stop = op->stop_flag;
-    launch_sweep_dense_apply(a, op->sw_T, r, out, op->sw_u, asis ? 1 : 0, s);
-    HIPC(hipGetLastError());
+    // The chain is 2 (n - b) + 1 dependent GEMV launches: replayed from a graph captured once
+    // per (mode, stop flag) on fixed buffers, so the host does not pay a launch per GEMV.
+    const int am = asis ? 1 : 0;
+    hipGraphExec_t exec = nullptr;
+    for (auto& g : op->sw_graphs)
+      if (g.asis == am && g.stop == op->stop_flag) exec = g.exec;
+    if (!exec) {
+      SweepArgs a = op->sweep;
+      a.stop = op->stop_flag;
+      hipGraph_t graph = nullptr;
+      HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      launch_sweep_dense_apply(a, op->sw_T, op->sw_in, op->sw_out, op->sw_u, am, s);
+      const hipError_t le = hipGetLastError();
+      HIPC(hipStreamEndCapture(s, &graph));
+      if (le != hipSuccess) {
+        (void)hipGraphDestroy(graph);
+        HIPC(le);
+      }
+      const hipError_t ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(graph);
+      HIPC(ie);
+      if (op->sw_graphs.size() >= 4) {  // stale stop flags (a reallocated GMRES workspace)
+        (void)hipGraphExecDestroy(op->sw_graphs.front().exec);
+        op->sw_graphs.erase(op->sw_graphs.begin());
+      }
+      op->sw_graphs.push_back({am, op->stop_flag, exec});
+    }
+    const size_t bytes = (size_t)op->n * op->n * sizeof(double2);
+    HIPC(hipMemcpyAsync(op->sw_in, r, bytes, hipMemcpyDeviceToDevice, s));
+    HIPC(hipGraphLaunch(exec, s));
+    HIPC(hipMemcpyAsync(out, op->sw_out, bytes, hipMemcpyDeviceToDevice, s));
     return;
   }
   launch_scale_copy(r, out, op->nloc, 1.0, s, op->stop_flag);
@@ -743,8 +788,7 @@ static void op_release(hh_op* op) {
   dfree(op->sw_y);
   dfree(op->sw_uF);
   dfree(op->sw_const);
-  dfree(op->sw_T);
-  dfree(op->sw_u);
+  sweep_dense_release(op);
   if (op->status_h) (void)hipHostFree(op->status_h);
   (void)hipGetLastError();
   delete op;
@@ -770,9 +814,7 @@ HH_API int hh_op_local_rows(hh_op* op, int* j_begin, int* j_end) {
 static void sweep_dense_configure(hh_op* op) {
   const int n = op->n, b = op->b;
   if (op->sw_mode == 0) {
-    dfree(op->sw_T);
-    dfree(op->sw_u);
-    op->sw_T = op->sw_u = nullptr;
+    sweep_dense_release(op);
     return;
   }
   if (op->sw_T) return;
@@ -803,11 +845,11 @@ static void sweep_dense_configure(hh_op* op) {
       launch_sweep_dense_setup(op->sweep, s0, std::min(batch, nsys - s0), scr, op->sw_T, s);
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(s));
+    op->sw_in = dalloc<double2>((size_t)n * n);
+    op->sw_out = dalloc<double2>((size_t)n * n);
   } catch (...) {
     dfree(scr);
-    dfree(op->sw_T);
-    dfree(op->sw_u);
-    op->sw_T = op->sw_u = nullptr;
+    sweep_dense_release(op);
     throw;
   }
   dfree(scr);

@@ -157,6 +157,17 @@ __global__ __launch_bounds__(256) void dense_gemv_kernel(const GemvStep g, const
   if (stop && *stop) return;
   __shared__ double2 xs[J * 64];
   const int y = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int i = min(blockIdx.x * 4 + (threadIdx.x >> 6), n - 1);  // rows past n: clamped, unused
+  // the matrix row does not depend on x: its loads go out first (unconditional, clamped
+  // columns, masked at use: xs is 0 there) and stream while x is staged in LDS
+  const double2* Trow = g.T + ((size_t)(g.mat + y) * n + i) * n;
+  double2 tv[J];
+  ufor<0, J>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    const int k = min(lane + 64 * j, n - 1);
+    tv[j] = make_double2(__builtin_nontemporal_load(&Trow[k].x), __builtin_nontemporal_load(&Trow[k].y));
+  });
   const double2* in = g.in + (size_t)y * n;
   for (int k = threadIdx.x; k < J * 64; k += 256) {
     double2 v = make_double2(0.0, 0.0);
@@ -167,17 +178,7 @@ __global__ __launch_bounds__(256) void dense_gemv_kernel(const GemvStep g, const
     xs[k] = v;
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= n) return;
-  const double2* Trow = g.T + ((size_t)(g.mat + y) * n + i) * n;
-  // every load unconditional from a clamped column; masked at use (xs is 0 there)
-  double2 tv[J];
-  ufor<0, J>([&](auto jc) {
-    constexpr int j = decltype(jc)::value;
-    const int k = min(lane + 64 * j, n - 1);
-    tv[j] = make_double2(__builtin_nontemporal_load(&Trow[k].x), __builtin_nontemporal_load(&Trow[k].y));
-  });
+  if (blockIdx.x * 4 + (threadIdx.x >> 6) >= n) return;
   double2 acc = make_double2(0.0, 0.0);
   ufor<0, J>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
