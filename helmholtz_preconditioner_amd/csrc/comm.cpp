@@ -118,6 +118,7 @@ class ShmComm final : public Comm {
     slots_ = reinterpret_cast<double*>(base_ + 4096);
     halo_ = base_ + 4096 + (size_t)w * kShmSlotDoubles * sizeof(double);
     HIPC(hipHostMalloc(reinterpret_cast<void**>(&pin_), kShmSlotDoubles * sizeof(double)));
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&hpin_), 4 * kShmHaloBytes));
     barrier();
     // every rank has mapped the segment: drop its name now so nothing can leak in /dev/shm
     // (the mappings stay valid until each rank unmaps)
@@ -126,6 +127,7 @@ class ShmComm final : public Comm {
   ~ShmComm() override {
     // no barrier here: a peer may already have exited
     if (pin_) (void)hipHostFree(pin_);
+    if (hpin_) (void)hipHostFree(hpin_);
     if (base_) munmap(base_, size_);
   }
   void allreduce(double* d, int count, bool max, hipStream_t s) override {
@@ -149,18 +151,23 @@ class ShmComm final : public Comm {
   void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi, size_t bytes,
             hipStream_t compute, hipStream_t, hipEvent_t) override {
     REQUIRE(bytes <= kShmHaloBytes, "shm halo row too large (n > 65536)");
-    // Every copy is ordered on `compute` and completed before the barrier that releases the
-    // peers: a plain hipMemcpy from pageable (shm) memory may return before its DMA has
-    // landed, and the boundary-row kernels on the non-blocking compute stream would not
-    // wait for it; a peer may also refill its slot as soon as the second barrier passes.
-    if (send_lo) HIPC(hipMemcpyAsync(slot(rank, 0), send_lo, bytes, hipMemcpyDeviceToHost, compute));
-    if (send_hi) HIPC(hipMemcpyAsync(slot(rank, 1), send_hi, bytes, hipMemcpyDeviceToHost, compute));
+    // Device <-> shared memory goes through this rank's pinned staging rows: DMA copies to /
+    // from pinned memory on `compute` (ordered after the kernels that produced `send_*` and
+    // before the boundary-row kernels that read `recv_*`), completed by a stream sync, and
+    // plain CPU copies between the pinned rows and the shared segment.  Pageable (shm)
+    // memory is never a DMA endpoint: its copy semantics are not stream-ordered.
+    if (send_lo) HIPC(hipMemcpyAsync(hpin_, send_lo, bytes, hipMemcpyDeviceToHost, compute));
+    if (send_hi) HIPC(hipMemcpyAsync(hpin_ + kShmHaloBytes, send_hi, bytes, hipMemcpyDeviceToHost, compute));
     HIPC(hipStreamSynchronize(compute));
+    if (send_lo) std::memcpy(slot(rank, 0), hpin_, bytes);
+    if (send_hi) std::memcpy(slot(rank, 1), hpin_ + kShmHaloBytes, bytes);
     barrier();
-    if (recv_lo) HIPC(hipMemcpyAsync(recv_lo, slot(rank - 1, 1), bytes, hipMemcpyHostToDevice, compute));
-    if (recv_hi) HIPC(hipMemcpyAsync(recv_hi, slot(rank + 1, 0), bytes, hipMemcpyHostToDevice, compute));
-    HIPC(hipStreamSynchronize(compute));
-    barrier();
+    if (recv_lo) std::memcpy(hpin_ + 2 * kShmHaloBytes, slot(rank - 1, 1), bytes);
+    if (recv_hi) std::memcpy(hpin_ + 3 * kShmHaloBytes, slot(rank + 1, 0), bytes);
+    barrier();  // the neighbours' slots may be refilled from here on
+    if (recv_lo) HIPC(hipMemcpyAsync(recv_lo, hpin_ + 2 * kShmHaloBytes, bytes, hipMemcpyHostToDevice, compute));
+    if (recv_hi) HIPC(hipMemcpyAsync(recv_hi, hpin_ + 3 * kShmHaloBytes, bytes, hipMemcpyHostToDevice, compute));
+    HIPC(hipStreamSynchronize(compute));  // hpin_ is reused by the next exchange
   }
 
  private:
@@ -192,6 +199,7 @@ class ShmComm final : public Comm {
   double* slots_ = nullptr;
   char* halo_ = nullptr;
   double* pin_ = nullptr;
+  char* hpin_ = nullptr;  // pinned halo staging: send lo, send hi, recv lo, recv hi
 };
 }  // namespace
 

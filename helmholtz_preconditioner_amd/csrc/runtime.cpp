@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cmath>
 #include <complex>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <memory>
@@ -329,6 +330,19 @@ void sweep_apply(hh_op* op, const double2* r, double2* out, bool asis) {
     // The chain is 2 (n - b) + 1 dependent GEMV launches: replayed from a graph captured once
     // per (mode, stop flag) on fixed buffers, so the host does not pay a launch per GEMV.
     const int am = asis ? 1 : 0;
+    // HH_SWEEP_GRAPH=0: eager launches of the same kernels (profilers that cannot follow
+    // graph replays)
+    static const bool use_graph = [] {
+      const char* e = std::getenv("HH_SWEEP_GRAPH");
+      return !(e && e[0] == '0');
+    }();
+    if (!use_graph) {
+      SweepArgs a = op->sweep;
+      a.stop = op->stop_flag;
+      launch_sweep_dense_apply(a, op->sw_T, r, out, op->sw_u, am, s);
+      HIPC(hipGetLastError());
+      return;
+    }
     hipGraphExec_t exec = nullptr;
     for (auto& g : op->sw_graphs)
       if (g.asis == am && g.stop == op->stop_flag) exec = g.exec;
@@ -487,7 +501,7 @@ void ensure_gmres(hh_op* op, int restart) {
   const size_t nH = (size_t)restart * R1, nG = 2 * (size_t)restart, nS = R1, nY = restart;
   const size_t total2 = nH + nG + nS + nY + (R1 + 8 + 1) / 2 + 8 + 2 * (size_t)restart + 8;
   op->gbuf = dalloc<double2>(total2);
-  HIPC(hipMemset(op->gbuf, 0, total2 * sizeof(double2)));
+  HIPC(hipMemsetAsync(op->gbuf, 0, total2 * sizeof(double2), op->ctx->stream));
   GivensState& g = op->gs;
   g.H = op->gbuf;
   g.G = g.H + nH;
@@ -498,7 +512,7 @@ void ensure_gmres(hh_op* op, int restart) {
   g.status_it = g.status + 8;
   dfree(op->gctrl);
   op->gctrl = dalloc<int>(8);
-  HIPC(hipMemset(op->gctrl, 0, 8 * sizeof(int)));
+  HIPC(hipMemsetAsync(op->gctrl, 0, 8 * sizeof(int), op->ctx->stream));
   g.ctrl = op->gctrl;
   g.restart = restart;
 }
@@ -691,7 +705,7 @@ HH_API int hh_op_create(hh_ctx* c, int n, int b, double cconst, double eta, doub
     op->tab_i = dalloc<double2>(3 * (size_t)n);
     HIPC(hipMemcpy(op->tab_i, ti.data(), ti.size() * sizeof(double2), hipMemcpyHostToDevice));
     op->zero_row = dalloc<double2>(n);
-    HIPC(hipMemset(op->zero_row, 0, n * sizeof(double2)));
+    HIPC(hipMemsetAsync(op->zero_row, 0, n * sizeof(double2), c->stream));
     // local slabs
     const int rows = op->je - op->jb;
     size_t off = 0;
@@ -735,8 +749,8 @@ HH_API int hh_op_create(hh_ctx* c, int n, int b, double cconst, double eta, doub
       }
       sl.halo_lo_buf = dalloc<double2>(n);
       sl.halo_hi_buf = dalloc<double2>(n);
-      HIPC(hipMemset(sl.halo_lo_buf, 0, n * sizeof(double2)));
-      HIPC(hipMemset(sl.halo_hi_buf, 0, n * sizeof(double2)));
+      HIPC(hipMemsetAsync(sl.halo_lo_buf, 0, n * sizeof(double2), c->stream));
+      HIPC(hipMemsetAsync(sl.halo_hi_buf, 0, n * sizeof(double2), c->stream));
       op->slabs.push_back(sl);
     }
     // partial-sum workspace: stencil tiles (+ boundary rows) of every slab, or streaming blocks
@@ -833,7 +847,7 @@ static void sweep_dense_configure(hh_op* op) {
   double2* scr = nullptr;
   try {
     op->sw_u = dalloc<double2>((size_t)n * n);
-    HIPC(hipMemset(op->sw_u, 0, (size_t)n * n * sizeof(double2)));
+    HIPC(hipMemsetAsync(op->sw_u, 0, (size_t)n * n * sizeof(double2), op->ctx->stream));
     // concurrency: ~1024 setup blocks, within a scratch budget of the remaining memory
     const size_t left = free_b - tbytes - (size_t)n * n * 16;
     const size_t budget = std::min(left / 4, (size_t)32 << 30);
@@ -1029,7 +1043,7 @@ HH_API int hh_vec_create(hh_op* op, hh_vec** v) {
   x->op = op;
   try {
     x->d = dalloc<double2>(op->nloc);
-    HIPC(hipMemset(x->d, 0, op->nloc * sizeof(double2)));
+    HIPC(hipMemsetAsync(x->d, 0, op->nloc * sizeof(double2), op->ctx->stream));
   } catch (...) {
     delete x;
     throw;
