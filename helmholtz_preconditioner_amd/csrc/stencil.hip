@@ -166,7 +166,12 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
   int iw, ie;
   bool lw, le;
   if constexpr (XM == XM_LDS) {
-    iw = i0 - 1; ie = i0 + TPB; lw = tid == 0; le = tid == TPB - 1;
+    // One broadcast load per wave and row serves both strip edges: lanes 0-31 read the W
+    // halo column, lanes 32-63 the E halo column (two cache lines per wave; tid 0 keeps W,
+    // tid TPB-1 keeps E).  Re-reading each lane's own column instead would cost a full row
+    // of line requests per load, and miss entirely once u is loaded non-temporally.
+    iw = ie = lane < kWave / 2 ? i0 - 1 : i0 + TPB;
+    lw = tid == 0; le = tid == TPB - 1;
   } else if constexpr (XM == XM_SHFL) {
     iw = i - lane - 1; ie = i - lane + kWave; lw = lane == 0; le = lane == kWave - 1;
   } else {
@@ -174,9 +179,9 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
   }
   lw = lw && iw >= 0;
   le = le && ie < n;
-  iw = max(iw, 0);
-  ie = min(ie, n - 1);
-  if constexpr (XM != XM_DIRECT) {
+  iw = min(max(iw, 0), n - 1);
+  ie = min(max(ie, 0), n - 1);
+  if constexpr (XM == XM_SHFL) {
     // lanes without an edge duty re-read their own column (an L1 hit) so that the load
     // stays unconditional
     iw = lw ? iw : ic_;
@@ -189,7 +194,7 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
     else v.ic = a.invc2_const;
     const double2* rp = rowp(r);
     v.eW = rp[iw];
-    v.eE = rp[ie];
+    if constexpr (XM != XM_LDS) v.eE = rp[ie];  // XM_LDS: eW holds both edges (see above)
   };
   auto load_u = [&](int r) { return ld2<NTU>(rowp(r) + ic_); };
   const cdouble_p tabj = (cdouble_p)(a.tab_j);
@@ -248,7 +253,7 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
       // ---- W/E neighbours ----
       const double2 uCm = act ? uC : z2;  // columns past n contribute zero (Dirichlet)
       const double2 eW = lw ? in.eW : z2;
-      const double2 eE = le ? in.eE : z2;
+      const double2 eE = le ? (XM == XM_LDS ? in.eW : in.eE) : z2;
       double2 uW, uE;
       if constexpr (XM == XM_LDS) {
         double2* buf = lrow[k & 1];
@@ -368,7 +373,9 @@ __global__ __launch_bounds__(kStencilThreads) void point_kernel(const PointArgs 
 
 // Default exchange/prefetch/store variant for every epilogue (tuned on MI355X, see
 // DESIGN.md "stencil variants"); the benchmark kernel (EPI_AX) can run all 12 variants.
-constexpr int kDefaultVariant = 30;  // XM_LDS, PF 1, NT stores + NT 1/c^2 loads, 512-wide strips
+constexpr int kDefaultVariant = 42;  // XM_LDS, PF 1, NT stores + NT loads of 1/c^2 and u, 512-wide strips
+constexpr int kSmallVariant = 18;    // the same with 256-wide strips (grids below 2048)
+constexpr int kCachedVariant = 30;   // 512-wide, cached u loads (A/B against the default)
 
 // Variant table: V = XM + 3 (PF - 1) + 6 NT + 12 NTU + 24 (512-wide strips)  (0..47).
 template <int V>
@@ -402,10 +409,11 @@ template <int EPI>
 void launch_stencil_t(bool const_c, const StencilArgs& a, int blocks, hipStream_t s, int v) {
   if constexpr (EPI == EPI_AX) {
     launch_any<EPI, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21,
-               22, 23, 24, 25, 26, 27, 30, 31, 32, 33>(v, const_c, a, blocks, s);
+               22, 23, 24, 25, 26, 27, 30, 31, 32, 33, 42, 43, 45>(v, const_c, a, blocks, s);
   } else {
     // every epilogue has the two default shapes: 256-wide (small grids) and 512-wide strips
-    if (v == 6) launch_v<EPI, 6>(const_c, a, blocks, s);
+    if (v == kSmallVariant) launch_v<EPI, kSmallVariant>(const_c, a, blocks, s);
+    else if (v == kCachedVariant) launch_v<EPI, kCachedVariant>(const_c, a, blocks, s);
     else launch_v<EPI, kDefaultVariant>(const_c, a, blocks, s);
   }
 }
@@ -436,10 +444,16 @@ int stencil_rows_per_block(int n, int rows) {
 }
 
 int stencil_resolve_variant(int epi, int requested, int n) {
-  const int autov = n < 2048 ? 6 : kDefaultVariant;  // 256-wide strips for small grids
+  // 256-wide strips for small grids.  The shifted-Laplace epilogues read u while its
+  // producer's lines may still sit in L2 (measured in GMRES, tools/tune_gmres_variant.py):
+  // they keep cached u loads.
+  const bool shifted = epi == EPI_RES_SL || epi == EPI_SL_FIRST || epi == EPI_SL_SWEEP;
+  const int autov = n < 2048 ? kSmallVariant : (shifted ? kCachedVariant : kDefaultVariant);
   if (requested < 0) return autov;
   if (epi == EPI_AX) return stencil_variant_valid(requested) ? requested : autov;
-  return (requested == 6 || requested == kDefaultVariant) ? requested : autov;
+  return (requested == kSmallVariant || requested == kDefaultVariant || requested == kCachedVariant)
+             ? requested
+             : autov;
 }
 
 int stencil_grid_blocks(int n, int rows, int rows_per_block) {
@@ -452,7 +466,7 @@ int stencil_grid_blocks(int n, int rows, int rows_per_block) {
 
 
 int stencil_default_variant() { return kDefaultVariant; }
-bool stencil_variant_valid(int v) { return (v >= 0 && v <= 27) || (v >= 30 && v <= 33); }
+bool stencil_variant_valid(int v) { return (v >= 0 && v <= 27) || (v >= 30 && v <= 33) || v == 42 || v == 43 || v == 45; }
 
 void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_out[1],
                     hipStream_t stream, int variant) {
