@@ -77,6 +77,7 @@ __device__ __forceinline__ void store2(double2* p, double2 v, bool nt) {
 struct RowIn {
   double ic;
   double2 eW, eE;
+  double2 b;  // the once-read second input (b or r) of the EPI_RES* / EPI_SL_SWEEP epilogues
 };
 
 template <bool NTL>
@@ -195,6 +196,7 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
     const double2* rp = rowp(r);
     v.eW = rp[iw];
     if constexpr (XM != XM_LDS) v.eE = rp[ie];  // XM_LDS: eW holds both edges (see above)
+    if constexpr (T::reads_in1) v.b = ld2<NT>(a.in1 + (size_t)r * n + ic_);
   };
   auto load_u = [&](int r) { return ld2<NTU>(rowp(r) + ic_); };
   const cdouble_p tabj = (cdouble_p)(a.tab_j);
@@ -246,9 +248,8 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
       const double2 uS = U[k % UR], uC = U[(k + 1) % UR], uN = U[(k + 2) % UR];
       const RowIn& in = IN[k % IR];
       const Tab& tb = TB[k % 2];
-      double2 bin = z2;
       const size_t p = (size_t)min(r, re - 1) * n + ic_;
-      if constexpr (T::reads_in1) bin = a.in1[p];
+      const double2 bin = T::reads_in1 ? in.b : z2;  // prefetched with the row's inputs
 
       // ---- W/E neighbours ----
       const double2 uCm = act ? uC : z2;  // columns past n contribute zero (Dirichlet)
@@ -444,11 +445,10 @@ int stencil_rows_per_block(int n, int rows) {
 }
 
 int stencil_resolve_variant(int epi, int requested, int n) {
-  // 256-wide strips for small grids.  The shifted-Laplace epilogues read u while its
-  // producer's lines may still sit in L2 (measured in GMRES, tools/tune_gmres_variant.py):
-  // they keep cached u loads.
-  const bool shifted = epi == EPI_RES_SL || epi == EPI_SL_FIRST || epi == EPI_SL_SWEEP;
-  const int autov = n < 2048 ? kSmallVariant : (shifted ? kCachedVariant : kDefaultVariant);
+  // 256-wide strips for small grids.  Every epilogue streams u non-temporally: with the
+  // second input (b / r) prefetched alongside 1/c^2 the shifted-Laplace epilogues gain too
+  // (tools/tune_gmres_variant.py, profiles/r01i_tune_gmres_variant.log).
+  const int autov = n < 2048 ? kSmallVariant : kDefaultVariant;
   if (requested < 0) return autov;
   if (epi == EPI_AX) return stencil_variant_valid(requested) ? requested : autov;
   return (requested == kSmallVariant || requested == kDefaultVariant || requested == kCachedVariant)
