@@ -53,6 +53,7 @@ struct StencilArgs {
   int n, nl;
   int row_begin, row_end;  // local rows computed by this launch
   int rows_per_block;      // strip height marched by one block
+  int row_step;            // first-row distance of consecutive bands (0: rows_per_block)
   int tiles_x, tiles_y, tiles_per_xcd;  // XCD-aware tile map
   int grid_blocks;         // 0: one block per tile; >0: persistent grid of this many blocks
   double2 mshift;          // mass-term multiplier for the shifted operator (EPI_SL_*)
@@ -107,7 +108,8 @@ int stencil_resolve_variant(int epi, int requested, int n);
 // Streaming roofline probes (probe.hip); returns the probe's bytes per point (0: unknown kind).
 int launch_probe_kind(int kind, int blocks, const double2* u, const double* ic, double2* y,
                       size_t len, hipStream_t s);
-int stencil_grid_blocks(int n, int rows, int rows_per_block);
+int stencil_grid_blocks(int n, int rows, int rows_per_block, int row_step = 0);
+int stencil_bands(int rows, int rows_per_block, int row_step);  // tiles along j
 int stencil_rows_per_block(int n, int rows);
 void launch_point(int op, bool const_c, const PointArgs& a, int blocks, hipStream_t stream);
 int point_blocks(size_t len);

@@ -216,15 +216,16 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
   };
 
   int nparts = 0;
-  auto launch_rows = [&](int si, int r0, int r1, int rpb) {
+  auto launch_rows = [&](int si, int r0, int r1, int rpb, int step = 0) {
     if (r1 <= r0) return;
     StencilArgs a = make_args(si);
     a.row_begin = r0;
     a.row_end = r1;
+    a.row_step = step;
     a.rows_per_block = (op->rpb_override > 0 && rpb > 1) ? std::min(op->rpb_override, r1 - r0) : rpb;
     a.grid_blocks = op->grid_override;
     a.partials = op->partials + (size_t)nparts * kMaxNorms;
-    REQUIRE((size_t)(nparts + stencil_grid_blocks(n, r1 - r0, a.rows_per_block)) * kMaxNorms <=
+    REQUIRE((size_t)(nparts + stencil_grid_blocks(n, r1 - r0, a.rows_per_block, step)) * kMaxNorms <=
                 op->partials_cap,
             "partials workspace too small for the stencil launch");
     int written = 0;
@@ -249,6 +250,8 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
     const Slab& sl = op->slabs[S - 1];
     if (S == 1 && s0.nl == 1) {
       launch_rows(0, 0, 1, 1);
+    } else if (S == 1 && lo_x && hi_x) {
+      launch_rows(0, 0, s0.nl, 1, s0.nl - 1);  // rows 0 and nl-1: one launch of two bands
     } else {
       if (lo_x) launch_rows(0, 0, 1, 1);
       if (hi_x) launch_rows(S - 1, sl.nl - 1, sl.nl, 1);

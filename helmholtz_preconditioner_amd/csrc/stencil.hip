@@ -157,7 +157,7 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
   const int ic_ = min(i, n - 1);  // clamped column for loads
   // row band (wave-uniform; readfirstlane keeps the row loop and its prefetch branches on
   // the scalar unit)
-  const int rb = __builtin_amdgcn_readfirstlane(a.row_begin + ty * a.rows_per_block);
+  const int rb = __builtin_amdgcn_readfirstlane(a.row_begin + ty * a.row_step);
   const int re = __builtin_amdgcn_readfirstlane(min(rb + a.rows_per_block, a.row_end));
 
   auto rowp = [&](int r) -> const double2* {
@@ -456,9 +456,14 @@ int stencil_resolve_variant(int epi, int requested, int n) {
              : autov;
 }
 
-int stencil_grid_blocks(int n, int rows, int rows_per_block) {
+int stencil_bands(int rows, int rows_per_block, int row_step) {
+  if (row_step <= 0) row_step = rows_per_block;
+  return rows <= rows_per_block ? 1 : (rows - rows_per_block + row_step - 1) / row_step + 1;
+}
+
+int stencil_grid_blocks(int n, int rows, int rows_per_block, int row_step) {
   const int tiles_x = (n + kStencilThreads - 1) / kStencilThreads;
-  const int tiles_y = (rows + rows_per_block - 1) / rows_per_block;
+  const int tiles_y = stencil_bands(rows, rows_per_block, row_step);
   const int tiles = tiles_x * tiles_y;
   const int per_xcd = (tiles + 7) / 8;
   return per_xcd * 8;
@@ -475,7 +480,10 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_
   const int v = stencil_resolve_variant(epi, variant, a.n);
   const int tpb = v >= 24 ? 512 : 256;
   a.tiles_x = (a.n + tpb - 1) / tpb;
-  a.tiles_y = (rows + a.rows_per_block - 1) / a.rows_per_block;
+  // bands start every row_step rows (spaced out only by the halo-row launch of a rank inside
+  // the decomposition: rows 0 and nl-1 in one launch)
+  if (a.row_step <= 0) a.row_step = a.rows_per_block;
+  a.tiles_y = stencil_bands(rows, a.rows_per_block, a.row_step);
   a.tiles_per_xcd = (a.tiles_x * a.tiles_y + 7) / 8;
   int blocks = a.tiles_per_xcd * 8;
   if (a.grid_blocks > 0 && a.grid_blocks < blocks) blocks = (a.grid_blocks + 7) / 8 * 8;
