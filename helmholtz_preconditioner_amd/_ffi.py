@@ -68,12 +68,16 @@ SIGNATURES = [
     ("hh_vec_fill_hash", c_int, [c_void_p, ctypes.c_uint64]),
     ("hh_op_apply_dev", c_int, [c_void_p, c_void_p, c_void_p, c_int]),
     ("hh_op_time_apply", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_dp, c_dp]),
+    ("hh_op_time_apply_set", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_dp,
+                                     c_dp]),
     ("hh_gmres", c_int, [c_void_p, c_void_p, c_void_p, c_double, c_double, c_int, c_long, c_int,
                          c_int, c_dp, c_long, GMRES_CALLBACK, c_void_p, c_lp, c_ip, c_dp, c_dp]),
     ("hh_op_tune", c_int, [c_void_p, c_int, c_int, c_int]),
     ("hh_op_sweep_mode", c_int, [c_void_p, c_int, c_ip]),
     ("hh_tune_krylov", c_int, [c_int, c_int]),
     ("hh_op_probe_stream", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_dp, c_ip]),
+    ("hh_op_probe_stream_set", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
+                                       c_dp, c_ip]),
     ("hh_op_last_stats", c_int, [c_void_p, ctypes.POINTER(HHStats)]),
 ]
 

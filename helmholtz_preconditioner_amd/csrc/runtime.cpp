@@ -1111,8 +1111,16 @@ HH_API int hh_op_apply_dev(hh_op* op, const hh_vec* x, hh_vec* y, int mode) {
 
 HH_API int hh_op_time_apply(hh_op* op, const hh_vec* x, hh_vec* y, int mode, int iters,
                             double* total_ms, double* kernel_ms) {
+  return hh_op_time_apply_set(op, &x, &y, 1, mode, iters, total_ms, kernel_ms);
+}
+
+HH_API int hh_op_time_apply_set(hh_op* op, const hh_vec* const* xs, hh_vec* const* ys, int nvec,
+                                int mode, int iters, double* total_ms, double* kernel_ms) {
   GUARD_BEGIN
-  REQUIRE(op && x && y && x != y && iters >= 1 && total_ms && kernel_ms, "bad arguments");
+  REQUIRE(op && xs && ys && nvec >= 1 && iters >= 1 && total_ms && kernel_ms, "bad arguments");
+  for (int k = 0; k < nvec; ++k)
+    REQUIRE(xs[k] && ys[k] && xs[k] != ys[k] && xs[k]->op == op && ys[k]->op == op,
+            "pair %d: vectors must be distinct and belong to this operator", k);
   HIPC(hipSetDevice(op->ctx->device));
   hipStream_t s = op->ctx->stream;
   // A plain apply on one slab of one rank is exactly one stencil launch: then the events
@@ -1139,7 +1147,7 @@ HH_API int hh_op_time_apply(hh_op* op, const hh_vec* x, hh_vec* y, int mode, int
       op->tk0 = k0[i];
       op->tk1 = k1[i];
     }
-    apply_mode(op, x->d, y->d, mode);
+    apply_mode(op, xs[i % nvec]->d, ys[i % nvec]->d, mode);
   }
   op->tk0 = op->tk1 = nullptr;
   HIPC(hipEventRecord(t1, s));
@@ -1198,8 +1206,18 @@ HH_API int hh_tune_krylov(int nt_loads, int blocks) {
 
 HH_API int hh_op_probe_stream(hh_op* op, int kind, int blocks, const hh_vec* x, hh_vec* y,
                               int iters, double* kernel_ms, int* bytes_per_point) {
+  return hh_op_probe_stream_set(op, kind, blocks, &x, &y, 1, iters, kernel_ms, bytes_per_point);
+}
+
+HH_API int hh_op_probe_stream_set(hh_op* op, int kind, int blocks, const hh_vec* const* xs,
+                                  hh_vec* const* ys, int nvec, int iters, double* kernel_ms,
+                                  int* bytes_per_point) {
   GUARD_BEGIN
-  REQUIRE(op && x && y && x != y && iters >= 1 && kernel_ms && bytes_per_point, "bad arguments");
+  REQUIRE(op && xs && ys && nvec >= 1 && iters >= 1 && kernel_ms && bytes_per_point,
+          "bad arguments");
+  for (int k = 0; k < nvec; ++k)
+    REQUIRE(xs[k] && ys[k] && xs[k] != ys[k] && xs[k]->op == op && ys[k]->op == op,
+            "pair %d: vectors must be distinct and belong to this operator", k);
   REQUIRE(!op->const_c && op->slabs.size() == 1, "probe needs a heterogeneous single-slab operator");
   REQUIRE(blocks >= 1 && blocks <= (1 << 20), "blocks out of range");
   HIPC(hipSetDevice(op->ctx->device));
@@ -1207,10 +1225,14 @@ HH_API int hh_op_probe_stream(hh_op* op, int kind, int blocks, const hh_vec* x, 
   hipEvent_t t0, t1;
   HIPC(hipEventCreate(&t0));
   HIPC(hipEventCreate(&t1));
-  const int bpp = launch_probe_kind(kind, blocks, x->d, op->slabs[0].invc2, y->d, op->nloc, s);
+  int bpp = 0;
+  for (int k = 0; k < nvec; ++k)  // warm-up, one launch per pair
+    bpp = launch_probe_kind(kind, blocks, xs[k]->d, op->slabs[0].invc2, ys[k]->d, op->nloc, s);
   REQUIRE(bpp > 0, "unknown probe kind %d", kind);
   HIPC(hipEventRecord(t0, s));
-  for (int i = 0; i < iters; ++i) launch_probe_kind(kind, blocks, x->d, op->slabs[0].invc2, y->d, op->nloc, s);
+  for (int i = 0; i < iters; ++i)
+    launch_probe_kind(kind, blocks, xs[i % nvec]->d, op->slabs[0].invc2, ys[i % nvec]->d,
+                      op->nloc, s);
   HIPC(hipEventRecord(t1, s));
   HIPC(hipEventSynchronize(t1));
   float ms = 0.f;

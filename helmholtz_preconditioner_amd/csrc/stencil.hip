@@ -174,7 +174,10 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
     iw = ie = lane < kWave / 2 ? i0 - 1 : i0 + TPB;
     lw = tid == 0; le = tid == TPB - 1;
   } else if constexpr (XM == XM_SHFL) {
-    iw = i - lane - 1; ie = i - lane + kWave; lw = lane == 0; le = lane == kWave - 1;
+    // the same broadcast per wave: its W halo column for lanes 0-31, its E one for 32-63;
+    // lane 0 keeps W, lane 63 keeps E (no block barrier: waves run independently)
+    iw = ie = lane < kWave / 2 ? i - lane - 1 : i - lane + kWave;
+    lw = lane == 0; le = lane == kWave - 1;
   } else {
     iw = i - 1; ie = i + 1; lw = act; le = act;
   }
@@ -182,12 +185,6 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
   le = le && ie < n;
   iw = min(max(iw, 0), n - 1);
   ie = min(max(ie, 0), n - 1);
-  if constexpr (XM == XM_SHFL) {
-    // lanes without an edge duty re-read their own column (an L1 hit) so that the load
-    // stays unconditional
-    iw = lw ? iw : ic_;
-    ie = le ? ie : ic_;
-  }
 
   const double2 z2 = make_double2(0.0, 0.0);
   auto load_row_in = [&](int r, RowIn& v) {
@@ -195,7 +192,7 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
     else v.ic = a.invc2_const;
     const double2* rp = rowp(r);
     v.eW = rp[iw];
-    if constexpr (XM != XM_LDS) v.eE = rp[ie];  // XM_LDS: eW holds both edges (see above)
+    if constexpr (XM == XM_DIRECT) v.eE = rp[ie];  // else eW holds both edges (see above)
     if constexpr (T::reads_in1) v.b = ld2<NT>(a.in1 + (size_t)r * n + ic_);
   };
   auto load_u = [&](int r) { return ld2<NTU>(rowp(r) + ic_); };
@@ -254,7 +251,7 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
       // ---- W/E neighbours ----
       const double2 uCm = act ? uC : z2;  // columns past n contribute zero (Dirichlet)
       const double2 eW = lw ? in.eW : z2;
-      const double2 eE = le ? (XM == XM_LDS ? in.eW : in.eE) : z2;
+      const double2 eE = le ? (XM == XM_DIRECT ? in.eE : in.eW) : z2;
       double2 uW, uE;
       if constexpr (XM == XM_LDS) {
         double2* buf = lrow[k & 1];
@@ -374,9 +371,10 @@ __global__ __launch_bounds__(kStencilThreads) void point_kernel(const PointArgs 
 
 // Default exchange/prefetch/store variant for every epilogue (tuned on MI355X, see
 // DESIGN.md "stencil variants"); the benchmark kernel (EPI_AX) can run all 12 variants.
-constexpr int kDefaultVariant = 42;  // XM_LDS, PF 1, NT stores + NT loads of 1/c^2 and u, 512-wide strips
-constexpr int kSmallVariant = 18;    // the same with 256-wide strips (grids below 2048)
-constexpr int kCachedVariant = 30;   // 512-wide, cached u loads (A/B against the default)
+constexpr int kDefaultVariant = 30;  // XM_LDS, PF 1, NT stores + NT 1/c^2 loads, cached u, 512-wide
+constexpr int kSmallVariant = 18;    // 256-wide strips, NT u loads (grids below 2048)
+constexpr int kSolveVariant = 42;    // kDefaultVariant with NT u loads: solve epilogues, rows <= kLongRow
+constexpr int kLongRow = 4608;
 
 // Variant table: V = XM + 3 (PF - 1) + 6 NT + 12 NTU + 24 (512-wide strips)  (0..47).
 template <int V>
@@ -410,11 +408,11 @@ template <int EPI>
 void launch_stencil_t(bool const_c, const StencilArgs& a, int blocks, hipStream_t s, int v) {
   if constexpr (EPI == EPI_AX) {
     launch_any<EPI, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21,
-               22, 23, 24, 25, 26, 27, 30, 31, 32, 33, 42, 43, 45>(v, const_c, a, blocks, s);
+               22, 23, 24, 25, 26, 27, 30, 31, 32, 33, 42, 43, 44, 45>(v, const_c, a, blocks, s);
   } else {
     // every epilogue has the two default shapes: 256-wide (small grids) and 512-wide strips
     if (v == kSmallVariant) launch_v<EPI, kSmallVariant>(const_c, a, blocks, s);
-    else if (v == kCachedVariant) launch_v<EPI, kCachedVariant>(const_c, a, blocks, s);
+    else if (v == kSolveVariant) launch_v<EPI, kSolveVariant>(const_c, a, blocks, s);
     else launch_v<EPI, kDefaultVariant>(const_c, a, blocks, s);
   }
 }
@@ -430,14 +428,20 @@ void launch_point_t(bool const_c, const PointArgs& a, int blocks, hipStream_t s)
 }  // namespace
 
 int stencil_rows_per_block(int n, int rows) {
-  // ~2048 tiles (8 per CU) counted in 256-wide strips: 32-row bands at 4096^2 (measured
-  // best, tools/tune_stencil.py); short bands keep small grids busy; long bands amortise
-  // the two halo rows.  A multiple of the 4-row unroll.
-  const int tiles_x = (n + kStencilThreads - 1) / kStencilThreads;
-  long want_y = 2048 / tiles_x;
-  if (want_y < 1) want_y = 1;
-  int rpb = (int)((rows + want_y - 1) / want_y);
-  rpb = (rpb + 3) / 4 * 4;
+  // Rows of 4608 points or fewer: ~2048 tiles (8 per CU) counted in 256-wide strips -- 32-row
+  // bands at 4096^2; short bands keep small grids busy.  Longer rows: 16-row bands (measured
+  // best at n = 5792 .. 16384 for both media, profiles/r01j_*, r01k_*).  A multiple of the
+  // 4-row unroll.
+  int rpb;
+  if (n > kLongRow) {
+    rpb = 16;
+  } else {
+    const int tiles_x = (n + kStencilThreads - 1) / kStencilThreads;
+    long want_y = 2048 / tiles_x;
+    if (want_y < 1) want_y = 1;
+    rpb = (int)((rows + want_y - 1) / want_y);
+    rpb = (rpb + 3) / 4 * 4;
+  }
   if (rpb < 4) rpb = 4;
   if (rpb > 256) rpb = 256;
   if (rpb > rows) rpb = rows > 0 ? rows : 1;
@@ -445,13 +449,18 @@ int stencil_rows_per_block(int n, int rows) {
 }
 
 int stencil_resolve_variant(int epi, int requested, int n) {
-  // 256-wide strips for small grids.  Every epilogue streams u non-temporally: with the
-  // second input (b / r) prefetched alongside 1/c^2 the shifted-Laplace epilogues gain too
-  // (tools/tune_gmres_variant.py, profiles/r01i_tune_gmres_variant.log).
-  const int autov = n < 2048 ? kSmallVariant : kDefaultVariant;
+  // 256-wide strips below n = 2048.  Above, the plain apply (EPI_AX) loads u through the
+  // cache: on inputs no earlier launch left on the die -- every apply of a solve -- that is
+  // the fastest shape at every size measured (n = 4096 .. 16384, profiles/r01l_* .. r01p_*).
+  // The solve epilogues, whose input the previous kernel has just written, gain ~1 % from
+  // NT u loads on rows up to kLongRow (tools/tune_gmres_variant.py,
+  // profiles/r01i_tune_gmres_variant.log) and lose 4-8 % beyond.
+  int autov = kDefaultVariant;
+  if (n < 2048) autov = kSmallVariant;
+  else if (epi != EPI_AX && n <= kLongRow) autov = kSolveVariant;
   if (requested < 0) return autov;
   if (epi == EPI_AX) return stencil_variant_valid(requested) ? requested : autov;
-  return (requested == kSmallVariant || requested == kDefaultVariant || requested == kCachedVariant)
+  return (requested == kSmallVariant || requested == kDefaultVariant || requested == kSolveVariant)
              ? requested
              : autov;
 }
@@ -471,7 +480,7 @@ int stencil_grid_blocks(int n, int rows, int rows_per_block, int row_step) {
 
 
 int stencil_default_variant() { return kDefaultVariant; }
-bool stencil_variant_valid(int v) { return (v >= 0 && v <= 27) || (v >= 30 && v <= 33) || v == 42 || v == 43 || v == 45; }
+bool stencil_variant_valid(int v) { return (v >= 0 && v <= 27) || (v >= 30 && v <= 33) || (v >= 42 && v <= 45); }
 
 void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_out[1],
                     hipStream_t stream, int variant) {

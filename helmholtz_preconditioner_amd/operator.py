@@ -215,11 +215,20 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
     def apply_device(self, x: DeviceVector, y: DeviceVector, mode: int = _ffi.HH_APPLY_A):
         check(lib.hh_op_apply_dev(self.handle, x.handle, y.handle, int(mode)))
 
-    def time_apply(self, x: DeviceVector, y: DeviceVector, iters: int, mode: int = _ffi.HH_APPLY_A):
-        """(total_ms, avg stencil-kernel ms) over `iters` back-to-back device applies."""
+    def time_apply(self, x, y, iters: int, mode: int = _ffi.HH_APPLY_A):
+        """(total_ms, avg stencil-kernel ms) over `iters` back-to-back device applies.
+        ``x``/``y`` may be equal-length lists of DeviceVectors: apply i then maps
+        x[i % len] -> y[i % len] (no apply re-reads what the previous one left in cache)."""
+        xs = list(x) if isinstance(x, (list, tuple)) else [x]
+        ys = list(y) if isinstance(y, (list, tuple)) else [y]
+        if len(xs) != len(ys) or not xs:
+            raise ValueError("x and y must be DeviceVectors or equal-length lists of them")
+        raw = lambda v: v.handle.value if isinstance(v.handle, ctypes.c_void_p) else v.handle
+        hx = (ctypes.c_void_p * len(xs))(*[raw(v) for v in xs])
+        hy = (ctypes.c_void_p * len(ys))(*[raw(v) for v in ys])
         t, k = ctypes.c_double(), ctypes.c_double()
-        check(lib.hh_op_time_apply(self.handle, x.handle, y.handle, int(mode), int(iters),
-                                   ctypes.byref(t), ctypes.byref(k)))
+        check(lib.hh_op_time_apply_set(self.handle, hx, hy, len(xs), int(mode), int(iters),
+                                       ctypes.byref(t), ctypes.byref(k)))
         return t.value, k.value
 
     def tune(self, variant: int = -1, rows_per_block: int = 0, grid_blocks: int = 0):

@@ -160,6 +160,12 @@ int hh_op_apply_dev(hh_op* op, const hh_vec* x, hh_vec* y, int mode);
  * recorded around the interior stencil launch of every apply. */
 int hh_op_time_apply(hh_op* op, const hh_vec* x, hh_vec* y, int mode, int iters,
                      double* total_ms, double* kernel_ms);
+/* The same over `nvec` distinct (x, y) pairs taken round-robin (apply i: xs[i % nvec] ->
+ * ys[i % nvec]): with nvec * 32 B/unknown well above the 256 MiB Infinity Cache no apply can
+ * reuse lines an earlier one left on the die, as in a solve, where each apply reads a new
+ * vector. */
+int hh_op_time_apply_set(hh_op* op, const hh_vec* const* xs, hh_vec* const* ys, int nvec,
+                         int mode, int iters, double* total_ms, double* kernel_ms);
 
 /* ------------------------------------------------------------------ solve */
 /* Replaces scipy.sparse.linalg.gmres(A, f_vec, M=M, tol=1e-3, callback=...)
@@ -202,6 +208,10 @@ int hh_tune_krylov(int nt_loads, int blocks);
  * `iters` launches; outputs the average kernel ms and the probe's bytes per point. */
 int hh_op_probe_stream(hh_op* op, int kind, int blocks, const hh_vec* x, hh_vec* y, int iters,
                        double* kernel_ms, int* bytes_per_point);
+/* The same over `nvec` (x, y) pairs taken round-robin (cold inputs, as hh_op_time_apply_set). */
+int hh_op_probe_stream_set(hh_op* op, int kind, int blocks, const hh_vec* const* xs,
+                           hh_vec* const* ys, int nvec, int iters, double* kernel_ms,
+                           int* bytes_per_point);
 
 /* Optional per-call counters of the last hh_gmres / hh_op_time_apply. */
 typedef struct {

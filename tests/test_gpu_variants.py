@@ -17,8 +17,8 @@ from oracle import helmholtz_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-# XM_LDS; cached / NT u loads; 256- and 512-wide strips; prefetch depth 1 and 2
-APPLY_VARIANTS = [6, 18, 24, 30, 42, 45]
+# LDS and wave-shuffle exchange; cached / NT u loads; 256- and 512-wide strips; prefetch 1 and 2
+APPLY_VARIANTS = [6, 8, 18, 24, 30, 32, 42, 44, 45]
 SOLVE_VARIANTS = [18, 30, 42]  # the shapes every epilogue is instantiated for
 
 

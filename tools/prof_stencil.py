@@ -16,6 +16,7 @@ p.add_argument("--medium", default="marmousi")
 p.add_argument("--gmres", action="store_true")
 p.add_argument("--variant", type=int, default=-1)
 p.add_argument("--rpb", type=int, default=0)
+p.add_argument("--rotate", type=int, default=3, help="distinct (x, y) pairs, as bench.py")
 a = p.parse_args()
 n = a.n
 om, h, eta = H.problem_params(n, 12, 100.0, 2.0)
@@ -23,9 +24,10 @@ cm = H.marmousi_like_c_mat(n) if a.medium == "marmousi" else H.constant_c_mat(n)
 A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm)
 if a.variant >= 0 or a.rpb > 0:
     A.tune(variant=a.variant, rows_per_block=a.rpb)
-x, y = A.vector(), A.vector()
-x.fill_hash(7)
-tot, k = A.time_apply(x, y, a.iters)
+xs, ys = [A.vector() for _ in range(a.rotate)], [A.vector() for _ in range(a.rotate)]
+for j, v in enumerate(xs):
+    v.fill_hash(7 + j)
+tot, k = A.time_apply(xs, ys, a.iters)
 bpp = A.bytes_per_point
 print(f"n={n} iters={a.iters} kernel {k*1e3:.1f} us  {bpp*n*n/(k*1e-3)/1e9:.0f} GB/s  total/iter {tot/a.iters*1e3:.1f} us")
 if a.gmres:

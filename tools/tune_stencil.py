@@ -20,6 +20,8 @@ p.add_argument("--variants", default="6,7,9,24,30,31,33")
 p.add_argument("--grids", default="0,1280")
 p.add_argument("--rpbs", default="16,32,64")
 p.add_argument("--medium", default="marmousi")
+p.add_argument("--rotate", type=int, default=1,
+               help="distinct (x, y) pairs applied round-robin (>1: no cross-launch cache reuse)")
 a = p.parse_args()
 variants = [int(v) for v in a.variants.split(",")]
 rpbs = [int(v) for v in a.rpbs.split(",")]
@@ -29,7 +31,7 @@ grids = [int(v) for v in a.grids.split(",")]
 def vname(v):
     w = v % 24
     return f"{['lds', 'direct', 'shfl'][w % 3]} pf{(w // 3) % 2 + 1}{' nt' if (w // 6) % 2 else ''}" \
-           f"{' ntu' if w >= 12 else ''}{' w512' if v >= 24 else ''}"
+           f"{' ntu' if w >= 12 else ''}{' w512' if v % 48 >= 24 else ''}{' occ6' if v >= 48 else ''}"
 
 # correctness on a ragged grid: every variant bit-identical to variant 0
 n = 1000
@@ -53,8 +55,10 @@ n = a.n
 om, h, eta = H.problem_params(n, 12, 100.0, 2.0)
 cm = H.marmousi_like_c_mat(n) if a.medium == "marmousi" else H.constant_c_mat(n)
 A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm)
-x, y = A.vector(), A.vector()
-x.fill_hash(7)
+xs, ys = [A.vector() for _ in range(a.rotate)], [A.vector() for _ in range(a.rotate)]
+for k, v in enumerate(xs):
+    v.fill_hash(7 + k)
+x, y = (xs, ys) if a.rotate > 1 else (xs[0], ys[0])
 bpp = A.bytes_per_point
 res = {}
 for rnd in range(a.rounds):
@@ -76,11 +80,11 @@ if not A.constant_medium:
     km = ctypes.c_double()
     ks = []
     for _ in range(a.rounds):
-        _ffi.check(_ffi.lib.hh_op_probe_stream(A.handle, 0, 8192, x.handle, y.handle, a.iters, ctypes.byref(km), ctypes.byref(ctypes.c_int())))
+        _ffi.check(_ffi.lib.hh_op_probe_stream(A.handle, 0, 8192, xs[0].handle, ys[0].handle, a.iters, ctypes.byref(km), ctypes.byref(ctypes.c_int())))
         ks.append(km.value)
     k = min(ks)
     print(f"probe y=u*ic (same 40 B/pt, no neighbours): {k*1e3:.1f} us = {bpp*n*n/(k*1e-3)/1e9:.0f} GB/s")
-print(f"n={n} medium={a.medium} bytes/pt={bpp}")
+print(f"n={n} medium={a.medium} bytes/pt={bpp} rotate={a.rotate}")
 print("GB/s(best)  variant               rpb  grid  kernel_us(min)  kernel_us(median)")
 for gbs, v, r, g, k, med in rows:
     desc = f"{v:2d} {vname(v)}"
