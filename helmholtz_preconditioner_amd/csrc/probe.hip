@@ -5,6 +5,8 @@
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
 
+#include <cmath>
+
 namespace hh {
 namespace {
 
@@ -88,6 +90,77 @@ __global__ __launch_bounds__(kT) void p6(const double2* __restrict__ u, const do
   }
 }
 
+// P7/P8: the stencil's traversal without its arithmetic or neighbours.  A 512-thread block
+// owns a 512-wide strip x 32-row band and marches it with one row of prefetch (NT loads and
+// stores, 40 B/point).  P7 deals tiles to XCDs in contiguous ranges as the stencil does; P8
+// takes tiles in plain blockIdx order.
+template <bool XCD, int RB>
+__global__ __launch_bounds__(512) void pmarch(const double2* __restrict__ u,
+                                              const double* __restrict__ ic,
+                                              double2* __restrict__ y, int n) {
+  constexpr int TW = 512;
+  const int tiles_x = (n + TW - 1) / TW, tiles_y = (n + RB - 1) / RB;
+  const int ntiles = tiles_x * tiles_y;
+  int t = blockIdx.x;
+  if (XCD) {
+    const int per = (ntiles + 7) / 8;
+    t = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  }
+  if (t >= ntiles) return;
+  const int i = min((t % tiles_x) * TW + (int)threadIdx.x, n - 1);
+  const int r0 = (t / tiles_x) * RB, r1 = min(r0 + RB, n);
+  auto ld = [&](int r, double2& uv, double& c) {
+    const size_t p = (size_t)r * n + i;
+    uv = make_double2(__builtin_nontemporal_load(&u[p].x), __builtin_nontemporal_load(&u[p].y));
+    c = __builtin_nontemporal_load(&ic[p]);
+  };
+  double2 ua, ub;
+  double ca, cb;
+  ld(r0, ua, ca);
+  for (int r = r0; r < r1; r += 2) {
+    ld(min(r + 1, r1 - 1), ub, cb);
+    double2* q = y + (size_t)r * n + i;
+    __builtin_nontemporal_store(ua.x * ca, &q->x);
+    __builtin_nontemporal_store(ua.y * ca, &q->y);
+    ld(min(r + 2, r1 - 1), ua, ca);
+    if (r + 1 < r1) {
+      q += n;
+      __builtin_nontemporal_store(ub.x * cb, &q->x);
+      __builtin_nontemporal_store(ub.y * cb, &q->y);
+    }
+  }
+}
+
+// P13/P14: a naive 5-point gather -- one point per thread, no marching: u at (i, j), (i +- 1,
+// j), (i, j +- 1) through the cache (the neighbours' lines are L2 / Infinity-Cache hits of
+// the blocks working on the adjacent rows at the same time), 1/c^2 and y non-temporal; one
+// block per 256 points in address order.  P13: blockIdx order (consecutive blocks on
+// different XCDs); P14: XCD k takes a contiguous range of rows.
+template <bool XCD>
+__global__ __launch_bounds__(256) void pnaive(const double2* __restrict__ u,
+                                              const double* __restrict__ ic,
+                                              double2* __restrict__ y, int n) {
+  const long nb = ((long)n * n + 255) / 256;
+  long b = blockIdx.x;
+  if (XCD) {
+    const long per = (nb + 7) / 8;
+    b = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  }
+  const long p = b * 256 + threadIdx.x;
+  if (b >= nb || p >= (long)n * n) return;
+  const int i = (int)(p % n), j = (int)(p / n);
+  const double2 z = make_double2(0.0, 0.0);
+  const double2 c = u[p];
+  const double2 w = i > 0 ? u[p - 1] : z;
+  const double2 e = i + 1 < n ? u[p + 1] : z;
+  const double2 sv = j > 0 ? u[p - n] : z;
+  const double2 nv = j + 1 < n ? u[p + n] : z;
+  const double k = __builtin_nontemporal_load(&ic[p]);
+  const double2 r = make_double2(k * c.x + w.x + e.x + sv.x + nv.x, k * c.y + w.y + e.y + sv.y + nv.y);
+  __builtin_nontemporal_store(r.x, &y[p].x);
+  __builtin_nontemporal_store(r.y, &y[p].y);
+}
+
 }  // namespace
 
 int launch_probe_kind(int kind, int blocks, const double2* u, const double* ic, double2* y,
@@ -101,6 +174,35 @@ int launch_probe_kind(int kind, int blocks, const double2* u, const double* ic, 
     case 4: hipLaunchKernelGGL(p4, g, b, 0, s, u, ic, y, len); return 24;
     case 5: hipLaunchKernelGGL(p5, g, b, 0, s, u, ic, y, len); return 40;
     case 6: hipLaunchKernelGGL(p6, g, b, 0, s, u, ic, y, len); return 32;
+    case 7: case 8: case 9: case 10: case 11: case 12: {
+      // marching tiles over the n x n grid (len = n^2); `blocks` is ignored.  7: 32-row bands
+      // XCD map; 8: 32-row bands blockIdx order; 9 / 10 / 11 / 12: 8 / 16 / 64 / 128-row
+      // bands, XCD map
+      const int n = (int)llround(std::sqrt((double)len));
+      if ((size_t)n * n != len) return 0;
+      const int rb = kind == 9 ? 8 : kind == 10 ? 16 : kind == 11 ? 64 : kind == 12 ? 128 : 32;
+      const int tiles = ((n + 511) / 512) * ((n + rb - 1) / rb);
+      const dim3 gm((tiles + 7) / 8 * 8), bm(512);
+      switch (kind) {
+        case 7: hipLaunchKernelGGL((pmarch<true, 32>), gm, bm, 0, s, u, ic, y, n); break;
+        case 8: hipLaunchKernelGGL((pmarch<false, 32>), gm, bm, 0, s, u, ic, y, n); break;
+        case 9: hipLaunchKernelGGL((pmarch<true, 8>), gm, bm, 0, s, u, ic, y, n); break;
+        case 10: hipLaunchKernelGGL((pmarch<true, 16>), gm, bm, 0, s, u, ic, y, n); break;
+        case 11: hipLaunchKernelGGL((pmarch<true, 64>), gm, bm, 0, s, u, ic, y, n); break;
+        default: hipLaunchKernelGGL((pmarch<true, 128>), gm, bm, 0, s, u, ic, y, n); break;
+      }
+      return 40;
+    }
+    case 13:
+    case 14: {
+      const int n = (int)llround(std::sqrt((double)len));
+      if ((size_t)n * n != len) return 0;
+      const long nb = ((long)len + 255) / 256;
+      const dim3 gn((unsigned)((nb + 7) / 8 * 8)), bn(256);
+      if (kind == 13) hipLaunchKernelGGL(pnaive<false>, gn, bn, 0, s, u, ic, y, n);
+      else hipLaunchKernelGGL(pnaive<true>, gn, bn, 0, s, u, ic, y, n);
+      return 40;
+    }
     default: return 0;
   }
 }

@@ -21,10 +21,16 @@ hy = (ctypes.c_void_p * R)(*[raw(v) for v in ys])
 print(f"n={n}, {R} rotating (x, y) pairs")
 names = ["1pt/lane u16 ic8 y16", "2pt/lane adjacent (ic16, u/y 32B stride)",
          "2pt/lane wave-strided (ic8)", "copy y=u", "read-only u+ic", "1pt/lane nontemporal",
-         "copy 2pt/lane adjacent"]
+         "copy 2pt/lane adjacent", "stencil traversal, XCD map (no arithmetic)",
+         "stencil traversal, blockIdx order", "stencil traversal, 8-row bands",
+         "stencil traversal, 16-row bands", "stencil traversal, 64-row bands",
+         "stencil traversal, 128-row bands", "naive 5-point gather, blockIdx order",
+         "naive 5-point gather, XCD row ranges"]
 km, bpp = ctypes.c_double(), ctypes.c_int()
 for blocks in (2048, 8192, 32768):
-    for kind in range(7):
+    for kind in range(15):
+        if kind >= 7 and blocks != 2048:
+            continue  # the marching probes size their own grid
         best = 1e9
         for _ in range(3):
             _ffi.check(_ffi.lib.hh_op_probe_stream_set(A.handle, kind, blocks, hx, hy, R, 21,
