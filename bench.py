@@ -270,16 +270,22 @@ def main():
         tg = float(ctx.allreduce_max([time.perf_counter() - t0])[0])
         its = len(hist)
         # algorithmic bytes / iteration (CGS, lazy normalisation): SpMV 40N + projection
-        # 16(j+2)N + update 16(j+3)N, + preconditioner sweeps 56N each (SURVEY 8d style)
+        # 16(j+2)N + update 16(j+3)N (SURVEY 8d style), + the preconditioner's own traffic:
+        # none for Jacobi (fused into the SpMV) and for the two-sweep shifted-Laplace M on one
+        # slab (M A in one launch, csrc/sl_fused.hip: 40 B/unknown in all); otherwise the
+        # stencil + sweep launches, 16 + 56 B per further sweep.
         js = [i % args.restart for i in range(its)]
         N = float(n) * n
-        pre = {"sl": bpp + 16 + 56 * (args.sl_sweeps - 1), "jacobi": 0, "none": 0}[args.precond]
+        fused = args.sl_sweeps == 2 and world == 1 and args.virtual_slabs == 1
+        sl_extra = 0 if fused else bpp + 16 + 56 * (args.sl_sweeps - 1)
+        pre = {"sl": sl_extra, "jacobi": 0, "none": 0}[args.precond]
         gbytes = sum((bpp + pre) * N + 16 * (j + 2) * N + 16 * (j + 3) * N for j in js)
         result["gmres"] = {
             "iters_per_s": round(its / tg, 3),
             "iterations": its,
             "restart": args.restart,
-            "precond": {"sl": f"shifted-Laplace(beta=0.5, {args.sl_sweeps} damped-Jacobi sweeps)",
+            "precond": {"sl": f"shifted-Laplace(beta=0.5, {args.sl_sweeps} damped-Jacobi sweeps"
+                              f"{', fused with the SpMV' if fused else ''})",
                         "jacobi": "Jacobi", "none": "none"}[args.precond],
             "ms_per_iter": round(tg * 1e3 / its, 4),
             "algorithmic_GBps": round(gbytes / tg / 1e9, 1),

@@ -108,6 +108,7 @@ struct hh_op {
   double beta = 0.5, damping = 1.0;
   int sweeps = 1;
   double2 mshift = make_double2(1.0, 0.0);
+  bool sl_fuse = true;  // two-sweep M A in one launch (sl_fused.hip) where it applies
   // reductions
   double* partials = nullptr;
   size_t partials_cap = 0;  // doubles
@@ -262,6 +263,37 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
   return nparts;
 }
 
+// w = M A (s v) for the two-sweep shifted-Laplace M in one launch (sl_fused.hip): T and the
+// first sweep never leave the chip.  Single slab of a single rank only (the fused band reads
+// v two rows beyond its own, which a cross-slab halo of one row does not carry).
+bool sl_fused_applies(const hh_op* op) {
+  return op->sl_fuse && op->sweeps == 2 && op->slabs.size() == 1 && op->ctx->world == 1;
+}
+void run_sl2(hh_op* op, const double2* v, const double* vs, double2* out) {
+  const Slab& s = op->slabs[0];
+  StencilArgs a{};
+  a.u = v + s.off;
+  a.halo_lo = op->zero_row;
+  a.halo_hi = op->zero_row;
+  a.invc2 = op->const_c ? nullptr : s.invc2;
+  a.invc2_const = op->invc2_const;
+  a.tab_i = op->tab_i;
+  a.tab_j = s.tab_j;
+  a.n = op->n;
+  a.nl = s.nl;
+  a.row_begin = 0;
+  a.row_end = s.nl;
+  a.rows_per_block = op->rpb_override > 0 ? std::min(op->rpb_override, s.nl) : s.rpb;
+  a.mshift = op->mshift;
+  a.damping = op->damping;
+  a.in_scale = vs;
+  a.out0 = out + s.off;
+  a.stop = op->stop_flag;
+  launch_sl2(op->const_c, a, op->ctx->stream);
+  HIPC(hipGetLastError());
+  op->stats.spmv_count++;
+}
+
 // Pointwise op over all local slabs; returns partial rows written.
 int run_point(hh_op* op, int pt, const double2* in0, double2* out0, bool shifted) {
   hh_ctx* c = op->ctx;
@@ -395,6 +427,10 @@ void apply_MA(hh_op* op, const double2* v, const double* vs, double2* out) {
       run_stencil(op, EPI_JAC, v, vs, nullptr, out, nullptr, false);
       break;
     case HH_PREC_SHIFTED_LAPLACE: {
+      if (sl_fused_applies(op)) {
+        run_sl2(op, v, vs, out);
+        break;
+      }
       ensure_scratch(op);
       double2* z1 = sl_first_dst(op, out);
       run_stencil(op, EPI_SL_FIRST, v, vs, nullptr, op->scrT, z1, true);
@@ -1170,6 +1206,13 @@ HH_API int hh_op_time_apply_set(hh_op* op, const hh_vec* const* xs, hh_vec* cons
   }
   (void)hipEventDestroy(t0);
   (void)hipEventDestroy(t1);
+  GUARD_END
+}
+
+HH_API int hh_op_sl_fusion(hh_op* op, int enable) {
+  GUARD_BEGIN
+  REQUIRE(op, "null op");
+  op->sl_fuse = enable != 0;
   GUARD_END
 }
 

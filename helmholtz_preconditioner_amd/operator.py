@@ -236,6 +236,11 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
         results are identical)."""
         check(lib.hh_op_tune(self.handle, int(variant), int(rows_per_block), int(grid_blocks)))
 
+    def sl_fusion(self, enable: bool = True):
+        """Two-sweep shifted-Laplace M: fused M A launch (default) or stencil + sweep pair
+        (identical results; for A/B timing)."""
+        check(lib.hh_op_sl_fusion(self.handle, int(bool(enable))))
+
     def stats(self):
         s = _ffi.HHStats()
         check(lib.hh_op_last_stats(self.handle, ctypes.byref(s)))

@@ -193,6 +193,10 @@ int hh_gmres(hh_op* op, const hh_vec* b, hh_vec* x, double rtol, double atol,
  * persistent grid of that many workgroups (0 = one per tile).  Results are identical
  * for every setting; only speed changes. */
 int hh_op_tune(hh_op* op, int variant, int rows_per_block, int grid_blocks);
+/* Two-sweep shifted-Laplace M: apply M A in one fused launch (default 1) or as the stencil
+ * + sweep pair (0).  Same results bit for bit; the fused form moves 40 instead of 112 B per
+ * unknown.  It applies to a single slab of a single rank; elsewhere the pair runs. */
+int hh_op_sl_fusion(hh_op* op, int enable);
 /* Sweeping preconditioner form (speed / memory only; results agree to rounding):
  *   mode -1 (default) dense transfer matrices when n <= 2048 and the n^3 x 16 B fit in HBM,
  *           else block-Thomas solves;  0 block-Thomas solves (O(n^2 b^2) memory, every solve
