@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--alpha", type=float, default=2.0)
     p.add_argument("--precond", default="sl", choices=["sl", "jacobi", "none"])
     p.add_argument("--sl-sweeps", type=int, default=2)
+    p.add_argument("--stencil", type=int, default=5, choices=[5, 9],
+                   help="5 = the reference's operator; 9 = the 9-point operator (SURVEY row F4)")
     p.add_argument("--gmres-iters", type=int, default=40, help="timed inner GMRES iterations")
     p.add_argument("--restart", type=int, default=20)
     p.add_argument("--no-gmres", action="store_true")
@@ -95,14 +97,15 @@ def local_f1(omega, n, j0, j1, r1=.5, r2=.125):
     return np.exp(-(4 * omega / np.pi) ** 2 * ((x[None, :] - r1) ** 2 + (yy - r2) ** 2)).ravel()
 
 
-def measured_traffic(n, medium, world):
+def measured_traffic(n, medium, world, stencil=5):
     """HBM bytes per stencil launch from the rocprofv3 PMC passes committed under profiles/
     (FETCH_SIZE x2 + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md, calibrated
     on the probe kernels in the same run).  PMC counters cannot be read inside the timed
     run, so this is the committed measurement of the same kernel and workload (None
     otherwise)."""
     path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-    if not (n == 4096 and medium == "marmousi" and world == 1 and os.path.exists(path)):
+    if not (n == 4096 and medium == "marmousi" and world == 1 and stencil == 5
+            and os.path.exists(path)):
         return None, None
     rec = json.load(open(path)).get("stencil_kernel<0")
     if not rec:
@@ -127,7 +130,10 @@ def cpu_baseline(args, n, omega, h, eta, c_mat):
     import numpy as np
     from oracle import helmholtz_oracle as O
     t0 = time.perf_counter()
-    A = O.build_A_matrix(args.b, args.C, eta, omega, h, n, c_mat)
+    if args.stencil == 9:
+        A = O.build_A9_matrix(args.b, args.C, eta, omega, h, n, c_mat)
+    else:
+        A = O.build_A_matrix(args.b, args.C, eta, omega, h, n, c_mat)
     t_build = time.perf_counter() - t0
     rng = np.random.default_rng(0)
     x = rng.standard_normal(n * n) + 1j * rng.standard_normal(n * n)
@@ -144,7 +150,19 @@ def cpu_baseline(args, n, omega, h, eta, c_mat):
                      f"(oracle CSR, {A.nnz} nnz), {t_spmv * 1e3:.1f} ms each; CSR build "
                      f"{t_build:.1f} s untimed"}
     if not args.no_gmres and args.cpu_gmres_iters > 0:
-        if args.precond == "sl":
+        if args.precond == "sl" and args.stencil == 9:
+            import scipy.sparse.linalg
+            Ab = O.build_A9_matrix(args.b, args.C, eta, omega, h, n, c_mat / np.sqrt(1 + 0.5j))
+            dinv = 1.0 / Ab.diagonal()
+
+            def mv(r, sweeps=args.sl_sweeps):
+                r = np.ravel(r)
+                z = 0.7 * dinv * r
+                for _ in range(sweeps - 1):
+                    z = z + 0.7 * dinv * (r - Ab @ z)
+                return z
+            M = scipy.sparse.linalg.LinearOperator(A.shape, matvec=mv, dtype=np.complex128)
+        elif args.precond == "sl":
             M, _ = O.shifted_laplace_jacobi(args.b, args.C, eta, omega, h, n, c_mat, beta=0.5,
                                             sweeps=args.sl_sweeps, damping=0.7)
         elif args.precond == "jacobi":
@@ -181,7 +199,8 @@ def main():
     j0, j1 = dist.slab_bounds(n, world, rank)
     t0 = time.perf_counter()
     c_mat = make_medium(args.medium, n, (j0, j1))
-    A = H.build_A_matrix(args.b, args.C, eta, omega, h, n, c_mat, context=ctx)
+    A = H.build_A_matrix(args.b, args.C, eta, omega, h, n, c_mat, context=ctx,
+                         stencil=args.stencil)
     t_init = time.perf_counter() - t0
     assert (A.row_begin, A.row_end) == (j0, j1)
     bpp = A.bytes_per_point
@@ -225,17 +244,18 @@ def main():
         "data": f"synthetic: {args.medium}-like velocity (seeded), hash-filled complex input, "
                 f"{R} rotating vector pairs",
         "config": {
-            "workload": f"config{args.config or 3}: {n}x{n} {args.medium} velocity, matrix-free PML stencil apply "
+            "workload": f"config{args.config or 3}: {n}x{n} {args.medium} velocity, matrix-free "
+                        f"{args.stencil}-point PML stencil apply "
                         f"(+ GMRES({args.restart}) {args.precond}-preconditioned)",
             "n": n, "unknowns": n * n, "wave_num": args.wave_num, "b": args.b, "C": args.C,
-            "alpha": args.alpha, "bytes_per_unknown": bpp,
+            "alpha": args.alpha, "bytes_per_unknown": bpp, "stencil_points": args.stencil,
             "parallelism": f"row-slab x{world} (RCCL halo)" if world > 1 else "single GPU",
         },
         "pct_hbm_peak": round(100.0 * value / (HBM_PEAK_GBPS * world), 2),
         "device_ms_per_step": round(dev_ms / args.steps, 5),
         "init_s": round(t_init, 3),
     }
-    traffic, traffic_src = measured_traffic(n, args.medium, world)
+    traffic, traffic_src = measured_traffic(n, args.medium, world, args.stencil)
     result["roofline"] = {
         "bound": "hbm",
         "achieved": round(achieved_min, 1),
@@ -244,7 +264,8 @@ def main():
         "frac": round(achieved_min / HBM_PEAK_GBPS, 4),
         "traffic": traffic,
         "traffic_source": traffic_src,
-        "kernel": "stencil_kernel<EPI_AX,false> (interior rows)",
+        "kernel": f"stencil_kernel<EPI_AX,{'true' if A.constant_medium else 'false'},"
+                  f"S9={'true' if args.stencil == 9 else 'false'}> (interior rows)",
         "kernel_ms": round(kern_ms, 5),
         "bytes_per_launch": bpp * interior_rows * n,
     }
@@ -276,7 +297,8 @@ def main():
         # stencil + sweep launches, 16 + 56 B per further sweep.
         js = [i % args.restart for i in range(its)]
         N = float(n) * n
-        fused = args.sl_sweeps == 2 and world == 1 and args.virtual_slabs == 1
+        fused = (args.sl_sweeps == 2 and world == 1 and args.virtual_slabs == 1
+                 and args.stencil == 5)
         sl_extra = 0 if fused else bpp + 16 + 56 * (args.sl_sweeps - 1)
         pre = {"sl": sl_extra, "jacobi": 0, "none": 0}[args.precond]
         gbytes = sum((bpp + pre) * N + 16 * (j + 2) * N + 16 * (j + 3) * N for j in js)

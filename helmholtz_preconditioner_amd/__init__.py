@@ -18,7 +18,7 @@ from .media import (constant_c_mat, init_c1_f1, init_c1_f2, init_c1_mat, init_c2
                     init_c2_f2, init_c2_mat, init_f1_mat, init_f2_mat, marmousi_like_c_mat,
                     problem_params)
 from .operator import (DeviceOperator, DevicePreconditioner, DeviceVector, Jacobi,  # noqa: F401
-                       ShiftedLaplace, Sweeping, build_A_matrix)
+                       ShiftedLaplace, STENCIL9_WEIGHTS, Sweeping, build_A_matrix)
 from .solver import gmres  # noqa: F401
 from .driver import gmres_counter, run_solver, true_relative_residual  # noqa: F401
 from .io import (load_c_mat, load_solution, load_velocity_model, plot_solution,  # noqa: F401
@@ -27,7 +27,7 @@ from . import dist  # noqa: F401
 
 __all__ = [
     "build_A_matrix", "gmres", "DeviceOperator", "DeviceVector", "Jacobi", "ShiftedLaplace",
-    "Sweeping",
+    "Sweeping", "STENCIL9_WEIGHTS",
     "Context", "default_context", "set_default_context", "device_count", "unique_id",
     "init_c1_mat", "init_c2_mat", "init_f1_mat", "init_f2_mat", "init_c1_f1", "init_c1_f2",
     "init_c2_f1", "init_c2_f2", "constant_c_mat", "marmousi_like_c_mat", "problem_params",

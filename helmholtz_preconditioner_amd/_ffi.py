@@ -72,6 +72,7 @@ SIGNATURES = [
                                      c_dp]),
     ("hh_gmres", c_int, [c_void_p, c_void_p, c_void_p, c_double, c_double, c_int, c_long, c_int,
                          c_int, c_dp, c_long, GMRES_CALLBACK, c_void_p, c_lp, c_ip, c_dp, c_dp]),
+    ("hh_op_set_stencil", c_int, [c_void_p, c_int, c_double, c_double, c_double]),
     ("hh_op_sl_fusion", c_int, [c_void_p, c_int]),
     ("hh_op_tune", c_int, [c_void_p, c_int, c_int, c_int]),
     ("hh_op_sweep_mode", c_int, [c_void_p, c_int, c_ip]),

@@ -41,6 +41,12 @@ enum PointOp : int {
   PT_COPY_NORM = 3,  // out0 = in0 (if distinct)             acc0 = |out0|^2
 };
 
+// Weights of the 9-point operator: Cartesian share alpha (g = (1 - alpha) / 2 on the
+// line-averaged part) and mass weights c (centre), d (edges), e (corners), c + 4d + 4e = 1.
+struct Stencil9W {
+  double alpha, g, c, d, e;
+};
+
 struct StencilArgs {
   const double2* u;        // input slab [nl][n]
   const double2* halo_lo;  // global row j0-1 (zero row at the bottom boundary)
@@ -64,6 +70,10 @@ struct StencilArgs {
   double2* out1;
   double* partials;        // [blocks][kMaxNorms] when the epilogue accumulates norms
   const int* stop;         // GMRES cycle stop flag: the launch is a no-op once *stop != 0
+  // 9-point operator, selected by tab_r2x != nullptr: R2 = 1/s2 of the local
+  // rows -1 .. nl ([nl + 2], entry r + 1 for row r) and the stencil weights (see stencil.hip)
+  const double2* tab_r2x;
+  Stencil9W w9;
 };
 
 struct PointArgs {
@@ -78,6 +88,8 @@ struct PointArgs {
   double damping;
   double* partials;        // [blocks][kMaxNorms]
   const int* stop;         // as StencilArgs::stop
+  int s9;                  // 1: 9-point operator, diagonal c M - alpha (W + E + S + N)
+  Stencil9W w9;
 };
 
 // CSR export of one slab (assemble.hip).
@@ -94,8 +106,10 @@ struct CsrArgs {
   long long* indptr;       // [local rows + 1], relative to the rank's first entry
   void* indices;           // int32 or int64 global column indices
   double2* data;
+  const double2* tab_r2x;  // 9-point operator (as StencilArgs), or nullptr
+  Stencil9W w9;
 };
-long long csr_rank_nnz(int n, int j0, int j1);
+long long csr_rank_nnz(int n, int j0, int j1, int points = 5);
 void launch_csr_export(const CsrArgs& a, int index_bytes, hipStream_t stream);
 
 // Kernel launchers (kernels.hip).  All are asynchronous on `stream`.

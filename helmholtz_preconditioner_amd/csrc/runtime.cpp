@@ -84,6 +84,7 @@ struct Slab {
   size_t off = 0;              // element offset inside the rank-local vector
   double* invc2 = nullptr;     // [nl][n]
   double2* tab_j = nullptr;    // [nl][4]
+  double2* tab_r2x = nullptr;  // 9-point only: R2 = 1/s2 of local rows -1 .. nl ([nl + 2])
   double2* halo_lo_buf = nullptr;
   double2* halo_hi_buf = nullptr;
   int rpb = 16;
@@ -109,6 +110,9 @@ struct hh_op {
   int sweeps = 1;
   double2 mshift = make_double2(1.0, 0.0);
   bool sl_fuse = true;  // two-sweep M A in one launch (sl_fused.hip) where it applies
+  // stencil: 5 (the reference's operator) or 9 (hh_op_set_stencil)
+  int points = 5;
+  Stencil9W w9{1.0, 0.0, 1.0, 0.0, 0.0};
   // reductions
   double* partials = nullptr;
   size_t partials_cap = 0;  // doubles
@@ -209,6 +213,8 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
     a.mshift = shifted ? op->mshift : make_double2(1.0, 0.0);
     a.damping = op->damping;
     a.in_scale = in_scale;
+    a.tab_r2x = op->points == 9 ? s.tab_r2x : nullptr;
+    a.w9 = op->w9;
     a.in1 = in1 ? in1 + s.off : nullptr;
     a.out0 = out0 ? out0 + s.off : nullptr;
     a.out1 = out1 ? out1 + s.off : nullptr;
@@ -267,7 +273,8 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
 // first sweep never leave the chip.  Single slab of a single rank only (the fused band reads
 // v two rows beyond its own, which a cross-slab halo of one row does not carry).
 bool sl_fused_applies(const hh_op* op) {
-  return op->sl_fuse && op->sweeps == 2 && op->slabs.size() == 1 && op->ctx->world == 1;
+  return op->sl_fuse && op->sweeps == 2 && op->slabs.size() == 1 && op->ctx->world == 1 &&
+         op->points == 5;
 }
 void run_sl2(hh_op* op, const double2* v, const double* vs, double2* out) {
   const Slab& s = op->slabs[0];
@@ -312,6 +319,8 @@ int run_point(hh_op* op, int pt, const double2* in0, double2* out0, bool shifted
     a.damping = op->damping;
     a.partials = op->partials + (size_t)nparts * kMaxNorms;
     a.stop = op->stop_flag;
+    a.s9 = op->points == 9 ? 1 : 0;
+    a.w9 = op->w9;
     const int blocks = point_blocks((size_t)s.nl * op->n);
     REQUIRE((size_t)(nparts + blocks) * kMaxNorms <= op->partials_cap,
             "partials workspace too small for the pointwise launch");
@@ -822,6 +831,7 @@ static void op_release(hh_op* op) {
   for (Slab& s : op->slabs) {
     dfree(s.invc2);
     dfree(s.tab_j);
+    dfree(s.tab_r2x);
     dfree(s.halo_lo_buf);
     dfree(s.halo_hi_buf);
   }
@@ -919,6 +929,7 @@ HH_API int hh_op_set_precond(hh_op* op, int kind, double beta, int sweeps, doubl
     REQUIRE(damping > 0, "damping must be positive");
   }
   if (is_sweep(kind)) {
+    REQUIRE(op->points == 5, "the sweeping preconditioner is built for the 5-point operator");
     // sequential in the layer index: no row-slab sharding (SURVEY 8e -> replicas only)
     REQUIRE(op->ctx->world == 1 && op->slabs.size() == 1,
             "the sweeping preconditioner needs the whole grid on one rank and one slab");
@@ -1005,7 +1016,7 @@ HH_API int hh_op_diagonal(hh_op* op, double* d) {
 HH_API int hh_op_csr_nnz(hh_op* op, int64_t* nnz) {
   GUARD_BEGIN
   REQUIRE(op && nnz, "null argument");
-  *nnz = csr_rank_nnz(op->n, op->jb, op->je);
+  *nnz = csr_rank_nnz(op->n, op->jb, op->je, op->points);
   GUARD_END
 }
 
@@ -1018,7 +1029,7 @@ HH_API int hh_op_export_csr(hh_op* op, int64_t* indptr, void* indices, int index
           "n^2 >= 2^31: int32 column indices overflow (use index_bytes = 8)");
   HIPC(hipSetDevice(op->ctx->device));
   hipStream_t s = op->ctx->stream;
-  const long long nnz = csr_rank_nnz(op->n, op->jb, op->je);
+  const long long nnz = csr_rank_nnz(op->n, op->jb, op->je, op->points);
   const size_t rows = op->nloc;
   long long* d_ptr = dalloc<long long>(rows + 1);
   void* d_idx = nullptr;
@@ -1046,6 +1057,8 @@ HH_API int hh_op_export_csr(hh_op* op, int64_t* indptr, void* indices, int index
       a.indptr = d_ptr;
       a.indices = d_idx;
       a.data = d_val;
+      a.tab_r2x = op->points == 9 ? sl.tab_r2x : nullptr;
+      a.w9 = op->w9;
       if (sl.nl > 0) launch_csr_export(a, index_bytes, s);
     }
     HIPC(hipGetLastError());
@@ -1206,6 +1219,35 @@ HH_API int hh_op_time_apply_set(hh_op* op, const hh_vec* const* xs, hh_vec* cons
   }
   (void)hipEventDestroy(t0);
   (void)hipEventDestroy(t1);
+  GUARD_END
+}
+
+HH_API int hh_op_set_stencil(hh_op* op, int points, double alpha, double c, double d) {
+  GUARD_BEGIN
+  REQUIRE(op, "null op");
+  REQUIRE(points == 5 || points == 9, "points must be 5 or 9 (got %d)", points);
+  REQUIRE(points == 5 || !is_sweep(op->pkind),
+          "the sweeping preconditioner is built for the 5-point operator");
+  HIPC(hipSetDevice(op->ctx->device));
+  if (points == 9) {
+    REQUIRE(std::isfinite(alpha) && std::isfinite(c) && std::isfinite(d), "non-finite weights");
+    // R2 = 1/s2(jh) of every local row and the two beyond the slab (1-based j = j0 .. j1 + 1;
+    // at the grid edges they multiply the zero Dirichlet rows only)
+    for (Slab& sl : op->slabs) {
+      if (sl.tab_r2x) continue;
+      std::vector<double2> t((size_t)sl.nl + 2);
+      for (int k = 0; k < sl.nl + 2; ++k) {
+        const double j = sl.j0 + k;  // local row k - 1 -> 1-based j0 + k
+        t[k] = d2(1.0 / s2(j * op->h, op->C, op->eta, op->omega));
+      }
+      sl.tab_r2x = dalloc<double2>(t.size());
+      HIPC(hipMemcpy(sl.tab_r2x, t.data(), t.size() * sizeof(double2), hipMemcpyHostToDevice));
+    }
+    op->w9 = Stencil9W{alpha, (1.0 - alpha) / 2.0, c, d, (1.0 - c - 4.0 * d) / 4.0};
+  } else {
+    op->w9 = Stencil9W{1.0, 0.0, 1.0, 0.0, 0.0};
+  }
+  op->points = points;
   GUARD_END
 }
 

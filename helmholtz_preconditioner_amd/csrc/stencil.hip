@@ -14,6 +14,17 @@
 // is 1/c^2 (absent for a constant medium).  Algorithmic HBM bytes per point:
 // 16 (read u) + 16 (write y) + 8 (read 1/c^2) = 40 B (32 B for constant c).
 //
+// 9-point operator (no reference counterpart, the reference is 5-point only,
+// code.py:216-218): alpha x the 5-point operator above + (1 - alpha) x its line-averaged form
+// (each second difference averaged over the two neighbouring lines, with those lines' PML
+// factors) + the mass term spread over the 9 points with weights c, d, e (c + 4d + 4e = 1):
+//   SW: g (Wm + Sm) + e M   S: alpha S - g (Wm + Em) + d M   SE: g (Em + Sp) + e M
+//   W : alpha W - g (Sm + Nm) + d M   C: c M - alpha (W + E + S + N)   E: alpha E - g (Sp + Np) + d M
+//   NW: g (Wp + Nm) + e M   N: alpha N - g (Wp + Ep) + d M   NE: g (Ep + Np) + e M
+// with g = (1 - alpha) / 2, M = OM R1 / c^2 at the centre, Wm/Em/Wp/Ep = AW/AE x R2 of rows
+// j-1 / j+1 and Sm/Nm/Sp/Np = BS/BN x R1 of columns i-1 / i+1.  Same HBM bytes as the 5-point
+// apply (40 B/pt): the diagonal neighbours come from a 4-row LDS ring.
+//
 // Kernel shape: a block owns a 256-wide strip of i and marches a band of rows in j with a
 // three-row register window (u_{j-1}, u_j, u_{j+1}) plus a one-row prefetch, so every u is
 // read from HBM once; the W/E neighbours are exchanged through a double-buffered LDS row
@@ -21,6 +32,7 @@
 // contiguous bands so the band-edge halo rows of vertically adjacent tiles hit the same L2.
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
+#include "hh_stencil9.hpp"
 
 #include <type_traits>
 
@@ -58,6 +70,10 @@ __device__ __forceinline__ void block_reduce_store(double (&acc)[kMaxNorms], dou
       partials[(size_t)slot * kMaxNorms + threadIdx.x] = s;
     }
   }
+}
+
+__device__ __forceinline__ double2 csel(bool c, double2 a, double2 b) {
+  return make_double2(c ? a.x : b.x, c ? a.y : b.y);
 }
 
 __device__ __forceinline__ void store2(double2* p, double2 v, bool nt) {
@@ -117,13 +133,13 @@ using cdouble_p = const __attribute__((address_space(4))) double*;
 // The row loop is unrolled by the register-ring length: ring slot m always holds row
 // rb-1+m (mod ring), so no value is copied between registers -- a copy of a register with
 // a load still in flight would make hipcc drain vmcnt and serialise the prefetch.
-template <int EPI, bool CONSTC, int XM, int PF, bool NT, bool NTU, int TPB>
+template <int EPI, bool CONSTC, int XM, int PF, bool NT, bool NTU, int TPB, bool S9>
 __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t);
 
 // Grid: either one block per tile, or a persistent grid of `gridDim.x` blocks (a multiple
 // of 8) in which block L works through the tiles of XCD L % 8 in order, so at any moment
 // each XCD streams one contiguous band window (L2 reuse of band-edge rows).
-template <int EPI, bool CONSTC, int XM, int PF, bool NT, bool NTU, int TPB>
+template <int EPI, bool CONSTC, int XM, int PF, bool NT, bool NTU, int TPB, bool S9>
 __global__ __launch_bounds__(TPB) void stencil_kernel(const StencilArgs a) {
   if (a.stop && *a.stop) return;  // queued GMRES cycle already stopped
   const int L = blockIdx.x;
@@ -132,18 +148,22 @@ __global__ __launch_bounds__(TPB) void stencil_kernel(const StencilArgs a) {
   for (int tt = q; tt < a.tiles_per_xcd; tt += Q) {
     const int t = (L & 7) * a.tiles_per_xcd + tt;
     if (t >= ntiles) break;  // uniform per block
-    stencil_tile<EPI, CONSTC, XM, PF, NT, NTU, TPB>(a, t);
+    stencil_tile<EPI, CONSTC, XM, PF, NT, NTU, TPB, S9>(a, t);
   }
 }
 
-template <int EPI, bool CONSTC, int XM, int PF, bool NT, bool NTU, int TPB>
+template <int EPI, bool CONSTC, int XM, int PF, bool NT, bool NTU, int TPB, bool S9>
 __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) {
   using T = EpiTraits<EPI>;
+  static_assert(!S9 || (XM == XM_LDS && PF == 1), "9-point stencil: LDS row ring, prefetch 1");
   constexpr int UR = (PF == 1) ? 4 : 6;  // u ring: u_{r-1} .. u_{r+1+PF}
   constexpr int IR = PF + 1;             // per-row input ring
   constexpr int UNR = UR;                // unroll (multiple of UR, IR and 2)
   static_assert(UNR % IR == 0 && UNR % 2 == 0, "ring sizes");
-  __shared__ double2 lrow[2][XM == XM_LDS ? TPB + 2 : 1];
+  // LDS rows: double-buffered centre row (5-point); ring of 4 rows (9-point: rows r-1, r, r+1
+  // are read at row r while row r+2's slot is free to be written one barrier later)
+  constexpr int NLROW = S9 ? 4 : 2;
+  __shared__ double2 lrow[NLROW][XM == XM_LDS ? TPB + 2 : 1];
 
   // XCD-aware tile map (see stencil_kernel): tile t is a 256-wide strip x one row band.
   const int tx = t % a.tiles_x;
@@ -190,7 +210,7 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
   auto load_row_in = [&](int r, RowIn& v) {
     if constexpr (!CONSTC) v.ic = ld1<NT>(a.invc2 + (size_t)r * n + ic_);
     else v.ic = a.invc2_const;
-    const double2* rp = rowp(r);
+    const double2* rp = rowp(S9 ? r + 1 : r);  // 9-point: edges of the row entering the ring
     v.eW = rp[iw];
     if constexpr (XM == XM_DIRECT) v.eE = rp[ie];  // else eW holds both edges (see above)
     if constexpr (T::reads_in1) v.b = ld2<NT>(a.in1 + (size_t)r * n + ic_);
@@ -199,7 +219,9 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
   const cdouble_p tabj = (cdouble_p)(a.tab_j);
   struct Tab {
     double2 R2, BS, BN, OM;
+    double2 R2m, R2p;  // 9-point: R2 of rows r-1 and r+1
   };
+  const cdouble_p tabx = (cdouble_p)(a.tab_r2x);
   auto load_tab = [&](int r, Tab& tb) {
     const int ru = __builtin_amdgcn_readfirstlane(r);
     const cdouble_p q = tabj + 8 * ru;
@@ -207,9 +229,21 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
     tb.BS = make_double2(q[2], q[3]);
     tb.BN = make_double2(q[4], q[5]);
     tb.OM = make_double2(q[6], q[7]);
+    if constexpr (S9) {
+      const cdouble_p x = tabx + 2 * ru;  // entry r + 1 is row r: rows r-1, r+1 at r, r + 2
+      tb.R2m = make_double2(x[0], x[1]);
+      tb.R2p = make_double2(x[4], x[5]);
+    }
   };
 
   const double2 AW = a.tab_i[ic_], AE = a.tab_i[n + ic_], R1 = a.tab_i[2 * n + ic_];
+  // 9-point: R1 of the neighbouring columns (clamped at the grid edge, where they multiply
+  // the zero Dirichlet values only)
+  double2 R1m = R1, R1p = R1;
+  if constexpr (S9) {
+    R1m = a.tab_i[2 * n + max(ic_ - 1, 0)];
+    R1p = a.tab_i[2 * n + min(ic_ + 1, n - 1)];
+  }
 
   double2 U[UR];
   RowIn IN[IR];
@@ -226,6 +260,22 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
     load_row_in(min(rb + 1, re - 1), IN[1]);
   }
   load_tab(rb, TB[0]);
+  if constexpr (S9) {
+    // rows rb-1 and rb enter the LDS ring before the loop (slot of row r: (r - rb + 1) & 3)
+    // (selects by value: `c ? U[0] : z2` on lvalues selects stack addresses and moves the
+    // whole register ring to scratch)
+    const double2 em = rowp(rb - 1)[iw], ec = rowp(rb)[iw];
+    lrow[0][tid + 1] = csel(act, U[0], z2);
+    lrow[1][tid + 1] = csel(act, U[1], z2);
+    if (tid == 0) {
+      lrow[0][0] = csel(lw, em, z2);
+      lrow[1][0] = csel(lw, ec, z2);
+    }
+    if (tid == TPB - 1) {
+      lrow[0][TPB + 1] = csel(le, em, z2);
+      lrow[1][TPB + 1] = csel(le, ec, z2);
+    }
+  }
 
   double sin = 1.0;
   if constexpr (T::scaled_in) {
@@ -253,7 +303,24 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
       const double2 eW = lw ? in.eW : z2;
       const double2 eE = le ? (XM == XM_DIRECT ? in.eE : in.eW) : z2;
       double2 uW, uE;
-      if constexpr (XM == XM_LDS) {
+      double2 uSW = z2, uSE = z2, uNW = z2, uNE = z2;
+      if constexpr (S9) {
+        // row r+1 enters the ring (its edges arrived with this row's inputs); rows r-1 and r
+        // are already there
+        double2* bS = lrow[k & 3];
+        double2* bC = lrow[(k + 1) & 3];
+        double2* bN = lrow[(k + 2) & 3];
+        bN[tid + 1] = csel(act, uN, z2);
+        if (tid == 0) bN[0] = eW;
+        if (tid == TPB - 1) bN[TPB + 1] = eE;
+        __syncthreads();
+        uSW = bS[tid];
+        uSE = bS[tid + 2];
+        uW = bC[tid];
+        uE = bC[tid + 2];
+        uNW = bN[tid];
+        uNE = bN[tid + 2];
+      } else if constexpr (XM == XM_LDS) {
         double2* buf = lrow[k & 1];
         buf[tid + 1] = uCm;
         if (tid == 0) buf[0] = eW;
@@ -278,16 +345,37 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
       const double2 N = cmul(tb.BN, R1);
       const double2 M = cscale(cmul(tb.OM, R1), in.ic);
       const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
-      const double2 D = csub(M, sum4);
-      double2 Db = D;
-      if constexpr (T::shifted) Db = csub(cmul(M, a.mshift), sum4);
-      const double2 Dc = (EPI == EPI_SL_SWEEP) ? Db : D;
-
-      double2 Au = cmul(S, uS);
-      Au = cfma(W, uW, Au);
-      Au = cfma(Dc, uC, Au);
-      Au = cfma(E, uE, Au);
-      Au = cfma(N, uN, Au);
+      double2 D, Db, Au;
+      if constexpr (!S9) {
+        D = csub(M, sum4);
+        Db = D;
+        if constexpr (T::shifted) Db = csub(cmul(M, a.mshift), sum4);
+        const double2 Dc = (EPI == EPI_SL_SWEEP) ? Db : D;
+        Au = cmul(S, uS);
+        Au = cfma(W, uW, Au);
+        Au = cfma(Dc, uC, Au);
+        Au = cfma(E, uE, Au);
+        Au = cfma(N, uN, Au);
+      } else {
+        const Stencil9W w = a.w9;
+        const double2 Mb = T::shifted ? cmul(M, a.mshift) : M;
+        D = stencil9_diag(M, sum4, w);
+        Db = stencil9_diag(Mb, sum4, w);
+        // the applied operator: A_beta in the second sweep, A everywhere else
+        const double2 Dc = (EPI == EPI_SL_SWEEP) ? Db : D;
+        const Coef9 q = stencil9_offdiag(W, E, S, N, AW, AE, tb.BS, tb.BN, R1m, R1p, tb.R2m,
+                                         tb.R2p, (EPI == EPI_SL_SWEEP) ? Mb : M, w);
+        // CSR column order: SW, S, SE, W, C, E, NW, N, NE
+        Au = cmul(q.sw, uSW);
+        Au = cfma(q.s, uS, Au);
+        Au = cfma(q.se, uSE, Au);
+        Au = cfma(q.w, uW, Au);
+        Au = cfma(Dc, uC, Au);
+        Au = cfma(q.e, uE, Au);
+        Au = cfma(q.nw, uNW, Au);
+        Au = cfma(q.n, uN, Au);
+        Au = cfma(q.ne, uNE, Au);
+      }
 
       if (act && live) {
         if constexpr (EPI == EPI_AX) {
@@ -352,14 +440,16 @@ __global__ __launch_bounds__(kStencilThreads) void point_kernel(const PointArgs 
       const double2 N = cmul(BN, R1);
       const double2 M = cscale(cmul(OM, R1), ic);
       const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
+      // 9-point diagonal: c M - alpha (W + E + S + N)  (hh_stencil9.hpp)
       if constexpr (OP == PT_DIAG) {
-        a.out0[p] = csub(M, sum4);
+        a.out0[p] = a.s9 ? stencil9_diag(M, sum4, a.w9) : csub(M, sum4);
       } else if constexpr (OP == PT_JAC) {
-        const double2 z = cdiv(a.in0[p], csub(M, sum4));
+        const double2 z = cdiv(a.in0[p], a.s9 ? stencil9_diag(M, sum4, a.w9) : csub(M, sum4));
         a.out0[p] = z;
         acc[0] += cabs2(z);
       } else if constexpr (OP == PT_SL_FIRST) {
-        const double2 Db = csub(cmul(M, a.mshift), sum4);
+        const double2 Mb = cmul(M, a.mshift);
+        const double2 Db = a.s9 ? stencil9_diag(Mb, sum4, a.w9) : csub(Mb, sum4);
         a.out0[p] = cscale(cdiv(a.in0[p], Db), a.damping);
       }
     }
@@ -375,26 +465,33 @@ constexpr int kDefaultVariant = 30;  // XM_LDS, PF 1, NT stores + NT 1/c^2 loads
 constexpr int kSmallVariant = 18;    // 256-wide strips, NT u loads (grids below 2048)
 constexpr int kSolveVariant = 42;    // kDefaultVariant with NT u loads: solve epilogues, rows <= kLongRow
 constexpr int kLongRow = 4608;
+// 9-point default at every size: 256-wide strips, NT u loads.  Its 133 VGPRs leave 3 waves per
+// SIMD, so a 512-thread block would run alone on its CU (4096^2 cold: 140 us for 256-wide vs
+// 180 us for 512-wide, profiles/r01v_tune_stencil9.log).
+constexpr int kStencil9Variant = kSmallVariant;
+bool stencil9_variant_valid(int v) {
+  return v == 6 || v == kSmallVariant || v == kDefaultVariant || v == kSolveVariant;
+}
 
 // Variant table: V = XM + 3 (PF - 1) + 6 NT + 12 NTU + 24 (512-wide strips)  (0..47).
 template <int V>
 constexpr int variant_tpb() { return V >= 24 ? 512 : 256; }
-template <int EPI, bool C, int V>
+template <int EPI, bool C, int V, bool S9 = false>
 struct VariantLaunch {
   static void go(const StencilArgs& a, int blocks, hipStream_t s) {
     constexpr int W = V % 24;
     constexpr int XM = W % 3, PF = (W / 3) % 2 + 1;
     constexpr bool NT = (W / 6) % 2 == 1, NTU = W >= 12;
     constexpr int TPB = variant_tpb<V>();
-    hipLaunchKernelGGL((stencil_kernel<EPI, C, XM, PF, NT, NTU, TPB>), dim3(blocks), dim3(TPB), 0,
-                       s, a);
+    hipLaunchKernelGGL((stencil_kernel<EPI, C, XM, PF, NT, NTU, TPB, S9>), dim3(blocks), dim3(TPB),
+                       0, s, a);
   }
 };
 
-template <int EPI, int V>
+template <int EPI, int V, bool S9 = false>
 void launch_v(bool const_c, const StencilArgs& a, int blocks, hipStream_t s) {
-  if (const_c) VariantLaunch<EPI, true, V>::go(a, blocks, s);
-  else VariantLaunch<EPI, false, V>::go(a, blocks, s);
+  if (const_c) VariantLaunch<EPI, true, V, S9>::go(a, blocks, s);
+  else VariantLaunch<EPI, false, V, S9>::go(a, blocks, s);
 }
 
 template <int EPI, int... Vs>
@@ -406,7 +503,13 @@ void launch_any(int v, bool const_c, const StencilArgs& a, int blocks, hipStream
 
 template <int EPI>
 void launch_stencil_t(bool const_c, const StencilArgs& a, int blocks, hipStream_t s, int v) {
-  if constexpr (EPI == EPI_AX) {
+  if (a.tab_r2x) {
+    // 9-point operator: LDS exchange, prefetch 1; 256- or 512-wide strips, NT or cached u
+    if (v == 6) launch_v<EPI, 6, true>(const_c, a, blocks, s);
+    else if (v == kDefaultVariant) launch_v<EPI, kDefaultVariant, true>(const_c, a, blocks, s);
+    else if (v == kSolveVariant) launch_v<EPI, kSolveVariant, true>(const_c, a, blocks, s);
+    else launch_v<EPI, kStencil9Variant, true>(const_c, a, blocks, s);
+  } else if constexpr (EPI == EPI_AX) {
     launch_any<EPI, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21,
                22, 23, 24, 25, 26, 27, 30, 31, 32, 33, 42, 43, 44, 45>(v, const_c, a, blocks, s);
   } else {
@@ -486,7 +589,9 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_
                     hipStream_t stream, int variant) {
   StencilArgs a = a_in;
   const int rows = a.row_end - a.row_begin;
-  const int v = stencil_resolve_variant(epi, variant, a.n);
+  int v = stencil_resolve_variant(epi, variant, a.n);
+  // the 9-point operator has its own shape set (launch_stencil_t)
+  if (a.tab_r2x) v = stencil9_variant_valid(variant) ? variant : kStencil9Variant;
   const int tpb = v >= 24 ? 512 : 256;
   a.tiles_x = (a.n + tpb - 1) / tpb;
   // bands start every row_step rows (spaced out only by the halo-row launch of a rank inside

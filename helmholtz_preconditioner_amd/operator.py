@@ -23,6 +23,10 @@ from . import _ffi
 from ._ffi import check, lib
 from .context import Context, default_context
 
+# Dispersion-optimal weights (alpha, c, d) of the 9-point operator (derived by
+# tools/optimize_9pt.py: phase-velocity error <= 0.42 % at >= 4 points per wavelength).
+STENCIL9_WEIGHTS = (0.7910350, 0.6276117, 0.0948567)
+
 
 def _medium_arguments(c_mat, n):
     """Map the reference's c_mat to (host array | None, c_const, mass_scale).
@@ -107,7 +111,8 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
     rank's slab when the context spans several ranks.
     """
 
-    def __init__(self, b, const, eta, omega, h, n, c_mat, context: Context | None = None):
+    def __init__(self, b, const, eta, omega, h, n, c_mat, context: Context | None = None,
+                 stencil: int = 5, stencil_weights=None):
         self.ctx = context or default_context()
         self.b, self.const, self.eta, self.omega, self.h, self.n = b, const, eta, complex(omega), h, n
         host, c_const, mass = _medium_arguments(c_mat, n)
@@ -123,7 +128,24 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
         self.row_begin, self.row_end = jb.value, je.value
         self.local_size = (je.value - jb.value) * n
         self._precond = (_ffi.HH_PREC_NONE, 0.5, 1, 1.0)
+        self.stencil, self.stencil_weights = 5, None
+        if stencil != 5 or stencil_weights is not None:
+            self.set_stencil(stencil, stencil_weights)
         super().__init__(dtype=np.complex128, shape=(self.local_size, self.local_size))
+
+    def set_stencil(self, points: int = 9, weights=None):
+        """Select the 5-point operator (the reference's, code.py:202-219) or the 9-point one
+        (no reference counterpart): ``weights`` = (alpha, c, d), default
+        :data:`STENCIL9_WEIGHTS`.  Applies, preconditioners, ``gmres`` and ``to_csr`` follow."""
+        points = int(points)
+        if points not in (5, 9):
+            raise ValueError("stencil must be 5 or 9")
+        w = tuple(float(v) for v in (weights if weights is not None else STENCIL9_WEIGHTS))
+        if len(w) != 3:
+            raise ValueError("stencil_weights must be (alpha, c, d)")
+        check(lib.hh_op_set_stencil(self.handle, points, *w))
+        self.stencil = points
+        self.stencil_weights = w if points == 9 else None
 
     # ----------------------------------------------------------------- plumbing
     @property
@@ -160,6 +182,8 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
 
     def _rmatvec(self, x):
         # A is complex-symmetric (A^T == A), so A^H x = conj(A conj(x)).
+        if self.stencil != 5:
+            raise NotImplementedError("A^H of the 9-point operator (not symmetric): use to_csr()")
         return np.conj(self._apply_host(np.conj(x), _ffi.HH_APPLY_A))
 
     def _adjoint(self):
@@ -174,7 +198,8 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
 
     @property
     def csr_nnz(self) -> int:
-        """Entries of this rank's rows in the assembled matrix (5 n^2 - 4 n on one rank)."""
+        """Entries of this rank's rows in the assembled matrix (5 n^2 - 4 n on one rank;
+        (3 n - 2)^2 for the 9-point operator)."""
         v = ctypes.c_int64()
         check(lib.hh_op_csr_nnz(self.handle, ctypes.byref(v)))
         return v.value
@@ -258,13 +283,17 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
             pass
 
 
-def build_A_matrix(b, const, eta, omega, h, n, c_mat, context: Context | None = None):
+def build_A_matrix(b, const, eta, omega, h, n, c_mat, context: Context | None = None,
+                   stencil: int = 5, stencil_weights=None):
     """Drop-in for ``build_A_matrix`` (code.py:202): same arguments, same operator.
 
     Returns a :class:`DeviceOperator` (a LinearOperator) instead of a scipy CSR
     matrix; ``A @ x`` / ``A.matvec(x)`` / ``A.diagonal()`` behave like the CSR's.
+    ``stencil=9`` (keyword only, not in the reference) selects the 9-point operator
+    (see :meth:`DeviceOperator.set_stencil`).
     """
-    return DeviceOperator(b, const, eta, omega, h, n, c_mat, context=context)
+    return DeviceOperator(b, const, eta, omega, h, n, c_mat, context=context, stencil=stencil,
+                          stencil_weights=stencil_weights)
 
 
 # ----------------------------------------------------------------- preconditioners

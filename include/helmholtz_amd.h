@@ -129,7 +129,8 @@ int hh_op_apply(hh_op* op, const double* x, double* y, int mode);
 int hh_op_diagonal(hh_op* op, double* d);
 
 /* Operator export: the CSR matrix build_A_matrix returns (code.py:202-219,
- * canonical scipy CSR: per row S, W, D, E, N in column order, nnz = 5n^2 - 4n), restricted
+ * canonical scipy CSR: per row S, W, D, E, N in column order, nnz = 5n^2 - 4n; for the
+ * 9-point operator SW, S, SE, W, C, E, NW, N, NE, nnz = (3n-2)^2), restricted
  * to this rank's rows, with global column indices.  Written on the device from the same
  * tables the stencil applies (the exported values are the applied operator, bit for bit),
  * then copied to the caller's host arrays.
@@ -193,6 +194,19 @@ int hh_gmres(hh_op* op, const hh_vec* b, hh_vec* x, double rtol, double atol,
  * persistent grid of that many workgroups (0 = one per tile).  Results are identical
  * for every setting; only speed changes. */
 int hh_op_tune(hh_op* op, int variant, int rows_per_block, int grid_blocks);
+/* Stencil of the operator (the reference itself is 5-point only,
+ * code.py:216-218, so this has no reference counterpart).  points = 5: the reference's
+ * operator (default).  points = 9: alpha x the 5-point operator + (1 - alpha) x its
+ * line-averaged form (each second difference averaged over the two neighbouring lines, with
+ * those lines' PML factors) + the mass term spread over the 3x3 points with weights c (centre),
+ * d (edges), e = (1 - c - 4d) / 4 (corners) -- the optimal 9-point PML scheme family
+ * (Chen, Cheng, Feng & Wu 2013).  Second order for any weights with alpha, c, d finite;
+ * tools/optimize_9pt.py derives the dispersion-optimal defaults the Python layer passes
+ * (alpha 0.7910350, c 0.6276117, d 0.0948567: phase-velocity error <= 0.42 % at >= 4 points
+ * per wavelength vs 10 % for 5 points).  Same HBM bytes per apply (40 B/unknown).  Every
+ * apply, preconditioner (none / Jacobi / shifted-Laplace), GMRES and the CSR export
+ * (nnz = (3n-2)^2) follow the selected stencil; the sweeping preconditioner needs 5 points. */
+int hh_op_set_stencil(hh_op* op, int points, double alpha, double c, double d);
 /* Two-sweep shifted-Laplace M: apply M A in one fused launch (default 1) or as the stencil
  * + sweep pair (0).  Same results bit for bit; the fused form moves 40 instead of 112 B per
  * unknown.  It applies to a single slab of a single rank; elsewhere the pair runs. */

@@ -39,6 +39,7 @@ __all__ = [
     "init_c1_mat", "init_c2_mat", "init_f1_mat", "init_f2_mat",
     "jacobi_preconditioner", "shifted_laplace_jacobi", "gmres_reference",
     "problem_params", "slab_apply_emulated",
+    "STENCIL9_WEIGHTS", "stencil9_coefficients", "build_A9_matrix", "phase_velocity_9pt",
 ]
 
 
@@ -121,6 +122,90 @@ def build_A_matrix(b, const, eta, omega, h, n, c_mat):
     A = scipy.sparse.csr_matrix((vals, (rows, cols)), shape=(NN, NN), dtype=np.complex128)
     A.sort_indices()
     return A
+
+
+# --------------------------------------------------------------------------
+# 9-point operator.  NO reference counterpart: the reference is 5-point
+# only (code.py:216-218), so this restatement is pinned by properties, not by reference
+# outputs ("parity unpinned" by the reference): it reduces to build_A_matrix exactly for
+# weights (1, 1, 0), it is second-order consistent (the 3x3 weights of every symbol sum
+# correctly), and its constant-medium dispersion matches phase_velocity_9pt.
+#
+#   A9 = alpha * A5_laplacian + (1 - alpha) * (line-averaged second differences)
+#        + mass term M (c u_C + d sum(edges) + e sum(corners)),  e = (1 - c - 4d) / 4
+# with the line-averaged part: the x second difference of code.py:83-106 averaged over
+# rows j-1 and j+1 (with those rows' 1/s2 factor) and the y one over columns i-1, i+1.
+# --------------------------------------------------------------------------
+STENCIL9_WEIGHTS = (0.7910350, 0.6276117, 0.0948567)  # (alpha, c, d), tools/optimize_9pt.py
+
+
+def stencil9_coefficients(const, eta, omega, h, n, c_mat, weights=STENCIL9_WEIGHTS):
+    """The nine coefficient arrays [j-1, i-1] of the 9-point operator, as a dict with keys
+    sw, s, se, w, c, e, nw, n, ne (neighbour offsets (di, dj) = (-1,-1), (0,-1), ...).
+    Entries for neighbours outside the grid are returned too; the assembly drops them."""
+    alpha, cw, dw = (float(v) for v in weights)
+    g = (1.0 - alpha) / 2.0
+    ew = (1.0 - cw - 4.0 * dw) / 4.0
+    W, E, S, N, D = stencil_coefficients(const, eta, omega, h, n, c_mat)
+    idx = np.arange(1, n + 1, dtype=np.float64)
+    I = idx[None, :]
+    J = idx[:, None]
+    inv_h2 = 1 / h ** 2
+    AW = inv_h2 * s1((I - .5) * h, const, eta, omega)
+    AE = inv_h2 * s1((I + .5) * h, const, eta, omega)
+    BS = inv_h2 * s2((J - .5) * h, const, eta, omega)
+    BN = inv_h2 * s2((J + .5) * h, const, eta, omega)
+    R2m = 1 / s2((J - 1) * h, const, eta, omega)
+    R2p = 1 / s2((J + 1) * h, const, eta, omega)
+    R1m = 1 / s1(np.maximum(I - 1, 1) * h, const, eta, omega)   # clamped like the kernel:
+    R1p = 1 / s1(np.minimum(I + 1, n) * h, const, eta, omega)   # only multiplies ghosts
+    cc = np.asarray(c_mat)[:n, :n].T
+    M = omega ** 2 / (s1(I * h, const, eta, omega) * s2(J * h, const, eta, omega) * cc ** 2)
+    Wm, Em, Wp, Ep = AW * R2m, AE * R2m, AW * R2p, AE * R2p
+    Sm, Nm, Sp, Np = BS * R1m, BN * R1m, BS * R1p, BN * R1p
+    return {
+        "sw": g * (Wm + Sm) + ew * M, "s": alpha * S - g * (Wm + Em) + dw * M,
+        "se": g * (Em + Sp) + ew * M, "w": alpha * W - g * (Sm + Nm) + dw * M,
+        "c": cw * M - alpha * (W + E + S + N), "e": alpha * E - g * (Sp + Np) + dw * M,
+        "nw": g * (Wp + Nm) + ew * M, "n": alpha * N - g * (Wp + Ep) + dw * M,
+        "ne": g * (Ep + Np) + ew * M,
+    }
+
+
+_OFF9 = (("sw", -1, -1), ("s", 0, -1), ("se", 1, -1), ("w", -1, 0), ("c", 0, 0),
+         ("e", 1, 0), ("nw", -1, 1), ("n", 0, 1), ("ne", 1, 1))
+
+
+def build_A9_matrix(b, const, eta, omega, h, n, c_mat, weights=STENCIL9_WEIGHTS):
+    """Global CSR of the 9-point operator (same arguments as build_A_matrix, code.py:202):
+    per row SW, S, SE, W, C, E, NW, N, NE where inside the grid; nnz = (3n-2)^2."""
+    co = stencil9_coefficients(const, eta, omega, h, n, c_mat, weights)
+    jj, ii = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+    rows, cols, vals = [], [], []
+    for key, di, dj in _OFF9:
+        ok = (ii + di >= 0) & (ii + di < n) & (jj + dj >= 0) & (jj + dj < n)
+        p = (jj * n + ii)[ok]
+        rows.append(p)
+        cols.append(p + dj * n + di)
+        vals.append(co[key][ok])
+    A = scipy.sparse.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
+                                shape=(n * n, n * n), dtype=np.complex128)
+    A.sort_indices()
+    return A
+
+
+def phase_velocity_9pt(weights, G, phi):
+    """Normalised numerical phase velocity of the constant-medium, PML-free 9-point scheme for
+    a plane wave of G points per wavelength at angle phi (weights (1, 1, 0): the 5-point one).
+    Symbol: alpha (2cos t + 2cos s - 4) + (1 - alpha)(4 cos t cos s - 2cos t - 2cos s)
+            + (wh/c)^2 (c + 2d (cos t + cos s) + 4e cos t cos s) = 0."""
+    alpha, cw, dw = weights
+    ew = (1 - cw - 4 * dw) / 4
+    kh = 2 * np.pi / np.asarray(G, dtype=np.float64)
+    ct, cs = np.cos(kh * np.cos(phi)), np.cos(kh * np.sin(phi))
+    L = alpha * (2 * ct + 2 * cs - 4) + (1 - alpha) * (4 * ct * cs - 2 * ct - 2 * cs)
+    m = cw + 2 * dw * (ct + cs) + 4 * ew * ct * cs
+    return np.sqrt(-L / m) / kh
 
 
 # --------------------------------------------------------------------------
