@@ -126,7 +126,7 @@ int stencil_grid_blocks(int n, int rows, int rows_per_block, int row_step = 0);
 int stencil_bands(int rows, int rows_per_block, int row_step);  // tiles along j
 // Fused M A for the two-sweep shifted-Laplace M (sl_fused.hip): a.u = v, a.out0 = w; single
 // slab whose halo rows are zero rows.
-void launch_sl2(bool const_c, const StencilArgs& a, hipStream_t stream);
+void launch_sl2(bool const_c, const StencilArgs& a, hipStream_t stream, int variant = -1);
 int stencil_rows_per_block(int n, int rows);
 void launch_point(int op, bool const_c, const PointArgs& a, int blocks, hipStream_t stream);
 int point_blocks(size_t len);

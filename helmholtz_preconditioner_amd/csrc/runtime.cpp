@@ -296,7 +296,9 @@ void run_sl2(hh_op* op, const double2* v, const double* vs, double2* out) {
   a.in_scale = vs;
   a.out0 = out + s.off;
   a.stop = op->stop_flag;
-  launch_sl2(op->const_c, a, op->ctx->stream);
+  if (op->tk0) HIPC(hipEventRecord(op->tk0, op->ctx->stream));
+  launch_sl2(op->const_c, a, op->ctx->stream, op->variant);
+  if (op->tk1) HIPC(hipEventRecord(op->tk1, op->ctx->stream));
   HIPC(hipGetLastError());
   op->stats.spmv_count++;
 }

@@ -210,13 +210,19 @@ void launch_t(bool const_c, const StencilArgs& a, int blocks, hipStream_t s) {
 
 }  // namespace
 
-void launch_sl2(bool const_c, const StencilArgs& a_in, hipStream_t stream) {
+void launch_sl2(bool const_c, const StencilArgs& a_in, hipStream_t stream, int variant) {
   StencilArgs a = a_in;
   const int n = a.n;
-  // shapes as the stencil's solve epilogues: 256-wide strips below n = 2048, non-temporal v
-  // (just written by the previous kernel) on rows up to 4608 points
-  const int tpb = n < 2048 ? 256 : 512;
-  const bool ntu = n <= 4608;
+  // 256-wide strips (126 VGPRs: 4 blocks per CU instead of 2 at 512; 4096^2 inside GMRES(20):
+  // 768 vs 754 it/s, profiles/r01v_tune_sl2*.log), non-temporal v (just written by the previous
+  // kernel) on rows up to 4608 points; a stencil tuning variant (hh_op_tune) of the LDS family
+  // picks the strip width (>= 24: 512) and NT v loads (% 24 >= 12)
+  int tpb = 256;
+  bool ntu = n <= 4608;
+  if (variant == 6 || variant == 18 || variant == 30 || variant == 42) {
+    tpb = variant >= 24 ? 512 : 256;
+    ntu = variant % 24 >= 12;
+  }
   const int rows = a.row_end - a.row_begin;
   a.row_step = a.rows_per_block;
   a.tiles_x = (n + (tpb - 2) - 1) / (tpb - 2);
