@@ -17,9 +17,14 @@ from oracle import helmholtz_oracle as O
 
 
 class SlabOperator:
-    def __init__(self, const, eta, omega, h, n, c_mat, j0, j1, jacobi=False):
+    def __init__(self, const, eta, omega, h, n, c_mat, j0, j1, jacobi=False, stencil=5):
         W, E, S, N, D = O.stencil_coefficients(const, eta, omega, h, n, c_mat)
         self.W, self.E, self.S, self.N, self.D = (a[j0:j1] for a in (W, E, S, N, D))
+        self.co9 = None
+        if stencil == 9:  # the same one-row halo carries the corner neighbours
+            co = O.stencil9_coefficients(const, eta, omega, h, n, c_mat)
+            self.co9 = {k: v[j0:j1] for k, v in co.items()}
+            self.D = self.co9["c"]
         self.n, self.j0, self.j1 = n, j0, j1
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
         self.jacobi = jacobi
@@ -48,6 +53,16 @@ class SlabOperator:
         X = x.reshape(-1, self.n)
         lo, hi = self._halo(X)
         ext = np.vstack([lo[None], X, hi[None]])
+        if self.co9 is not None:
+            m, c = X.shape[0], self.co9
+            y = np.zeros_like(X)
+            for dj, (kw, kc, ke) in ((-1, ("sw", "s", "se")), (0, ("w", "c", "e")),
+                                     (1, ("nw", "n", "ne"))):
+                R = ext[1 + dj:1 + dj + m]
+                y[:, 1:] += c[kw][:, 1:] * R[:, :-1]
+                y += c[kc] * R
+                y[:, :-1] += c[ke][:, :-1] * R[:, 1:]
+            return y.ravel()
         y = self.S * ext[:-2]
         y[:, 1:] += self.W[:, 1:] * X[:, :-1]
         y += self.D * X

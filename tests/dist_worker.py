@@ -23,13 +23,14 @@ def main():
     p.add_argument("--out")
     p.add_argument("--n", type=int, default=150)
     p.add_argument("--slabs", type=int, default=1)
+    p.add_argument("--stencil", type=int, default=5)
     a = p.parse_args()
     ctx = H.Context(device=0, rank=a.rank, world=a.world, nccl_id=bytes.fromhex(a.id),
                     virtual_slabs=a.slabs, transport="shm")
     n = a.n
     om, h, eta = H.problem_params(n, 12, 6.0, 2.0)
     cm = H.init_c1_mat(.5, .5, n)
-    A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, context=ctx)
+    A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, context=ctx, stencil=a.stencil)
     j0, j1 = A.row_begin, A.row_end
     rng = np.random.default_rng(5)
     xg = (rng.standard_normal(n * n) + 1j * rng.standard_normal(n * n)).reshape(n, n)

@@ -16,6 +16,7 @@ import pytest
 
 from conftest import ROOT, load_golden, medium
 from helmholtz_preconditioner_amd import dist as hdist
+from oracle import helmholtz_oracle as O
 
 
 def test_slab_bounds_tile_the_grid():
@@ -95,3 +96,54 @@ def test_distributed_gmres_mirror_matches_reference(case, world):
             assert int(p["info"]) == int(z["info"])
             assert np.max(np.abs(p["hist"] - z["history"]) / z["history"]) < 1e-9
         assert np.linalg.norm(x - z["x"]) / np.linalg.norm(z["x"]) < 1e-9
+
+
+def _gloo_worker9(rank, world, port, out):
+    import torch.distributed as dist
+    import dist_mirror as DM
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 48
+    om, h, eta = O.problem_params(n, 6, 4.0, 2.0)
+    j0, j1 = hdist.slab_bounds(n, world, rank)
+    op = DM.SlabOperator(81.0, eta, om, h, n, medium("c1", n), j0, j1, jacobi=True, stencil=9)
+    xg = np.random.default_rng(3).standard_normal(n * n) + 0j
+    y = op.apply(xg[j0 * n:j1 * n])
+    f = O.init_f1_mat(.5, .125, om, n)[j0:j1].ravel()
+    x, info, hist = DM.gmres_dist(op, f, 1e-3, 20, 60)
+    np.savez(out, x=x, info=info, hist=hist, y=y)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_9pt_mirror_matches_single_domain(world):
+    """SURVEY row F4 over the N > 1 path: the 9-point operator's slab apply (one-row halo) and
+    Jacobi-GMRES over gloo against the single-domain oracle CSR and scipy gmres."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    with tempfile.TemporaryDirectory() as td:
+        outs = [os.path.join(td, f"r{r}.npz") for r in range(world)]
+        ps = [ctx.Process(target=_gloo_worker9, args=(r, world, port, outs[r])) for r in range(world)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(timeout=300)
+            assert p.exitcode == 0
+        parts = [np.load(o) for o in outs]
+    n = 48
+    om, h, eta = O.problem_params(n, 6, 4.0, 2.0)
+    R = O.build_A9_matrix(6, 81.0, eta, om, h, n, medium("c1", n))
+    xg = np.random.default_rng(3).standard_normal(n * n) + 0j
+    y = np.concatenate([p["y"] for p in parts])
+    assert np.linalg.norm(y - R @ xg) <= 1e-14 * np.linalg.norm(R @ xg)
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    xr, infor, histr, _ = O.gmres_reference(R, f, M=O.jacobi_preconditioner(R), rtol=1e-3,
+                                            restart=20, maxiter=60)
+    x = np.concatenate([p["x"] for p in parts])
+    for p in parts:
+        assert int(p["info"]) == infor and len(p["hist"]) == len(histr)
+        assert np.max(np.abs(p["hist"] - histr) / histr) < 1e-9
+    assert np.linalg.norm(x - xr) / np.linalg.norm(xr) < 1e-9

@@ -6,7 +6,8 @@ the RCCL production path (slab ownership, one-row halo exchange, rank-ordered gl
 reductions), checked against the single-domain result on the same GPU:
   * the operator apply: bit-identical slabs;
   * GMRES (none / Jacobi / shifted-Laplace): residual history and field to 1e-8 (the
-    reductions sum partials in a different order; the contract is 1e-6).
+    reductions sum partials in a different order; the contract is 1e-6);
+  * both the reference's 5-point operator and the 9-point one.
 It also rehearses `bench.py --gpus 2` end to end under torch.distributed.run.
 """
 import json
@@ -25,10 +26,11 @@ pytestmark = pytest.mark.gpu
 WORKER = os.path.join(ROOT, "tests", "dist_worker.py")
 
 
-def _single_domain(n):
+def _single_domain(n, stencil=5):
     ctx = H.Context(device=0)
     om, h, eta = H.problem_params(n, 12, 6.0, 2.0)
-    A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.init_c1_mat(.5, .5, n), context=ctx)
+    A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.init_c1_mat(.5, .5, n), context=ctx,
+                         stencil=stencil)
     rng = np.random.default_rng(5)
     xg = rng.standard_normal(n * n) + 1j * rng.standard_normal(n * n)
     res = dict(y=A @ xg)
@@ -42,17 +44,18 @@ def _single_domain(n):
     return res
 
 
-@pytest.mark.parametrize("world,slabs", [(2, 1), (3, 1), (2, 2), (4, 1), (3, 2)])
-def test_multiprocess_slabs_match_single_domain(tmp_path, world, slabs):
+@pytest.mark.parametrize("world,slabs,stencil", [(2, 1, 5), (3, 1, 5), (2, 2, 5), (4, 1, 5),
+                                                (3, 2, 5), (3, 1, 9), (2, 2, 9)])
+def test_multiprocess_slabs_match_single_domain(tmp_path, world, slabs, stencil):
     n = 150
-    ref = _single_domain(n)
+    ref = _single_domain(n, stencil)
     tok = os.urandom(128).hex()
     procs = []
     for r in range(world):
         out = tmp_path / f"r{r}.npz"
         procs.append((subprocess.Popen([sys.executable, WORKER, "--rank", str(r), "--world",
                                         str(world), "--id", tok, "--out", str(out), "--n", str(n),
-                                        "--slabs", str(slabs)],
+                                        "--slabs", str(slabs), "--stencil", str(stencil)],
                                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT), out))
     for p, _ in procs:
         try:
