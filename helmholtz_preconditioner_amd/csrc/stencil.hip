@@ -164,6 +164,8 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
   // are read at row r while row r+2's slot is free to be written one barrier later)
   constexpr int NLROW = S9 ? 4 : 2;
   __shared__ double2 lrow[NLROW][XM == XM_LDS ? TPB + 2 : 1];
+  // 9-point: the y second difference of the current row, double-buffered (see the S9 step)
+  __shared__ double2 ly[2][S9 ? TPB + 2 : 1];
 
   // XCD-aware tile map (see stencil_kernel): tile t is a 256-wide strip x one row band.
   const int tx = t % a.tiles_x;
@@ -239,10 +241,12 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
   const double2 AW = a.tab_i[ic_], AE = a.tab_i[n + ic_], R1 = a.tab_i[2 * n + ic_];
   // 9-point: R1 of the neighbouring columns (clamped at the grid edge, where they multiply
   // the zero Dirichlet values only)
-  double2 R1m = R1, R1p = R1;
+  // 9-point: R1 of the strip's halo column for the two edge lanes (it only ever multiplies
+  // zeros off the grid, so the clamped column is fine there)
+  double2 R1e = R1;
   if constexpr (S9) {
-    R1m = a.tab_i[2 * n + max(ic_ - 1, 0)];
-    R1p = a.tab_i[2 * n + min(ic_ + 1, n - 1)];
+    const int ce = tid == 0 ? i0 - 1 : i0 + TPB;
+    R1e = a.tab_i[2 * n + min(max(ce, 0), n - 1)];
   }
 
   double2 U[UR];
@@ -276,6 +280,19 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
       lrow[1][TPB + 1] = csel(le, ec, z2);
     }
   }
+  // 9-point register ring: x second differences X and W+E sums H of rows r-1 (m) and r (c)
+  double2 Xm = z2, Xc = z2, Hm = z2, Hc = z2;
+  if constexpr (S9) {
+    __syncthreads();
+    const cdouble_p x = tabx + 2 * __builtin_amdgcn_readfirstlane(rb);  // R2 of rows rb-1, rb
+    const double2 R2a = make_double2(x[0], x[1]), R2b = make_double2(x[2], x[3]);
+    const double2 w0 = lrow[0][tid], e0 = lrow[0][tid + 2];
+    const double2 w1 = lrow[1][tid], e1 = lrow[1][tid + 2];
+    Xm = cmul(R2a, cfma(AE, csub(e0, U[0]), cmul(AW, csub(w0, U[0]))));
+    Xc = cmul(R2b, cfma(AE, csub(e1, U[1]), cmul(AW, csub(w1, U[1]))));
+    Hm = cadd(w0, e0);
+    Hc = cadd(w1, e1);
+  }
 
   double sin = 1.0;
   if constexpr (T::scaled_in) {
@@ -302,24 +319,39 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
       const double2 uCm = act ? uC : z2;  // columns past n contribute zero (Dirichlet)
       const double2 eW = lw ? in.eW : z2;
       const double2 eE = le ? (XM == XM_DIRECT ? in.eE : in.eW) : z2;
-      double2 uW, uE;
-      double2 uSW = z2, uSE = z2, uNW = z2, uNE = z2;
+      double2 uW = z2, uE = z2;
+      double2 Yc = z2, Yw = z2, Ye = z2, Xp = z2, Hp = z2;
       if constexpr (S9) {
-        // row r+1 enters the ring (its edges arrived with this row's inputs); rows r-1 and r
-        // are already there
+        // Separable form: with X(r') = R2(r') (AW (uW - uC) + AE (uE - uC)) the x second
+        // difference of row r' and Y(i') = R1(i') (BS (uS - uC) + BN (uN - uC)) the y one of
+        // column i' (this row's BS, BN), the operator is
+        //   alpha (X(r) + Y(i)) + g (X(r-1) + X(r+1) + Y(i-1) + Y(i+1)) + M (c uC + d edges + e corners)
+        // -- each X and each Y computed once.  Row r+1 enters the LDS ring (its edges arrived
+        // with this row's inputs) and Y(i) of row r goes to LDS for the neighbouring columns;
+        // the edge lanes add Y of the strip's halo columns from the ring's halo slots.
         double2* bS = lrow[k & 3];
         double2* bC = lrow[(k + 1) & 3];
         double2* bN = lrow[(k + 2) & 3];
+        double2* yb = ly[k & 1];
+        Yc = cmul(R1, cfma(tb.BN, csub(uN, uC), cmul(tb.BS, csub(uS, uC))));
         bN[tid + 1] = csel(act, uN, z2);
-        if (tid == 0) bN[0] = eW;
-        if (tid == TPB - 1) bN[TPB + 1] = eE;
+        yb[tid + 1] = csel(act, Yc, z2);
+        if (tid == 0) {
+          bN[0] = eW;
+          const double2 hS = bS[0], hC = bC[0];
+          yb[0] = cmul(R1e, cfma(tb.BN, csub(eW, hC), cmul(tb.BS, csub(hS, hC))));
+        }
+        if (tid == TPB - 1) {
+          bN[TPB + 1] = eE;
+          const double2 hS = bS[TPB + 1], hC = bC[TPB + 1];
+          yb[TPB + 1] = cmul(R1e, cfma(tb.BN, csub(eE, hC), cmul(tb.BS, csub(hS, hC))));
+        }
         __syncthreads();
-        uSW = bS[tid];
-        uSE = bS[tid + 2];
-        uW = bC[tid];
-        uE = bC[tid + 2];
-        uNW = bN[tid];
-        uNE = bN[tid + 2];
+        const double2 uNW = bN[tid], uNE = bN[tid + 2];
+        Yw = yb[tid];
+        Ye = yb[tid + 2];
+        Xp = cmul(tb.R2p, cfma(AE, csub(uNE, uN), cmul(AW, csub(uNW, uN))));
+        Hp = cadd(uNW, uNE);
       } else if constexpr (XM == XM_LDS) {
         double2* buf = lrow[k & 1];
         buf[tid + 1] = uCm;
@@ -363,18 +395,18 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
         Db = stencil9_diag(Mb, sum4, w);
         // the applied operator: A_beta in the second sweep, A everywhere else
         const double2 Dc = (EPI == EPI_SL_SWEEP) ? Db : D;
-        const Coef9 q = stencil9_offdiag(W, E, S, N, AW, AE, tb.BS, tb.BN, R1m, R1p, tb.R2m,
-                                         tb.R2p, (EPI == EPI_SL_SWEEP) ? Mb : M, w);
-        // CSR column order: SW, S, SE, W, C, E, NW, N, NE
-        Au = cmul(q.sw, uSW);
-        Au = cfma(q.s, uS, Au);
-        Au = cfma(q.se, uSE, Au);
-        Au = cfma(q.w, uW, Au);
-        Au = cfma(Dc, uC, Au);
-        Au = cfma(q.e, uE, Au);
-        Au = cfma(q.nw, uNW, Au);
-        Au = cfma(q.n, uN, Au);
-        Au = cfma(q.ne, uNE, Au);
+        const double2 Mo = (EPI == EPI_SL_SWEEP) ? Mb : M;
+        const double2 lap = cadd(Xc, Yc);
+        const double2 avg = cadd(cadd(Xm, Xp), cadd(Yw, Ye));
+        const double2 edges = cadd(Hc, cadd(uS, uN));
+        const double2 corners = cadd(Hm, Hp);
+        const double2 mix = cadd(cadd(cscale(uC, w.c), cscale(edges, w.d)), cscale(corners, w.e));
+        Au = cfma(Mo, mix, cadd(cscale(lap, w.alpha), cscale(avg, w.g)));
+        (void)Dc;
+        Xm = Xc;
+        Xc = Xp;
+        Hm = Hc;
+        Hc = Hp;
       }
 
       if (act && live) {
@@ -465,9 +497,9 @@ constexpr int kDefaultVariant = 30;  // XM_LDS, PF 1, NT stores + NT 1/c^2 loads
 constexpr int kSmallVariant = 18;    // 256-wide strips, NT u loads (grids below 2048)
 constexpr int kSolveVariant = 42;    // kDefaultVariant with NT u loads: solve epilogues, rows <= kLongRow
 constexpr int kLongRow = 4608;
-// 9-point default at every size: 256-wide strips, NT u loads.  Its 133 VGPRs leave 3 waves per
-// SIMD, so a 512-thread block would run alone on its CU (4096^2 cold: 140 us for 256-wide vs
-// 180 us for 512-wide, profiles/r01v_tune_stencil9.log).
+// The 9-point operator instantiates the four LDS-exchange shapes below and takes the 5-point
+// defaults: in its separable form (101-109 VGPRs, 4 waves per SIMD) it runs at the 5-point
+// kernel's speed (4096^2 cold: 119.3 vs 119.6 us, profiles/r01v_tune_stencil9.log).
 constexpr int kStencil9Variant = kSmallVariant;
 bool stencil9_variant_valid(int v) {
   return v == 6 || v == kSmallVariant || v == kDefaultVariant || v == kSolveVariant;
@@ -590,8 +622,8 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_
   StencilArgs a = a_in;
   const int rows = a.row_end - a.row_begin;
   int v = stencil_resolve_variant(epi, variant, a.n);
-  // the 9-point operator has its own shape set (launch_stencil_t)
-  if (a.tab_r2x) v = stencil9_variant_valid(variant) ? variant : kStencil9Variant;
+  // the 9-point operator has a subset of the shapes (launch_stencil_t): others take the default
+  if (a.tab_r2x && !stencil9_variant_valid(v)) v = stencil_resolve_variant(epi, -1, a.n);
   const int tpb = v >= 24 ? 512 : 256;
   a.tiles_x = (a.n + tpb - 1) / tpb;
   // bands start every row_step rows (spaced out only by the halo-row launch of a rank inside
