@@ -40,6 +40,7 @@ __all__ = [
     "jacobi_preconditioner", "shifted_laplace_jacobi", "gmres_reference",
     "problem_params", "slab_apply_emulated",
     "STENCIL9_WEIGHTS", "stencil9_coefficients", "build_A9_matrix", "phase_velocity_9pt",
+    "coefficients_at", "apply_at_points",
 ]
 
 
@@ -75,6 +76,22 @@ def s2(x, const, eta, omega):
 # Stencil coefficients.  Unknown p = (j-1)*n + (i-1); i is the fast axis
 # (x1 = i*h), j the slow axis / layer (x2 = j*h)  -- code.py:81-113, 206-218.
 # --------------------------------------------------------------------------
+def coefficients_at(const, eta, omega, h, I, J, cc):
+    """(W, E, S, N, D) at 1-based points (I, J) (arrays of one shape), with cc the velocity
+    c_mat[i-1, j-1] there (quirk Q3 already applied by the caller); formulas of
+    code.py:83-109.  The vectorised core of stencil_coefficients."""
+    I = np.asarray(I, dtype=np.float64)
+    J = np.asarray(J, dtype=np.float64)
+    inv_h2 = 1 / h ** 2
+    W = inv_h2 * (s1((I - .5) * h, const, eta, omega) / s2(J * h, const, eta, omega))
+    E = inv_h2 * (s1((I + .5) * h, const, eta, omega) / s2(J * h, const, eta, omega))
+    S = inv_h2 * (s2((J - .5) * h, const, eta, omega) / s1(I * h, const, eta, omega))
+    N = inv_h2 * (s2((J + .5) * h, const, eta, omega) / s1(I * h, const, eta, omega))
+    D = omega ** 2 / (s1(I * h, const, eta, omega) * s2(J * h, const, eta, omega) * cc ** 2) \
+        - (W + E + S + N)
+    return W, E, S, N, D
+
+
 def stencil_coefficients(const, eta, omega, h, n, c_mat):
     """Return (W, E, S, N, D) as (n, n) complex arrays indexed [j-1, i-1].
 
@@ -87,16 +104,32 @@ def stencil_coefficients(const, eta, omega, h, n, c_mat):
     idx = np.arange(1, n + 1, dtype=np.float64)
     I = idx[None, :]          # i along columns (fast axis)
     J = idx[:, None]          # j along rows   (slow axis)
-    inv_h2 = 1 / h ** 2
-    W = inv_h2 * (s1((I - .5) * h, const, eta, omega) / s2(J * h, const, eta, omega))
-    E = inv_h2 * (s1((I + .5) * h, const, eta, omega) / s2(J * h, const, eta, omega))
-    S = inv_h2 * (s2((J - .5) * h, const, eta, omega) / s1(I * h, const, eta, omega))
-    N = inv_h2 * (s2((J + .5) * h, const, eta, omega) / s1(I * h, const, eta, omega))
     # c_mat[i-1, j-1] at (row j-1, col i-1) of our [j, i] layout -> transpose.
     cc = np.asarray(c_mat)[:n, :n].T
-    D = omega ** 2 / (s1(I * h, const, eta, omega) * s2(J * h, const, eta, omega) * cc ** 2) \
-        - (W + E + S + N)
-    return W, E, S, N, D
+    return coefficients_at(const, eta, omega, h, I, J, cc)
+
+
+def apply_at_points(const, eta, omega, h, n, c_of, x, P, stencil=5, weights=None):
+    """(A x)[P] for flat 0-based indices P without assembling A (for grids too large to
+    assemble on the host).  ``c_of(I, J)`` returns the velocity c_mat[i-1, j-1] at 1-based
+    points; ``x`` is the full (n*n,) vector.  stencil=9 uses stencil9_coefficients' formulas
+    (weights default STENCIL9_WEIGHTS)."""
+    P = np.asarray(P, dtype=np.int64)
+    J, I = P // n + 1, P % n + 1
+    X = np.asarray(x)
+
+    def u(di, dj):
+        ii, jj = I + di, J + dj
+        ok = (ii >= 1) & (ii <= n) & (jj >= 1) & (jj <= n)
+        out = np.zeros(P.shape, dtype=np.complex128)
+        out[ok] = X[(jj[ok] - 1) * n + (ii[ok] - 1)]
+        return out
+
+    if stencil == 5:
+        W, E, S, N, D = coefficients_at(const, eta, omega, h, I, J, c_of(I, J))
+        return S * u(0, -1) + W * u(-1, 0) + D * u(0, 0) + E * u(1, 0) + N * u(0, 1)
+    co = _coef9(const, eta, omega, h, n, I, J, c_of(I, J), weights or STENCIL9_WEIGHTS)
+    return sum(co[k] * u(di, dj) for k, di, dj in _OFF9)
 
 
 def build_A_matrix(b, const, eta, omega, h, n, c_mat):
@@ -139,17 +172,14 @@ def build_A_matrix(b, const, eta, omega, h, n, c_mat):
 STENCIL9_WEIGHTS = (0.7910350, 0.6276117, 0.0948567)  # (alpha, c, d), tools/optimize_9pt.py
 
 
-def stencil9_coefficients(const, eta, omega, h, n, c_mat, weights=STENCIL9_WEIGHTS):
-    """The nine coefficient arrays [j-1, i-1] of the 9-point operator, as a dict with keys
-    sw, s, se, w, c, e, nw, n, ne (neighbour offsets (di, dj) = (-1,-1), (0,-1), ...).
-    Entries for neighbours outside the grid are returned too; the assembly drops them."""
+def _coef9(const, eta, omega, h, n, I, J, cc, weights):
+    """the nine coefficients at 1-based points (I, J), cc = velocity there (see below)."""
     alpha, cw, dw = (float(v) for v in weights)
     g = (1.0 - alpha) / 2.0
     ew = (1.0 - cw - 4.0 * dw) / 4.0
-    W, E, S, N, D = stencil_coefficients(const, eta, omega, h, n, c_mat)
-    idx = np.arange(1, n + 1, dtype=np.float64)
-    I = idx[None, :]
-    J = idx[:, None]
+    I = np.asarray(I, dtype=np.float64)
+    J = np.asarray(J, dtype=np.float64)
+    W, E, S, N, D = coefficients_at(const, eta, omega, h, I, J, cc)
     inv_h2 = 1 / h ** 2
     AW = inv_h2 * s1((I - .5) * h, const, eta, omega)
     AE = inv_h2 * s1((I + .5) * h, const, eta, omega)
@@ -159,7 +189,6 @@ def stencil9_coefficients(const, eta, omega, h, n, c_mat, weights=STENCIL9_WEIGH
     R2p = 1 / s2((J + 1) * h, const, eta, omega)
     R1m = 1 / s1(np.maximum(I - 1, 1) * h, const, eta, omega)   # clamped like the kernel:
     R1p = 1 / s1(np.minimum(I + 1, n) * h, const, eta, omega)   # only multiplies ghosts
-    cc = np.asarray(c_mat)[:n, :n].T
     M = omega ** 2 / (s1(I * h, const, eta, omega) * s2(J * h, const, eta, omega) * cc ** 2)
     Wm, Em, Wp, Ep = AW * R2m, AE * R2m, AW * R2p, AE * R2p
     Sm, Nm, Sp, Np = BS * R1m, BN * R1m, BS * R1p, BN * R1p
@@ -170,6 +199,15 @@ def stencil9_coefficients(const, eta, omega, h, n, c_mat, weights=STENCIL9_WEIGH
         "nw": g * (Wp + Nm) + ew * M, "n": alpha * N - g * (Wp + Ep) + dw * M,
         "ne": g * (Ep + Np) + ew * M,
     }
+
+
+def stencil9_coefficients(const, eta, omega, h, n, c_mat, weights=STENCIL9_WEIGHTS):
+    """The nine coefficient arrays [j-1, i-1] of the 9-point operator, as a dict with keys
+    sw, s, se, w, c, e, nw, n, ne (neighbour offsets (di, dj) = (-1,-1), (0,-1), ...).
+    Entries for neighbours outside the grid are returned too; the assembly drops them."""
+    idx = np.arange(1, n + 1, dtype=np.float64)
+    cc = np.asarray(c_mat)[:n, :n].T
+    return _coef9(const, eta, omega, h, n, idx[None, :], idx[:, None], cc, weights)
 
 
 _OFF9 = (("sw", -1, -1), ("s", 0, -1), ("se", 1, -1), ("w", -1, 0), ("c", 0, 0),
