@@ -630,8 +630,12 @@ HH_API int hh_ctx_create_ex(int device, int rank, int world, const unsigned char
       c->comm = transport == TRANSPORT_RCCL ? make_rccl_comm(rank, world, id)
                                             : make_shm_comm(rank, world, id);
   } catch (...) {
+    if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+    if (c->ev_halo) (void)hipEventDestroy(c->ev_halo);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
+    dfree(c->dscratch);
+    if (c->hpinned) (void)hipHostFree(c->hpinned);
     throw;
   }
   *out = c.release();
@@ -1179,18 +1183,33 @@ HH_API int hh_op_time_apply_set(hh_op* op, const hh_vec* const* xs, hh_vec* cons
   // no per-launch event is inserted between them.  Otherwise (halo exchange, several
   // launches) events are recorded around the interior stencil launch of every apply.
   const bool single = mode == HH_APPLY_A && op->ctx->world == 1 && op->slabs.size() == 1;
+  // every event is released on every exit path (a failing call must not leak them)
+  struct Events {
+    std::vector<hipEvent_t> ev;
+    hipEvent_t make() {
+      hipEvent_t e = nullptr;
+      HIPC(hipEventCreate(&e));
+      ev.push_back(e);
+      return e;
+    }
+    ~Events() {
+      for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    }
+  } events;
+  struct TimingHooks {  // the operator's timing hooks never outlive this call
+    hh_op* op;
+    ~TimingHooks() { op->tk0 = op->tk1 = nullptr; }
+  } hooks{op};
   std::vector<hipEvent_t> k0, k1;
   if (!single) {
     k0.resize(iters);
     k1.resize(iters);
     for (int i = 0; i < iters; ++i) {
-      HIPC(hipEventCreate(&k0[i]));
-      HIPC(hipEventCreate(&k1[i]));
+      k0[i] = events.make();
+      k1[i] = events.make();
     }
   }
-  hipEvent_t t0, t1;
-  HIPC(hipEventCreate(&t0));
-  HIPC(hipEventCreate(&t1));
+  hipEvent_t t0 = events.make(), t1 = events.make();
   HIPC(hipStreamSynchronize(s));
   HIPC(hipEventRecord(t0, s));
   for (int i = 0; i < iters; ++i) {
@@ -1214,13 +1233,9 @@ HH_API int hh_op_time_apply_set(hh_op* op, const hh_vec* const* xs, hh_vec* cons
       float km = 0.f;
       HIPC(hipEventElapsedTime(&km, k0[i], k1[i]));
       ksum += km;
-      (void)hipEventDestroy(k0[i]);
-      (void)hipEventDestroy(k1[i]);
     }
     *kernel_ms = ksum / iters;
   }
-  (void)hipEventDestroy(t0);
-  (void)hipEventDestroy(t1);
   GUARD_END
 }
 
