@@ -495,6 +495,7 @@ __global__ __launch_bounds__(kStencilThreads) void point_kernel(const PointArgs 
 // DESIGN.md "stencil variants"); the benchmark kernel (EPI_AX) can run all 12 variants.
 constexpr int kDefaultVariant = 30;  // XM_LDS, PF 1, NT stores + NT 1/c^2 loads, cached u, 512-wide
 constexpr int kSmallVariant = 18;    // 256-wide strips, NT u loads (grids below 2048)
+constexpr int kSmallCachedVariant = 6;  // 256-wide strips, cached u (plain apply below 2048)
 constexpr int kSolveVariant = 42;    // kDefaultVariant with NT u loads: solve epilogues, rows <= kLongRow
 constexpr int kLongRow = 4608;
 // The 9-point operator instantiates the four LDS-exchange shapes below and takes the 5-point
@@ -590,8 +591,11 @@ int stencil_resolve_variant(int epi, int requested, int n) {
   // The solve epilogues, whose input the previous kernel has just written, gain ~1 % from
   // NT u loads on rows up to kLongRow (tools/tune_gmres_variant.py,
   // profiles/r01i_tune_gmres_variant.log) and lose 4-8 % beyond.
+  //   Below n = 2048 a grid's vectors fit the 256 MiB Infinity Cache: the plain apply then
+  // loads u through the cache as well (1024^2: 8.6 vs 9.6 us with NT u loads,
+  // profiles/r01w_tune_const_1024.log).
   int autov = kDefaultVariant;
-  if (n < 2048) autov = kSmallVariant;
+  if (n < 2048) autov = epi == EPI_AX ? kSmallCachedVariant : kSmallVariant;
   else if (epi != EPI_AX && n <= kLongRow) autov = kSolveVariant;
   if (requested < 0) return autov;
   if (epi == EPI_AX) return stencil_variant_valid(requested) ? requested : autov;
