@@ -37,6 +37,8 @@ def _medium_arguments(c_mat, n):
       trick c_mat / sqrt(1 + i beta)) -> |c| field and mass scale 1/z^2, which gives the
       reference's omega^2 / (s1 s2 c_mat^2) exactly in exact arithmetic.
     """
+    if int(n) < 1:
+        raise ValueError(f"n must be >= 1 (got {n})")
     c = np.asarray(c_mat)
     if c.ndim != 2 or c.shape[0] < n + 2 or c.shape[1] < n + 2:
         raise ValueError(f"c_mat must be at least ({n + 2}, {n + 2}); got {c.shape}")

@@ -1,0 +1,118 @@
+"""GPU tier: error behaviour of the boundary (include/helmholtz_amd.h through the ctypes shim).
+
+The reference raises Python exceptions (scipy's ValueError on shape mismatches, numpy errors);
+the build raises ValueError / TypeError in the shim for what it can check on the host, and
+HHError (a negative hh_err with hh_last_error()'s message) for what the C library rejects.
+After any rejected call the objects stay usable.
+"""
+import numpy as np
+import pytest
+import scipy.sparse.linalg
+
+import helmholtz_preconditioner_amd as H
+from conftest import medium, rand_complex
+from oracle import helmholtz_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = H.Context(device=0)
+    H.set_default_context(c)
+    yield c
+    H.set_default_context(None)
+
+
+@pytest.fixture(scope="module")
+def op(ctx):
+    n = 40
+    om, h, eta = O.problem_params(n, 6, 3.0, 2.0)
+    A = H.build_A_matrix(6, 81.0, eta, om, h, n, medium("c1", n), context=ctx)
+    R = O.build_A_matrix(6, 81.0, eta, om, h, n, medium("c1", n))
+    return A, R, (om, h, eta)
+
+
+def _still_works(A, R):
+    x = rand_complex(A.shape[0], 1)
+    assert np.linalg.norm(A @ x - R @ x) <= 1e-12 * np.linalg.norm(R @ x)
+
+
+def test_bad_operator_arguments(ctx):
+    om, h, eta = O.problem_params(8, 2, 3.0, 2.0)
+    with pytest.raises(ValueError, match="n must be"):
+        H.build_A_matrix(2, 81.0, eta, om, h, 0, np.ones((2, 2)), context=ctx)
+    with pytest.raises(ValueError, match="c_mat must be"):
+        H.build_A_matrix(2, 81.0, eta, om, h, 8, np.ones((5, 5)), context=ctx)
+    cm = np.ones((10, 10), complex)
+    cm[0, 0] = 1j
+    with pytest.raises(ValueError, match="single common phase"):
+        H.build_A_matrix(2, 81.0, eta, om, h, 8, cm, context=ctx)
+    with pytest.raises(H.HHError, match="positive"):
+        H.build_A_matrix(2, 81.0, 0.0, om, h, 8, np.ones((10, 10)), context=ctx)
+    with pytest.raises(ValueError, match="stencil must be 5 or 9"):
+        H.build_A_matrix(2, 81.0, eta, om, h, 8, np.ones((10, 10)), context=ctx, stencil=7)
+
+
+def test_bad_apply_and_vector_shapes(op):
+    A, R, _ = op
+    with pytest.raises(ValueError, match="dimension mismatch"):
+        A @ np.ones(A.shape[0] + 1, complex)
+    with pytest.raises(ValueError, match="expected"):
+        A.vector(np.ones(3, complex))
+    x, y = A.vector(), A.vector()
+    with pytest.raises(ValueError):
+        A.time_apply([x, y], [y], 2)
+    with pytest.raises(H.HHError, match="distinct"):
+        A.time_apply(x, x, 2)
+    _still_works(A, R)
+
+
+def test_bad_solver_arguments(op):
+    A, R, (om, h, eta) = op
+    f = np.ones(A.shape[0], complex)
+    with pytest.raises(H.HHError, match="restart must be"):
+        H.gmres(A, f, restart=40, maxiter=2)
+    with pytest.raises(ValueError, match="unknown preconditioner"):
+        H.gmres(A, f, M="ilu", maxiter=2)
+    with pytest.raises(TypeError, match="host LinearOperator"):
+        H.gmres(A, f, M=scipy.sparse.linalg.aslinearoperator(R), maxiter=2)
+    B = H.build_A_matrix(6, 81.0, eta, om, h, A.n, medium("c1", A.n))
+    with pytest.raises(ValueError, match="different operator"):
+        H.gmres(A, f, M=H.Jacobi(B), maxiter=2)
+    with pytest.raises(ValueError, match="Unknown callback_type"):
+        H.gmres(A, f, callback=lambda r: None, callback_type="nope", maxiter=2)
+    with pytest.raises(ValueError, match="expected"):
+        H.gmres(A, f[:-1], maxiter=2)
+    with pytest.raises(TypeError):
+        H.gmres(R, f, maxiter=2)
+    # the operator and the solver still work after every rejection
+    x, info, hist = H.gmres(A, f, rtol=1e-3, maxiter=5, callback=lambda r: None,
+                            callback_type="legacy", return_history=True)
+    xr, infor, histr, _ = O.gmres_reference(R, f, rtol=1e-3, maxiter=5)
+    assert info == infor and np.max(np.abs(hist - histr) / histr) < 1e-6
+    _still_works(A, R)
+
+
+def test_bad_tuning_and_preconditioner_settings(op):
+    A, R, _ = op
+    with pytest.raises(H.HHError, match="not instantiated"):
+        A.tune(999)
+    with pytest.raises(H.HHError, match="sweeps must be"):
+        A.set_preconditioner(H._ffi.HH_PREC_SHIFTED_LAPLACE, 0.5, 0, 0.7)
+    with pytest.raises(H.HHError, match="unknown preconditioner kind"):
+        A.set_preconditioner(17)
+    A.tune(-1)
+    A.set_preconditioner(H._ffi.HH_PREC_NONE)
+    _still_works(A, R)
+
+
+def test_sweeping_needs_one_slab():
+    c = H.Context(device=0, virtual_slabs=2)
+    n = 32
+    om, h, eta = O.problem_params(n, 6, 3.0, 2.0)
+    A = H.build_A_matrix(6, 81.0, eta, om, h, n, medium("c1", n), context=c)
+    with pytest.raises(H.HHError, match="one rank and one slab"):
+        H.gmres(A, np.ones(n * n, complex), M=H.Sweeping(A), maxiter=2)
+    R = O.build_A_matrix(6, 81.0, eta, om, h, n, medium("c1", n))
+    _still_works(A, R)
