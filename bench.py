@@ -297,8 +297,7 @@ def main():
         # stencil + sweep launches, 16 + 56 B per further sweep.
         js = [i % args.restart for i in range(its)]
         N = float(n) * n
-        fused = (args.sl_sweeps == 2 and world == 1 and args.virtual_slabs == 1
-                 and args.stencil == 5)
+        fused = args.sl_sweeps == 2 and world == 1 and args.virtual_slabs == 1
         sl_extra = 0 if fused else bpp + 16 + 56 * (args.sl_sweeps - 1)
         pre = {"sl": sl_extra, "jacobi": 0, "none": 0}[args.precond]
         gbytes = sum((bpp + pre) * N + 16 * (j + 2) * N + 16 * (j + 3) * N for j in js)

@@ -125,7 +125,7 @@ int launch_probe_kind(int kind, int blocks, const double2* u, const double* ic, 
 int stencil_grid_blocks(int n, int rows, int rows_per_block, int row_step = 0);
 int stencil_bands(int rows, int rows_per_block, int row_step);  // tiles along j
 // Fused M A for the two-sweep shifted-Laplace M (sl_fused.hip): a.u = v, a.out0 = w; single
-// slab whose halo rows are zero rows.
+// slab whose halo rows are zero rows; a.tab_r2x != nullptr selects the 9-point operator.
 void launch_sl2(bool const_c, const StencilArgs& a, hipStream_t stream, int variant = -1);
 int stencil_rows_per_block(int n, int rows);
 void launch_point(int op, bool const_c, const PointArgs& a, int blocks, hipStream_t stream);

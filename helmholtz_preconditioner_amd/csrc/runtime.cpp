@@ -273,8 +273,7 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
 // first sweep never leave the chip.  Single slab of a single rank only (the fused band reads
 // v two rows beyond its own, which a cross-slab halo of one row does not carry).
 bool sl_fused_applies(const hh_op* op) {
-  return op->sl_fuse && op->sweeps == 2 && op->slabs.size() == 1 && op->ctx->world == 1 &&
-         op->points == 5;
+  return op->sl_fuse && op->sweeps == 2 && op->slabs.size() == 1 && op->ctx->world == 1;
 }
 void run_sl2(hh_op* op, const double2* v, const double* vs, double2* out) {
   const Slab& s = op->slabs[0];
@@ -296,6 +295,8 @@ void run_sl2(hh_op* op, const double2* v, const double* vs, double2* out) {
   a.in_scale = vs;
   a.out0 = out + s.off;
   a.stop = op->stop_flag;
+  a.tab_r2x = op->points == 9 ? s.tab_r2x : nullptr;  // selects the 9-point kernel
+  a.w9 = op->w9;
   if (op->tk0) HIPC(hipEventRecord(op->tk0, op->ctx->stream));
   launch_sl2(op->const_c, a, op->ctx->stream, op->variant);
   if (op->tk1) HIPC(hipEventRecord(op->tk1, op->ctx->stream));

@@ -19,6 +19,7 @@
 // to the two-launch path.
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
+#include "hh_stencil9.hpp"
 
 #include <type_traits>
 
@@ -189,7 +190,235 @@ __device__ __forceinline__ void sl2_tile(const StencilArgs& a, const int t) {
   __syncthreads();  // LDS reuse by the block's next tile
 }
 
+// The same fused M A for the 9-point operator, in stencil.hip's separable form
+// term for term (so w is bit-identical to the two-launch path): with X(r) the x second
+// difference of row r, Y(i) the y one of column i and H(r) = u_W + u_E of row r,
+//   A u = alpha (X(r) + Y(i)) + g (X(r-1) + X(r+1) + Y(i-1) + Y(i+1)) + M (c u_C + d edges + e corners).
+// Each stage (first sweep on row s = r+1, second sweep on row r) brings one new row into LDS
+// (v row s+1 / z1 row r+1) and exchanges its Y through LDS: one barrier per stage.  X and H of
+// the two previous rows stay in registers.  The strip's edge lanes add Y of the v halo columns
+// (i0-2, i0+TPB-1) from the v ring's halo slots; z1 needs no halo (the strips overlap).
+// Row inputs (1/c^2, edges, tables) are prefetched three rows ahead: the first sweep on row s
+// needs the edges and 1/s2 of row s+1.
 template <bool CONSTC, bool NTU, int TPB>
+__device__ __forceinline__ void sl2_tile9(const StencilArgs& a, const int t) {
+  constexpr int WO = TPB - 2;
+  __shared__ double2 lv[4][TPB + 2];  // v rows, slot(row) = (row - rb + 2) & 3
+  __shared__ double2 lyv[TPB + 2];    // Y of v on the first-sweep row
+  __shared__ double2 lz[TPB + 2];     // z1 row entering the second sweep
+  __shared__ double2 lyz[TPB + 2];    // Y of z1 on the second-sweep row
+  const int tx = t % a.tiles_x;
+  const int ty = t / a.tiles_x;
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int n = a.n, nl = a.nl;
+  const int i0 = tx * WO;
+  const int c = i0 + tid - 1;
+  const bool cin = c >= 0 && c < n;
+  const int cc = min(max(c, 0), n - 1);
+  const bool outl = tid >= 1 && tid <= TPB - 2 && cin;
+  const int rb = __builtin_amdgcn_readfirstlane(a.row_begin + ty * a.row_step);
+  const int re = __builtin_amdgcn_readfirstlane(min(rb + a.rows_per_block, a.row_end));
+  int ie = lane < kWave / 2 ? i0 - 2 : i0 + TPB - 1;
+  const bool lw = tid == 0 && i0 - 2 >= 0;
+  const bool le = tid == TPB - 1 && i0 + TPB - 1 < n;
+  ie = min(max(ie, 0), n - 1);
+  const double2 z2 = make_double2(0.0, 0.0);
+  const Stencil9W w = a.w9;
+
+  auto rowp = [&](int r) -> const double2* {
+    return r < 0 ? a.halo_lo : (r >= nl ? a.halo_hi : a.u + (size_t)r * n);
+  };
+  auto load_v = [&](int r) -> double2 {
+    const double2* p = rowp(r) + cc;
+    if constexpr (NTU)
+      return make_double2(__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y));
+    else
+      return *p;
+  };
+  auto load_in = [&](int r, RowIn& v) {
+    const int rc = min(max(r, 0), nl - 1);
+    if constexpr (!CONSTC) v.ic = __builtin_nontemporal_load(a.invc2 + (size_t)rc * n + cc);
+    else v.ic = a.invc2_const;
+    v.e = rowp(r)[ie];
+  };
+  const cdouble_p tabj = (cdouble_p)(a.tab_j);
+  auto load_tab = [&](int r, RowTab& tb) {
+    const int ru = __builtin_amdgcn_readfirstlane(min(max(r, 0), nl - 1));
+    const cdouble_p q = tabj + 8 * ru;
+    tb.R2 = make_double2(q[0], q[1]);
+    tb.BS = make_double2(q[2], q[3]);
+    tb.BN = make_double2(q[4], q[5]);
+    tb.OM = make_double2(q[6], q[7]);
+  };
+  const double2 AW = a.tab_i[cc], AE = a.tab_i[n + cc], R1 = a.tab_i[2 * n + cc];
+  const double2 R1e = a.tab_i[2 * n + ie];  // the edge lanes' halo column
+  const double sin = a.in_scale ? *a.in_scale : 1.0;
+  auto xdiff = [&](double2 R2, double2 uW, double2 uC, double2 uE) {
+    return cmul(R2, cfma(AE, csub(uE, uC), cmul(AW, csub(uW, uC))));
+  };
+  auto ydiff = [&](double2 R, const RowTab& tb, double2 uS, double2 uC, double2 uN) {
+    return cmul(R, cfma(tb.BN, csub(uN, uC), cmul(tb.BS, csub(uS, uC))));
+  };
+  // the 9-point product from the separable terms (stencil.hip, S9 step, same association)
+  auto op9 = [&](double2 Mo, double2 Xm, double2 Xc, double2 Xp, double2 Yc, double2 Yw,
+                 double2 Ye, double2 Hm, double2 Hc, double2 Hp, double2 uS, double2 uC,
+                 double2 uN) {
+    const double2 lap = cadd(Xc, Yc);
+    const double2 avg = cadd(cadd(Xm, Xp), cadd(Yw, Ye));
+    const double2 edges = cadd(Hc, cadd(uS, uN));
+    const double2 corners = cadd(Hm, Hp);
+    const double2 mix = cadd(cadd(cscale(uC, w.c), cscale(edges, w.d)), cscale(corners, w.e));
+    return cfma(Mo, mix, cadd(cscale(lap, w.alpha), cscale(avg, w.g)));
+  };
+  auto sum4_of = [&](const RowTab& tb) {
+    const double2 W = cmul(AW, tb.R2);
+    const double2 E = cmul(AE, tb.R2);
+    const double2 S = cmul(tb.BS, R1);
+    const double2 N = cmul(tb.BN, R1);
+    return cadd(cadd(cadd(W, E), S), N);
+  };
+
+  double2 Xvm, Xvc, Hvm, Hvc;  // v: X, H of rows s-1, s
+  double2 Xzm, Xzc, Hzm, Hzc;  // z1: X, H of rows r-1, r
+  // first sweep on row s: row s+1 (vN, its edge eN, tables tbN) enters the v ring
+  auto stage1 = [&](int s, double2 vS, double2 vC, double2 vN, double2 eN, const RowIn& in,
+                    const RowTab& tb, const RowTab& tbN, double2& T, double2& z1)
+      __attribute__((always_inline)) {
+    double2* lS = lv[(s - 1 - rb + 2) & 3];
+    double2* lC = lv[(s - rb + 2) & 3];
+    double2* lN = lv[(s + 1 - rb + 2) & 3];
+    const double2 Yc = ydiff(R1, tb, vS, vC, vN);
+    lN[tid + 1] = csel(cin, vN, z2);
+    lyv[tid + 1] = csel(cin, Yc, z2);
+    if (tid == 0) {
+      const double2 e = csel(lw, eN, z2);
+      lN[0] = e;
+      lyv[0] = ydiff(R1e, tb, lS[0], lC[0], e);
+    }
+    if (tid == TPB - 1) {
+      const double2 e = csel(le, eN, z2);
+      lN[TPB + 1] = e;
+      lyv[TPB + 1] = ydiff(R1e, tb, lS[TPB + 1], lC[TPB + 1], e);
+    }
+    __syncthreads();
+    const double2 vNW = lN[tid], vNE = lN[tid + 2];
+    const double2 Yw = lyv[tid], Ye = lyv[tid + 2];
+    const double2 Xp = xdiff(tbN.R2, vNW, vN, vNE);
+    const double2 Hp = cadd(vNW, vNE);
+    const double2 M = cscale(cmul(tb.OM, R1), in.ic);
+    const double2 Db = stencil9_diag(cmul(M, a.mshift), sum4_of(tb), w);
+    T = cscale(op9(M, Xvm, Xvc, Xp, Yc, Yw, Ye, Hvm, Hvc, Hp, vS, vC, vN), sin);
+    z1 = csel(cin && s >= 0 && s < nl, cscale(cdiv(T, Db), a.damping), z2);
+    Xvm = Xvc;
+    Xvc = Xp;
+    Hvm = Hvc;
+    Hvc = Hp;
+  };
+  // second sweep on row r: w = z1 + damp (T - A_beta z1) / Db; z1 row r+1 enters
+  auto stage2 = [&](double2 zS, double2 zC, double2 zN, double2 T, const RowIn& in,
+                    const RowTab& tb, const RowTab& tbN) __attribute__((always_inline)) -> double2 {
+    const double2 Yc = ydiff(R1, tb, zS, zC, zN);
+    lz[tid + 1] = zN;
+    lyz[tid + 1] = Yc;
+    __syncthreads();
+    const double2 zNW = lz[tid], zNE = lz[tid + 2];
+    const double2 Yw = lyz[tid], Ye = lyz[tid + 2];
+    const double2 Xp = xdiff(tbN.R2, zNW, zN, zNE);
+    const double2 Hp = cadd(zNW, zNE);
+    const double2 M = cscale(cmul(tb.OM, R1), in.ic);
+    const double2 Mb = cmul(M, a.mshift);
+    const double2 Db = stencil9_diag(Mb, sum4_of(tb), w);
+    const double2 Au = op9(Mb, Xzm, Xzc, Xp, Yc, Yw, Ye, Hzm, Hzc, Hp, zS, zC, zN);
+    Xzm = Xzc;
+    Xzc = Xp;
+    Hzm = Hzc;
+    Hzc = Hp;
+    return cadd(zC, cscale(cdiv(csub(T, Au), Db), a.damping));
+  };
+
+  // rings of four by row, slot(row) = (row - rb + 2) & 3: v rows r .. r+3, z1 / T rows
+  // r-1 .. r+1, row inputs and tables rows r .. r+3 (r+3 in flight)
+  double2 V[4], Z[4], TT[4];
+  RowIn IN[4];
+  RowTab TB[4];
+  if (tid == 0) {  // halo slots of the z1 rows: only lanes 0 / TPB-1 read them, for outputs
+    lz[0] = z2;    // nobody stores
+    lyz[0] = z2;
+  }
+  if (tid == TPB - 1) {
+    lz[TPB + 1] = z2;
+    lyz[TPB + 1] = z2;
+  }
+  V[0] = load_v(rb - 2);
+  V[1] = load_v(rb - 1);
+  V[2] = load_v(rb);
+  V[3] = load_v(rb + 1);
+  RowIn inm2;
+  load_in(rb - 2, inm2);  // edges of row rb-2 (the ring's first row)
+  load_in(rb - 1, IN[1]);
+  load_in(rb, IN[2]);
+  load_in(rb + 1, IN[3]);
+  load_in(rb + 2, IN[0]);
+  RowTab tbm2;
+  load_tab(rb - 2, tbm2);
+  load_tab(rb - 1, TB[1]);
+  load_tab(rb, TB[2]);
+  load_tab(rb + 1, TB[3]);
+  load_tab(rb + 2, TB[0]);
+  // rows rb-2 and rb-1 enter the v ring; X, H of both from it
+  lv[0][tid + 1] = csel(cin, V[0], z2);
+  lv[1][tid + 1] = csel(cin, V[1], z2);
+  if (tid == 0) {
+    lv[0][0] = csel(lw, inm2.e, z2);
+    lv[1][0] = csel(lw, IN[1].e, z2);
+  }
+  if (tid == TPB - 1) {
+    lv[0][TPB + 1] = csel(le, inm2.e, z2);
+    lv[1][TPB + 1] = csel(le, IN[1].e, z2);
+  }
+  __syncthreads();
+  Xvm = xdiff(tbm2.R2, lv[0][tid], V[0], lv[0][tid + 2]);
+  Hvm = cadd(lv[0][tid], lv[0][tid + 2]);
+  Xvc = xdiff(TB[1].R2, lv[1][tid], V[1], lv[1][tid + 2]);
+  Hvc = cadd(lv[1][tid], lv[1][tid + 2]);
+  stage1(rb - 1, V[0], V[1], V[2], IN[2].e, IN[1], TB[1], TB[2], TT[1], Z[1]);
+  V[0] = load_v(rb + 2);
+  __syncthreads();  // lyv is rewritten by the next first sweep
+  stage1(rb, V[1], V[2], V[3], IN[3].e, IN[2], TB[2], TB[3], TT[2], Z[2]);
+  // the second sweep's register ring starts with X, H of z1 rows rb-1 and rb
+  lz[tid + 1] = Z[1];
+  lyz[tid + 1] = Z[2];
+  __syncthreads();
+  Xzm = xdiff(TB[1].R2, lz[tid], Z[1], lz[tid + 2]);
+  Hzm = cadd(lz[tid], lz[tid + 2]);
+  Xzc = xdiff(TB[2].R2, lyz[tid], Z[2], lyz[tid + 2]);
+  Hzc = cadd(lyz[tid], lyz[tid + 2]);
+  __syncthreads();
+
+  for (int r0 = rb; r0 < re; r0 += 4) {
+    unroll<0, 4>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      const int r = r0 + k;
+      const bool live = r < re;
+      V[(k + 1) & 3] = load_v(min(r + 3, re + 1));
+      load_in(min(r + 3, re + 1), IN[(k + 1) & 3]);
+      load_tab(min(r + 3, re + 1), TB[(k + 1) & 3]);
+      stage1(r + 1, V[(k + 2) & 3], V[(k + 3) & 3], V[k & 3], IN[k & 3].e, IN[(k + 3) & 3],
+             TB[(k + 3) & 3], TB[k & 3], TT[(k + 3) & 3], Z[(k + 3) & 3]);
+      const double2 wv = stage2(Z[(k + 1) & 3], Z[(k + 2) & 3], Z[(k + 3) & 3], TT[(k + 2) & 3],
+                                IN[(k + 2) & 3], TB[(k + 2) & 3], TB[(k + 3) & 3]);
+      if (outl && live) {
+        double2* p = a.out0 + (size_t)r * n + c;
+        __builtin_nontemporal_store(wv.x, &p->x);
+        __builtin_nontemporal_store(wv.y, &p->y);
+      }
+    });
+  }
+  __syncthreads();  // LDS reuse by the block's next tile
+}
+
+template <bool CONSTC, bool NTU, int TPB, bool S9>
 __global__ __launch_bounds__(TPB) void sl2_kernel(const StencilArgs a) {
   if (a.stop && *a.stop) return;  // queued GMRES cycle already stopped
   const int L = blockIdx.x;
@@ -198,14 +427,21 @@ __global__ __launch_bounds__(TPB) void sl2_kernel(const StencilArgs a) {
   for (int tt = q; tt < a.tiles_per_xcd; tt += Q) {
     const int t = (L & 7) * a.tiles_per_xcd + tt;
     if (t >= ntiles) break;  // uniform per block
-    sl2_tile<CONSTC, NTU, TPB>(a, t);
+    if constexpr (S9) sl2_tile9<CONSTC, NTU, TPB>(a, t);
+    else sl2_tile<CONSTC, NTU, TPB>(a, t);
   }
 }
 
 template <int TPB, bool NTU>
 void launch_t(bool const_c, const StencilArgs& a, int blocks, hipStream_t s) {
-  if (const_c) hipLaunchKernelGGL((sl2_kernel<true, NTU, TPB>), dim3(blocks), dim3(TPB), 0, s, a);
-  else hipLaunchKernelGGL((sl2_kernel<false, NTU, TPB>), dim3(blocks), dim3(TPB), 0, s, a);
+  const bool s9 = a.tab_r2x != nullptr;  // 9-point operator (the tables themselves are unused)
+  if (const_c) {
+    if (s9) hipLaunchKernelGGL((sl2_kernel<true, NTU, TPB, true>), dim3(blocks), dim3(TPB), 0, s, a);
+    else hipLaunchKernelGGL((sl2_kernel<true, NTU, TPB, false>), dim3(blocks), dim3(TPB), 0, s, a);
+  } else {
+    if (s9) hipLaunchKernelGGL((sl2_kernel<false, NTU, TPB, true>), dim3(blocks), dim3(TPB), 0, s, a);
+    else hipLaunchKernelGGL((sl2_kernel<false, NTU, TPB, false>), dim3(blocks), dim3(TPB), 0, s, a);
+  }
 }
 
 }  // namespace

@@ -97,19 +97,43 @@ def test_gmres_epilogue_variants_vs_oracle(ctx, M_kind):
     A.tune(-1, 0, 0)
 
 
-@pytest.mark.parametrize("n,kind,rpb", [(97, "c2", 0), (700, "c1", 0), (700, "c1", 13),
-                                        (1100, "const", 0), (2100, "c1", 0), (2100, "c1", 5)])
-def test_fused_shifted_laplace_matches_two_launch_path(ctx, n, kind, rpb):
+def _sl9_reference(b, C, eta, om, h, n, cm, beta=0.5, damping=0.7):
+    """two damped-Jacobi sweeps on the shifted 9-point operator (oracle.build_A9_matrix)"""
+    import scipy.sparse.linalg
+    Ab = O.build_A9_matrix(b, C, eta, om, h, n, cm / np.sqrt(1 + 1j * beta))
+    dinv = 1.0 / Ab.diagonal()
+
+    def mv(r):
+        r = np.ravel(r)
+        z = damping * dinv * r
+        return z + damping * dinv * (r - Ab @ z)
+    return scipy.sparse.linalg.LinearOperator(Ab.shape, matvec=mv, dtype=np.complex128)
+
+
+@pytest.mark.parametrize("n,kind,rpb,stencil", [
+    (97, "c2", 0, 5), (700, "c1", 0, 5), (700, "c1", 13, 5), (1100, "const", 0, 5),
+    (2100, "c1", 0, 5), (2100, "c1", 5, 5),
+    (97, "c2", 0, 9), (700, "c1", 13, 9), (1100, "const", 0, 9), (2100, "c1", 0, 9),
+    (2100, "c1", 7, 9)])
+def test_fused_shifted_laplace_matches_two_launch_path(ctx, n, kind, rpb, stencil):
     """The one-launch M A of the two-sweep shifted-Laplace M (csrc/sl_fused.hip) against the
     stencil + sweep launch pair: bit-identical GMRES histories and fields (ragged n, 256- and
-    512-wide strips, odd band heights), and the first iterations against the oracle."""
+    512-wide strips, odd band heights, both stencils), and the first iterations against the
+    oracle."""
     b, C, wn, al = 12, 81.0, 10.0, 2.0
     cm = medium(kind, n)
     om, h, eta = O.problem_params(n, b, wn, al)
     f = O.init_f1_mat(.5, .125, om, n).ravel()
-    A = H.build_A_matrix(b, C, eta, om, h, n, cm, context=ctx)
+    A = H.build_A_matrix(b, C, eta, om, h, n, cm, context=ctx, stencil=stencil)
     M = H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7)
     A.tune(-1, rpb, 0)
+    x = rand_complex(n * n, 8)
+    ys = []
+    for fused in (True, False):
+        A.sl_fusion(fused)
+        M.configure()
+        ys.append(A._apply_host(x, H._ffi.HH_APPLY_PREC_A))
+    np.testing.assert_array_equal(ys[0], ys[1])
     res = []
     for fused in (True, False):
         A.sl_fusion(fused)
@@ -121,8 +145,13 @@ def test_fused_shifted_laplace_matches_two_launch_path(ctx, n, kind, rpb):
     A.tune(-1, 0, 0)
     np.testing.assert_array_equal(res[0][2], res[1][2])
     np.testing.assert_array_equal(res[0][0], res[1][0])
-    Aref = O.build_A_matrix(b, C, eta, om, h, n, cm)
-    Mref = O.shifted_laplace_jacobi(b, C, eta, om, h, n, cm, beta=0.5, sweeps=2, damping=0.7)[0]
+    if stencil == 9:
+        Aref = O.build_A9_matrix(b, C, eta, om, h, n, cm)
+        Mref = _sl9_reference(b, C, eta, om, h, n, cm)
+    else:
+        Aref = O.build_A_matrix(b, C, eta, om, h, n, cm)
+        Mref = O.shifted_laplace_jacobi(b, C, eta, om, h, n, cm, beta=0.5, sweeps=2,
+                                        damping=0.7)[0]
     # the reference's own rounding drift passes 1e-6 by iteration 6 at n = 2100
     K = 6 if n < 2000 else 4
     xr, infor, histr, _ = O.gmres_reference(Aref, f, M=Mref, rtol=1e-3, restart=20, maxiter=K)
