@@ -103,14 +103,14 @@ def measured_traffic(n, medium, world, stencil=5):
     on the probe kernels in the same run).  PMC counters cannot be read inside the timed
     run, so this is the committed measurement of the same kernel and workload (None
     otherwise)."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-    if not (n == 4096 and medium == "marmousi" and world == 1 and stencil == 5
-            and os.path.exists(path)):
+    name = "r01_pmc_traffic.json" if stencil == 5 else "r01_pmc_traffic_s9.json"
+    path = os.path.join(ROOT, "profiles", name)
+    if not (n == 4096 and medium == "marmousi" and world == 1 and os.path.exists(path)):
         return None, None
     rec = json.load(open(path)).get("stencil_kernel<0")
     if not rec:
         return None, None
-    return int(rec["fetch_x2"] + rec["write"]), ("profiles/r01_pmc_traffic.json: FETCH_SIZE x2 "
+    return int(rec["fetch_x2"] + rec["write"]), (f"profiles/{name}: FETCH_SIZE x2 "
                                                  "+ WRITE_SIZE per launch, same kernel/workload")
 
 

@@ -1,6 +1,7 @@
 """Profiling driver: only the operator apply (and optionally one GMRES cycle) at the bench
 workload, so rocprofv3 kernel-trace / PMC passes stay short.
 usage: python tools/prof_stencil.py [--n 4096] [--iters 50] [--medium marmousi] [--gmres]
+                                   [--stencil 9]
 """
 import argparse
 import os
@@ -17,11 +18,12 @@ p.add_argument("--gmres", action="store_true")
 p.add_argument("--variant", type=int, default=-1)
 p.add_argument("--rpb", type=int, default=0)
 p.add_argument("--rotate", type=int, default=3, help="distinct (x, y) pairs, as bench.py")
+p.add_argument("--stencil", type=int, default=5, choices=[5, 9])
 a = p.parse_args()
 n = a.n
 om, h, eta = H.problem_params(n, 12, 100.0, 2.0)
 cm = H.marmousi_like_c_mat(n) if a.medium == "marmousi" else H.constant_c_mat(n)
-A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm)
+A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, stencil=a.stencil)
 if a.variant >= 0 or a.rpb > 0:
     A.tune(variant=a.variant, rows_per_block=a.rpb)
 xs, ys = [A.vector() for _ in range(a.rotate)], [A.vector() for _ in range(a.rotate)]
