@@ -32,6 +32,7 @@ HH_APPLY_A, HH_APPLY_JACOBI_A, HH_APPLY_PREC, HH_APPLY_PREC_A = 0, 1, 2, 3
 HH_TRANSPORT_RCCL, HH_TRANSPORT_SHM = 0, 1
 
 GMRES_CALLBACK = ctypes.CFUNCTYPE(None, c_void_p, c_long, c_double)
+GMRES_CYCLE_CALLBACK = ctypes.CFUNCTYPE(None, c_void_p, c_long)
 
 
 class HHStats(ctypes.Structure):
@@ -73,6 +74,7 @@ SIGNATURES = [
     ("hh_gmres", c_int, [c_void_p, c_void_p, c_void_p, c_double, c_double, c_int, c_long, c_int,
                          c_int, c_dp, c_long, GMRES_CALLBACK, c_void_p, c_lp, c_ip, c_dp, c_dp]),
     ("hh_op_set_stencil", c_int, [c_void_p, c_int, c_double, c_double, c_double]),
+    ("hh_op_set_cycle_callback", c_int, [c_void_p, GMRES_CYCLE_CALLBACK, c_void_p]),
     ("hh_op_sl_fusion", c_int, [c_void_p, c_int]),
     ("hh_op_tune", c_int, [c_void_p, c_int, c_int, c_int]),
     ("hh_op_sweep_mode", c_int, [c_void_p, c_int, c_ip]),

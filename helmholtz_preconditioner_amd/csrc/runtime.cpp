@@ -154,6 +154,9 @@ struct hh_op {
   // tuning (hh_op_tune): stencil variant for the plain apply, rows per block override
   int variant = -1;
   int rpb_override = 0;
+  // hh_op_set_cycle_callback: scipy's callback_type='x' hook, once per restart cycle
+  hh_gmres_cycle_callback cycle_cb = nullptr;
+  void* cycle_user = nullptr;
   int grid_override = 0;
   hh_stats stats{};
 };
@@ -1240,6 +1243,14 @@ HH_API int hh_op_time_apply_set(hh_op* op, const hh_vec* const* xs, hh_vec* cons
   GUARD_END
 }
 
+HH_API int hh_op_set_cycle_callback(hh_op* op, hh_gmres_cycle_callback cb, void* user) {
+  GUARD_BEGIN
+  REQUIRE(op, "null op");
+  op->cycle_cb = cb;
+  op->cycle_user = user;
+  GUARD_END
+}
+
 HH_API int hh_op_set_stencil(hh_op* op, int points, double alpha, double c, double d) {
   GUARD_BEGIN
   REQUIRE(op, "null op");
@@ -1508,6 +1519,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       op->sw_const = nullptr;
       return HH_OK;
     }
+    if (op->cycle_cb) op->cycle_cb(op->cycle_user, op->stats.restarts);
     if (rnorm <= atol) break;
     else if (breakdown) break;
     else if (presid <= ptol) ptol_max_factor = std::max(eps, 0.25 * ptol_max_factor);

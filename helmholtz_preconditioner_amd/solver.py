@@ -61,9 +61,6 @@ def gmres(A, b, x0=None, *, rtol=1e-5, atol=0., restart=None, maxiter=None, M=No
         raise ValueError(f"Unknown callback_type: {callback_type!r}")
     if callback is None:
         callback_type = None
-    if callback_type == 'x':
-        raise NotImplementedError("callback_type='x' would download x every restart; "
-                                  "use 'pr_norm' or 'legacy'")
     n = A.shape[0]
     if restart is None:
         restart = 20
@@ -86,15 +83,24 @@ def gmres(A, b, x0=None, *, rtol=1e-5, atol=0., restart=None, maxiter=None, M=No
     cap = int(min(cap, 1 << 22))
     hist = np.zeros(max(cap, 1), dtype=np.float64)
     cb = _ffi.GMRES_CALLBACK(0)
-    if callback is not None:
+    ccb = _ffi.GMRES_CYCLE_CALLBACK(0)
+    if callback is not None and callback_type in ('legacy', 'pr_norm'):
         def _cb(_user, _it, rel):
             callback(rel)
         cb = _ffi.GMRES_CALLBACK(_cb)
+    elif callback is not None:  # 'x': the iterate after every restart cycle (downloaded for
+        def _ccb(_user, _cycle):  # numpy b, the DeviceVector itself otherwise)
+            callback(xv.download() if host_in else xv)
+        ccb = _ffi.GMRES_CYCLE_CALLBACK(_ccb)
     iters, info, rnorm, bnorm = ctypes.c_long(), ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
-    check(lib.hh_gmres(A.handle, bv.handle, xv.handle, float(rtol), float(atol), int(restart),
-                       int(maxiter), int(legacy), int(bool(reorth)), _ffi.dptr(hist), cap, cb,
-                       None, ctypes.byref(iters), ctypes.byref(info), ctypes.byref(rnorm),
-                       ctypes.byref(bnorm)))
+    check(lib.hh_op_set_cycle_callback(A.handle, ccb, None))
+    try:
+        check(lib.hh_gmres(A.handle, bv.handle, xv.handle, float(rtol), float(atol),
+                           int(restart), int(maxiter), int(legacy), int(bool(reorth)),
+                           _ffi.dptr(hist), cap, cb, None, ctypes.byref(iters),
+                           ctypes.byref(info), ctypes.byref(rnorm), ctypes.byref(bnorm)))
+    finally:
+        check(lib.hh_op_set_cycle_callback(A.handle, _ffi.GMRES_CYCLE_CALLBACK(0), None))
     A.last_solve = dict(iterations=iters.value, info=info.value, rnorm=rnorm.value,
                         bnorm=bnorm.value, stats=A.stats())
     x = xv.download() if host_in else xv

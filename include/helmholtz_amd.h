@@ -186,6 +186,12 @@ int hh_gmres(hh_op* op, const hh_vec* b, hh_vec* x, double rtol, double atol,
              int restart, long maxiter, int legacy_maxiter, int reorth,
              double* hist, long hist_cap, hh_gmres_callback cb, void* user,
              long* iters_out, int* info_out, double* rnorm_out, double* bnorm_out);
+/* Per-restart-cycle hook of the following hh_gmres calls on `op` (NULL removes it): called
+ * after each cycle's x update and true residual, where scipy calls callback(x) for
+ * callback_type='x' (iterative.py, after `r = b - matvec(x)`; not after the legacy exit);
+ * x is complete on the device, so the hook may download it (hh_vec_download). */
+typedef void (*hh_gmres_cycle_callback)(void* user, long cycle);
+int hh_op_set_cycle_callback(hh_op* op, hh_gmres_cycle_callback cb, void* user);
 
 /* Performance tuning of the stencil kernel used by HH_APPLY_A: variant in [0, 24)
  * selects the W/E exchange (LDS row / direct cached loads / wave shuffle), prefetch

@@ -163,3 +163,30 @@ def test_gmres_device_vectors_large(ctx):
     assert isinstance(xv, H.DeviceVector)
     assert np.max(np.abs(hist - histr) / histr) < TOL
     assert relerr(xv.download(), xr) < TOL
+
+
+@pytest.mark.parametrize("ctype", ["x", "pr_norm"])
+def test_gmres_callback_types_match_scipy(ctx, ctype):
+    """callback_type='x' (the iterate after each restart cycle) and 'pr_norm' (per inner
+    iteration; maxiter counts restart cycles) as scipy.sparse.linalg.gmres calls them."""
+    import scipy.sparse.linalg
+    n, b, C, wn, al = 40, 6, 61.0, 1.0, 2.0
+    cm = medium("c2", n)
+    om, h, eta = O.problem_params(n, b, wn, al)
+    Aref = O.build_A_matrix(b, C, eta, om, h, n, cm)
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    ref, got = [], []
+    xr, infor = scipy.sparse.linalg.gmres(Aref, f, rtol=1e-5, restart=10, maxiter=8,
+                                          M=O.jacobi_preconditioner(Aref),
+                                          callback=lambda v: ref.append(np.copy(v)),
+                                          callback_type=ctype)
+    A = H.build_A_matrix(b, C, eta, om, h, n, cm, context=ctx)
+    x, info = H.gmres(A, f, rtol=1e-5, restart=10, maxiter=8, M="jacobi",
+                      callback=lambda v: got.append(np.copy(v)), callback_type=ctype)
+    assert info == infor and len(got) == len(ref) > 1
+    if ctype == "x":
+        for g, r in zip(got, ref):
+            assert relerr(g, r) < 1e-6
+    else:
+        assert np.max(np.abs(np.array(got) - np.array(ref)) / np.array(ref)) < 1e-6
+    assert relerr(x, xr) < 1e-6
