@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--alpha", type=float, default=2.0)
     p.add_argument("--precond", default="sl", choices=["sl", "jacobi", "none"])
     p.add_argument("--sl-sweeps", type=int, default=2)
+    p.add_argument("--variant", type=int, default=-1,
+                   help="force a stencil kernel shape (hh_op_tune; -1 = the built-in choice)")
     p.add_argument("--stencil", type=int, default=5, choices=[5, 9],
                    help="5 = the reference's operator; 9 = the 9-point operator (SURVEY row F4)")
     p.add_argument("--gmres-iters", type=int, default=40, help="timed inner GMRES iterations")
@@ -107,7 +109,7 @@ def measured_traffic(n, medium, world, stencil=5):
     path = os.path.join(ROOT, "profiles", name)
     if not (n == 4096 and medium == "marmousi" and world == 1 and os.path.exists(path)):
         return None, None
-    rec = json.load(open(path)).get("stencil_kernel<0")
+    rec = json.load(open(path)).get("tile_kernel<0" if stencil == 5 else "stencil_kernel<0")
     if not rec:
         return None, None
     return int(rec["fetch_x2"] + rec["write"]), (f"profiles/{name}: FETCH_SIZE x2 "
@@ -203,6 +205,8 @@ def main():
                          stencil=args.stencil)
     t_init = time.perf_counter() - t0
     assert (A.row_begin, A.row_end) == (j0, j1)
+    if args.variant >= 0:
+        A.tune(args.variant)
     bpp = A.bytes_per_point
 
     # ---------------- SpMV: K timed steps, inputs resident in HBM ----------------
@@ -264,8 +268,10 @@ def main():
         "frac": round(achieved_min / HBM_PEAK_GBPS, 4),
         "traffic": traffic,
         "traffic_source": traffic_src,
-        "kernel": f"stencil_kernel<EPI_AX,{'true' if A.constant_medium else 'false'},"
-                  f"S9={'true' if args.stencil == 9 else 'false'}> (interior rows)",
+        "kernel": (f"tile_kernel<EPI_AX,{'true' if A.constant_medium else 'false'},4 rows> "
+                   "(interior rows)") if (args.stencil == 5 and n >= 2048 and args.variant < 0) else
+                  (f"stencil_kernel<EPI_AX,{'true' if A.constant_medium else 'false'},"
+                   f"S9={'true' if args.stencil == 9 else 'false'}> (interior rows)"),
         "kernel_ms": round(kern_ms, 5),
         "bytes_per_launch": bpp * interior_rows * n,
     }

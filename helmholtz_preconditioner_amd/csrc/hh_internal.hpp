@@ -117,7 +117,9 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a, int nblocks_out
                     hipStream_t stream, int variant = -1);
 int stencil_default_variant();
 bool stencil_variant_valid(int v);  // instantiated for the plain apply
-// the variant a launch really uses (requested < 0: size-dependent default)
+// the variant a launch really uses (requested < 0: size-dependent default; kVariantInSolve:
+// the default inside a GMRES cycle, whose inputs the previous kernel has just written)
+constexpr int kVariantInSolve = -2;
 int stencil_resolve_variant(int epi, int requested, int n);
 // Streaming roofline probes (probe.hip); returns the probe's bytes per point (0: unknown kind).
 int launch_probe_kind(int kind, int blocks, const double2* u, const double* ic, double2* y,

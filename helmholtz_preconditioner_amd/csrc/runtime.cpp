@@ -239,7 +239,8 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
                 op->partials_cap,
             "partials workspace too small for the stencil launch");
     int written = 0;
-    launch_stencil(epi, op->const_c, a, &written, c->stream, op->variant);
+    const int variant = (op->variant < 0 && op->stop_flag) ? kVariantInSolve : op->variant;
+    launch_stencil(epi, op->const_c, a, &written, c->stream, variant);
     nparts += written;
   };
 

@@ -443,6 +443,85 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
   if constexpr (T::nacc > 0 || XM == XM_LDS) __syncthreads();  // LDS reuse by the next tile
 }
 
+// Non-marching tile shape (tuning variants kTileVariant + R, plain apply of the 5-point
+// operator only): a 256-thread block computes an R-row x 256-column tile in one shot -- every
+// load of its R + 2 input rows, R 1/c^2 rows and R broadcast edge values is issued up front --
+// and exchanges W/E neighbours by wave shuffles (no LDS, no barrier).  Blocks run in plain
+// order, so the concurrently resident tiles cover one narrow address window of the grid (the
+// flat stream's access pattern), and vertically adjacent tiles (tiles_x blocks apart, a
+// multiple of 8) share an XCD's L2 for their halo rows.  Same per-point arithmetic as
+// stencil_tile: bit-identical results.
+template <int EPI, bool CONSTC, int R, bool NT, bool NTU>
+__global__ __launch_bounds__(kStencilThreads) void tile_kernel(const StencilArgs a) {
+  static_assert(EPI == EPI_AX || EPI == EPI_JAC, "tile shape: plain and Jacobi-fused apply");
+  if (a.stop && *a.stop) return;  // queued GMRES cycle already stopped
+  constexpr int TPB = kStencilThreads;
+  const int n = a.n;
+  const int tiles_x = a.tiles_x;
+  const int t = blockIdx.x;
+  const int tx = t % tiles_x, ty = t / tiles_x;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int i = tx * TPB + tid;
+  const bool act = i < n;
+  const int ic_ = min(i, n - 1);
+  const int rb = __builtin_amdgcn_readfirstlane(a.row_begin + ty * R);
+  const int re = __builtin_amdgcn_readfirstlane(min(rb + R, a.row_end));
+  auto rowp = [&](int r) -> const double2* {
+    return r < 0 ? a.halo_lo : (r >= a.nl ? a.halo_hi : a.u + (size_t)r * n);
+  };
+  // wave-edge lanes: lanes 0-31 load the wave's W halo column, 32-63 its E one (broadcast)
+  int iw = lane < kWave / 2 ? i - lane - 1 : i - lane + kWave;
+  const bool lw = lane == 0 && iw >= 0;
+  const bool le = lane == kWave - 1 && iw < n;
+  iw = min(max(iw, 0), n - 1);
+  const double2 z2 = make_double2(0.0, 0.0);
+  double2 U[R + 2], EG[R];
+  double IC[R];
+  #pragma unroll
+  for (int m = 0; m < R + 2; ++m) U[m] = ld2<NTU>(rowp(min(rb - 1 + m, re)) + ic_);
+  #pragma unroll
+  for (int m = 0; m < R; ++m) {
+    const int r = min(rb + m, re - 1);
+    IC[m] = CONSTC ? a.invc2_const : ld1<NT>(a.invc2 + (size_t)r * n + ic_);
+    EG[m] = rowp(r)[iw];
+  }
+  const cdouble_p tabj = (cdouble_p)(a.tab_j);
+  const double2 AW = a.tab_i[ic_], AE = a.tab_i[n + ic_], R1 = a.tab_i[2 * n + ic_];
+  double sin = 1.0;
+  if (a.in_scale) sin = *a.in_scale;
+  #pragma unroll
+  for (int m = 0; m < R; ++m) {
+    const int r = rb + m;
+    const int ru = __builtin_amdgcn_readfirstlane(min(r, re - 1));
+    const cdouble_p q = tabj + 8 * ru;
+    const double2 R2 = make_double2(q[0], q[1]), BS = make_double2(q[2], q[3]);
+    const double2 BN = make_double2(q[4], q[5]), OM = make_double2(q[6], q[7]);
+    const double2 uS = U[m], uC = U[m + 1], uN = U[m + 2];
+    const double2 uCm = act ? uC : z2;
+    const double2 sw = make_double2(__shfl_up(uCm.x, 1), __shfl_up(uCm.y, 1));
+    const double2 se = make_double2(__shfl_down(uCm.x, 1), __shfl_down(uCm.y, 1));
+    const double2 e = EG[m];
+    const double2 uW = lane == 0 ? (lw ? e : z2) : sw;
+    const double2 uE = lane == kWave - 1 ? (le ? e : z2) : se;
+    const double2 W = cmul(AW, R2);
+    const double2 E = cmul(AE, R2);
+    const double2 S = cmul(BS, R1);
+    const double2 N = cmul(BN, R1);
+    const double2 M = cscale(cmul(OM, R1), IC[m]);
+    const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
+    const double2 D = csub(M, sum4);
+    double2 Au = cmul(S, uS);
+    Au = cfma(W, uW, Au);
+    Au = cfma(D, uC, Au);
+    Au = cfma(E, uE, Au);
+    Au = cfma(N, uN, Au);
+    if (act && r < re) {
+      if constexpr (EPI == EPI_AX) store2(a.out0 + (size_t)r * n + ic_, cscale(Au, sin), NT);
+      else store2(a.out0 + (size_t)r * n + ic_, cscale(cdiv(Au, D), sin), NT);
+    }
+  }
+}
+
 // Pointwise operations needing only the diagonal D (or D_beta) of a point.
 template <int OP, bool CONSTC>
 __global__ __launch_bounds__(kStencilThreads) void point_kernel(const PointArgs a) {
@@ -498,6 +577,14 @@ constexpr int kSmallVariant = 18;    // 256-wide strips, NT u loads (grids below
 constexpr int kSmallCachedVariant = 6;  // 256-wide strips, cached u (plain apply below 2048)
 constexpr int kSolveVariant = 42;    // kDefaultVariant with NT u loads: solve epilogues, rows <= kLongRow
 constexpr int kLongRow = 4608;
+// Non-marching tile variants (plain 5-point apply): kTileVariant + 0/16 (NT u loads: + 16) +
+// R rows per tile.
+constexpr int kTileVariant = 96;
+constexpr int kTileDefault = kTileVariant + 4;  // 4-row tiles, cached u, NT 1/c^2 and stores
+constexpr bool tile_variant_known(int v) {
+  const int w = v - kTileVariant, R = w % 16;
+  return w >= 0 && w < 64 && R >= 2 && R <= 8 && R != 7;
+}
 // The 9-point operator instantiates the four LDS-exchange shapes below and takes the 5-point
 // defaults: in its separable form (101-109 VGPRs, 4 waves per SIMD) it runs at the 5-point
 // kernel's speed (4096^2 cold: 119.3 vs 119.6 us, profiles/r01v_tune_stencil9.log).
@@ -594,11 +681,19 @@ int stencil_resolve_variant(int epi, int requested, int n) {
   //   Below n = 2048 a grid's vectors fit the 256 MiB Infinity Cache: the plain apply then
   // loads u through the cache as well (1024^2: 8.6 vs 9.6 us with NT u loads,
   // profiles/r01w_tune_const_1024.log).
+  //   A standalone plain apply (requested == -1) on n >= 2048 takes the non-marching tile
+  // shape (tile_kernel, 4-row tiles): on cold inputs 5.84 vs 5.54 TB/s at 4096^2 and 5.8-6.0
+  // vs 5.2-5.7 TB/s at 8192 .. 16384 (profiles/r01y_tune_tile*.log).  Inside a GMRES cycle
+  // (requested == kVariantInSolve) the marching shape is kept: there the tile shape measured
+  // 3-4 % slower (profiles/r01y_tune_tile_gmres.log).
   int autov = kDefaultVariant;
   if (n < 2048) autov = epi == EPI_AX ? kSmallCachedVariant : kSmallVariant;
   else if (epi != EPI_AX && n <= kLongRow) autov = kSolveVariant;
+  else if (epi == EPI_AX && requested != kVariantInSolve) autov = kTileDefault;
   if (requested < 0) return autov;
   if (epi == EPI_AX) return stencil_variant_valid(requested) ? requested : autov;
+  if (epi == EPI_JAC && requested >= kTileVariant && stencil_variant_valid(requested))
+    return requested;  // the tile shape has the Jacobi-fused apply too
   return (requested == kSmallVariant || requested == kDefaultVariant || requested == kSolveVariant)
              ? requested
              : autov;
@@ -619,7 +714,10 @@ int stencil_grid_blocks(int n, int rows, int rows_per_block, int row_step) {
 
 
 int stencil_default_variant() { return kDefaultVariant; }
-bool stencil_variant_valid(int v) { return (v >= 0 && v <= 27) || (v >= 30 && v <= 33) || (v >= 42 && v <= 45); }
+bool stencil_variant_valid(int v) {
+  return (v >= 0 && v <= 27) || (v >= 30 && v <= 33) || (v >= 42 && v <= 45) ||
+         (v >= kTileVariant && v < kTileVariant + 64 && tile_variant_known(v));
+}
 
 void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_out[1],
                     hipStream_t stream, int variant) {
@@ -627,7 +725,48 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_
   const int rows = a.row_end - a.row_begin;
   int v = stencil_resolve_variant(epi, variant, a.n);
   // the 9-point operator has a subset of the shapes (launch_stencil_t): others take the default
-  if (a.tab_r2x && !stencil9_variant_valid(v)) v = stencil_resolve_variant(epi, -1, a.n);
+  if (a.tab_r2x && !stencil9_variant_valid(v)) {
+    v = stencil_resolve_variant(epi, -1, a.n);
+    if (!stencil9_variant_valid(v))  // (the non-marching tile default is 5-point only)
+      v = a.n < 2048 ? (epi == EPI_AX ? kSmallCachedVariant : kSmallVariant)
+                     : (epi != EPI_AX && a.n <= kLongRow ? kSolveVariant : kDefaultVariant);
+  }
+  if (v >= kTileVariant && a.row_step > 0)  // spaced bands (halo rows): marching shape
+    v = stencil_resolve_variant(epi, kVariantInSolve, a.n);
+  if (v >= kTileVariant) {  // non-marching tiles (plain / Jacobi 5-point apply, tile_kernel)
+    const int w = v - kTileVariant, R = w % 16;
+    const bool ntu = (w / 16) % 2 == 1, nt = w < 32;
+    a.tiles_x = (a.n + kStencilThreads - 1) / kStencilThreads;
+    const int tiles = a.tiles_x * ((rows + R - 1) / R);
+    nblocks_out[0] = 0;
+    auto go = [&](auto ke, auto kr) {
+      constexpr int E = decltype(ke)::value;
+      constexpr int RR = decltype(kr)::value;
+      const dim3 g(tiles), b(kStencilThreads);
+      if (const_c) {
+        if (!nt) hipLaunchKernelGGL((tile_kernel<E, true, RR, false, false>), g, b, 0, stream, a);
+        else if (ntu) hipLaunchKernelGGL((tile_kernel<E, true, RR, true, true>), g, b, 0, stream, a);
+        else hipLaunchKernelGGL((tile_kernel<E, true, RR, true, false>), g, b, 0, stream, a);
+      } else {
+        if (!nt) hipLaunchKernelGGL((tile_kernel<E, false, RR, false, false>), g, b, 0, stream, a);
+        else if (ntu) hipLaunchKernelGGL((tile_kernel<E, false, RR, true, true>), g, b, 0, stream, a);
+        else hipLaunchKernelGGL((tile_kernel<E, false, RR, true, false>), g, b, 0, stream, a);
+      }
+    };
+    auto go_r = [&](auto ke) {
+      switch (R) {
+        case 2: go(ke, std::integral_constant<int, 2>{}); break;
+        case 3: go(ke, std::integral_constant<int, 3>{}); break;
+        case 4: go(ke, std::integral_constant<int, 4>{}); break;
+        case 5: go(ke, std::integral_constant<int, 5>{}); break;
+        case 6: go(ke, std::integral_constant<int, 6>{}); break;
+        default: go(ke, std::integral_constant<int, 8>{}); break;
+      }
+    };
+    if (epi == EPI_JAC) go_r(std::integral_constant<int, EPI_JAC>{});
+    else go_r(std::integral_constant<int, EPI_AX>{});
+    return;
+  }
   const int tpb = v >= 24 ? 512 : 256;
   a.tiles_x = (a.n + tpb - 1) / tpb;
   // bands start every row_step rows (spaced out only by the halo-row launch of a rank inside

@@ -18,7 +18,9 @@ from oracle import helmholtz_oracle as O
 pytestmark = pytest.mark.gpu
 
 # LDS and wave-shuffle exchange; cached / NT u loads; 256- and 512-wide strips; prefetch 1 and 2
-APPLY_VARIANTS = [6, 8, 18, 24, 30, 32, 42, 44, 45]
+APPLY_VARIANTS = [6, 8, 18, 24, 30, 32, 42, 44, 45,
+                  # non-marching tiles (tile_kernel): 2 .. 8 rows, cached / NT u, NT / plain stores
+                  98, 99, 100, 101, 102, 104, 116, 132]
 SOLVE_VARIANTS = [18, 30, 42]  # the shapes every epilogue is instantiated for
 
 
@@ -161,3 +163,44 @@ def test_fused_shifted_laplace_matches_two_launch_path(ctx, n, kind, rpb, stenci
     assert info == infor and len(hist) == len(histr)
     assert np.max(np.abs(hist - histr) / histr) < 1e-6
     assert relerr(x, xr) < 1e-6
+
+
+@pytest.mark.parametrize("slabs", [1, 3])
+def test_default_tile_apply_on_slabs(slabs):
+    """n >= 2048: a standalone apply takes the non-marching tile shape by default; on virtual
+    slabs (in-place neighbour rows) it is bit-identical to the single domain and the oracle."""
+    n = 2100
+    om, h, eta = O.problem_params(n, 12, 30.0, 2.0)
+    cm = medium("c1", n)
+    x = rand_complex(n * n, 3)
+    c1 = H.Context(device=0)
+    y1 = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, context=c1) @ x
+    assert relerr(y1, O.build_A_matrix(12, 81.0, eta, om, h, n, cm) @ x) < 1e-12
+    cs = H.Context(device=0, virtual_slabs=slabs)
+    A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, context=cs)
+    np.testing.assert_array_equal(A @ x, y1)
+    A.tune(30)  # the marching shape: the same numbers
+    np.testing.assert_array_equal(A @ x, y1)
+
+
+@pytest.mark.parametrize("M_kind", ["none", "jacobi"])
+def test_gmres_with_tile_shape_forced(ctx, M_kind):
+    """the tile shape forced inside GMRES (plain and Jacobi-fused applies) gives the marching
+    shape's histories and fields bit for bit"""
+    n = 2100
+    om, h, eta = O.problem_params(n, 12, 30.0, 2.0)
+    cm = medium("c2", n)
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, context=ctx)
+    M = None if M_kind == "none" else "jacobi"
+    out = []
+    for v in (-1, 100, 116):
+        A.tune(v, 0, 0)
+        x, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=25, M=M,
+                                callback=lambda r: None, callback_type="legacy",
+                                return_history=True)
+        out.append((x, hist))
+    A.tune(-1, 0, 0)
+    for x, hist in out[1:]:
+        np.testing.assert_array_equal(hist, out[0][1])
+        np.testing.assert_array_equal(x, out[0][0])

@@ -11,7 +11,7 @@ from collections import defaultdict
 N = 4096 * 4096
 ALGO = {  # kernel-name fragment -> (read bytes, write bytes) per launch at 4096^2
     "p0(": (24 * N, 16 * N), "p1(": (24 * N, 16 * N), "p3(": (16 * N, 16 * N),
-    "p4(": (24 * N, 0), "stencil_kernel<0": (24 * N, 16 * N),
+    "p4(": (24 * N, 0), "stencil_kernel<0": (24 * N, 16 * N), "tile_kernel<0": (24 * N, 16 * N),
 }
 
 
