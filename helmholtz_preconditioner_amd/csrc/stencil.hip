@@ -448,8 +448,8 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
 // load of its R + 2 input rows, R 1/c^2 rows and R broadcast edge values is issued up front --
 // and exchanges W/E neighbours by wave shuffles (no LDS, no barrier).  Blocks run in plain
 // order, so the concurrently resident tiles cover one narrow address window of the grid (the
-// flat stream's access pattern), and vertically adjacent tiles (tiles_x blocks apart, a
-// multiple of 8) share an XCD's L2 for their halo rows.  Same per-point arithmetic as
+// flat stream's access pattern); the two halo rows a tile shares with each vertical
+// neighbour come mostly from L2 / the Infinity Cache.  Same per-point arithmetic as
 // stencil_tile: bit-identical results.
 template <int EPI, bool CONSTC, int R, bool NT, bool NTU>
 __global__ __launch_bounds__(kStencilThreads) void tile_kernel(const StencilArgs a) {
@@ -736,6 +736,8 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_
   if (v >= kTileVariant) {  // non-marching tiles (plain / Jacobi 5-point apply, tile_kernel)
     const int w = v - kTileVariant, R = w % 16;
     const bool ntu = (w / 16) % 2 == 1, nt = w < 32;
+    // (padding tiles_x to a multiple of 8, which would put vertically adjacent tiles on one
+    // XCD, measured 3-7 % SLOWER at n = 5792 and 11584: profiles/r01y_tune_tile_pad.log)
     a.tiles_x = (a.n + kStencilThreads - 1) / kStencilThreads;
     const int tiles = a.tiles_x * ((rows + R - 1) / R);
     nblocks_out[0] = 0;
