@@ -24,6 +24,7 @@ def main():
     p.add_argument("--n", type=int, default=150)
     p.add_argument("--slabs", type=int, default=1)
     p.add_argument("--stencil", type=int, default=5)
+    p.add_argument("--apply-only", action="store_true")
     a = p.parse_args()
     ctx = H.Context(device=0, rank=a.rank, world=a.world, nccl_id=bytes.fromhex(a.id),
                     virtual_slabs=a.slabs, transport="shm")
@@ -37,7 +38,7 @@ def main():
     y = A @ xg[j0:j1].ravel()
     f = H.init_f1_mat(.5, .125, om, n)[j0:j1].ravel()
     out = dict(j0=j0, j1=j1, y=y)
-    for name, M in (("none", None), ("jacobi", "jacobi"),
+    for name, M in () if a.apply_only else (("none", None), ("jacobi", "jacobi"),
                     ("sl", H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7))):
         x, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=50, M=M,
                                 callback=lambda r: None, callback_type="legacy",

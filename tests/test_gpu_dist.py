@@ -105,3 +105,35 @@ def test_bench_two_ranks_rehearsal(tmp_path):
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["config"]["n"] == 768 and res["value"] > 0
     assert res["gmres"]["iterations"] == 6
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_multiprocess_apply_large_grid(tmp_path, world):
+    """n = 2100: every rank's interior rows take the non-marching tile kernel (the default
+    standalone apply from n = 2048), the cross-rank halo rows the marching one; the slabs
+    together are bit-identical to the single domain."""
+    n = 2100
+    ctx = H.Context(device=0)
+    om, h, eta = H.problem_params(n, 12, 6.0, 2.0)
+    A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.init_c1_mat(.5, .5, n), context=ctx)
+    rng = np.random.default_rng(5)
+    yref = A @ (rng.standard_normal(n * n) + 1j * rng.standard_normal(n * n))
+    tok = os.urandom(128).hex()
+    procs = []
+    for r in range(world):
+        out = tmp_path / f"r{r}.npz"
+        procs.append((subprocess.Popen([sys.executable, WORKER, "--rank", str(r), "--world",
+                                        str(world), "--id", tok, "--out", str(out), "--n", str(n),
+                                        "--apply-only"],
+                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT), out))
+    for p, _ in procs:
+        try:
+            p.wait(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q, _ in procs:
+                q.kill()
+            raise
+    for p, _ in procs:
+        assert p.returncode == 0, p.stdout.read().decode()[-3000:]
+    y = np.concatenate([np.load(o)["y"] for _, o in procs])
+    np.testing.assert_array_equal(y, yref)
