@@ -522,6 +522,113 @@ __global__ __launch_bounds__(kStencilThreads) void tile_kernel(const StencilArgs
   }
 }
 
+// The tile shape for the 9-point operator (stencil_tile's separable S9 form, same association,
+// bit-identical): every row of the tile and its two halo rows gets its x second difference X
+// and W+E sum H from wave shuffles (+ the broadcast edge values at the wave edges); the y
+// second difference Y of each output row is exchanged by shuffles too, the wave-edge lanes
+// computing Y of the halo column from the edge values of the three rows.
+template <int EPI, bool CONSTC, int R, bool NT, bool NTU>
+__global__ __launch_bounds__(kStencilThreads) void tile9_kernel(const StencilArgs a) {
+  static_assert(EPI == EPI_AX || EPI == EPI_JAC, "tile shape: plain and Jacobi-fused apply");
+  if (a.stop && *a.stop) return;
+  constexpr int TPB = kStencilThreads;
+  const int n = a.n;
+  const int tiles_x = a.tiles_x;
+  const int t = blockIdx.x;
+  const int tx = t % tiles_x, ty = t / tiles_x;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int i = tx * TPB + tid;
+  const bool act = i < n;
+  const int ic_ = min(i, n - 1);
+  const int rb = __builtin_amdgcn_readfirstlane(a.row_begin + ty * R);
+  const int re = __builtin_amdgcn_readfirstlane(min(rb + R, a.row_end));
+  auto rowp = [&](int r) -> const double2* {
+    return r < 0 ? a.halo_lo : (r >= a.nl ? a.halo_hi : a.u + (size_t)r * n);
+  };
+  int iw = lane < kWave / 2 ? i - lane - 1 : i - lane + kWave;
+  const bool lw = lane == 0 && iw >= 0;
+  const bool le = lane == kWave - 1 && iw < n;
+  iw = min(max(iw, 0), n - 1);
+  const double2 z2 = make_double2(0.0, 0.0);
+  double2 U[R + 2], EG[R + 2];
+  double IC[R];
+  #pragma unroll
+  for (int m = 0; m < R + 2; ++m) {
+    const double2* rp = rowp(min(rb - 1 + m, re));
+    U[m] = ld2<NTU>(rp + ic_);
+    EG[m] = rp[iw];
+  }
+  #pragma unroll
+  for (int m = 0; m < R; ++m) {
+    const int r = min(rb + m, re - 1);
+    IC[m] = CONSTC ? a.invc2_const : ld1<NT>(a.invc2 + (size_t)r * n + ic_);
+  }
+  const cdouble_p tabj = (cdouble_p)(a.tab_j);
+  const cdouble_p tabx = (cdouble_p)(a.tab_r2x);
+  const double2 AW = a.tab_i[ic_], AE = a.tab_i[n + ic_], R1 = a.tab_i[2 * n + ic_];
+  const double2 R1e = a.tab_i[2 * n + iw];  // the wave-edge lanes' halo column
+  const Stencil9W w = a.w9;
+  double sin = 1.0;
+  if (a.in_scale) sin = *a.in_scale;
+  auto shfl_up = [&](double2 v) { return make_double2(__shfl_up(v.x, 1), __shfl_up(v.y, 1)); };
+  auto shfl_dn = [&](double2 v) { return make_double2(__shfl_down(v.x, 1), __shfl_down(v.y, 1)); };
+  // X and H of tile row m (0 .. R+1 <-> rows rb-1 .. rb+R)
+  auto xh = [&](int m, double2& X, double2& Hs) {
+    const int ru = __builtin_amdgcn_readfirstlane(min(rb - 1 + m, re) + 1);  // tab_r2x entry
+    const double2 R2 = make_double2(tabx[2 * ru], tabx[2 * ru + 1]);
+    const double2 uC = U[m];
+    const double2 uCm = act ? uC : z2;
+    const double2 sw = shfl_up(uCm), se = shfl_dn(uCm);
+    const double2 e = EG[m];
+    const double2 uW = lane == 0 ? (lw ? e : z2) : sw;
+    const double2 uE = lane == kWave - 1 ? (le ? e : z2) : se;
+    X = cmul(R2, cfma(AE, csub(uE, uC), cmul(AW, csub(uW, uC))));
+    Hs = cadd(uW, uE);
+  };
+  double2 Xm, Xc, Hm, Hc;
+  xh(0, Xm, Hm);
+  xh(1, Xc, Hc);
+  #pragma unroll
+  for (int m = 1; m <= R; ++m) {
+    const int r = rb + m - 1;
+    const int ru = __builtin_amdgcn_readfirstlane(min(r, re - 1));
+    const cdouble_p q = tabj + 8 * ru;
+    const double2 R2 = make_double2(q[0], q[1]), BS = make_double2(q[2], q[3]);
+    const double2 BN = make_double2(q[4], q[5]), OM = make_double2(q[6], q[7]);
+    double2 Xp, Hp;
+    xh(m + 1, Xp, Hp);
+    const double2 uS = U[m - 1], uC = U[m], uN = U[m + 1];
+    const double2 Yc = cmul(R1, cfma(BN, csub(uN, uC), cmul(BS, csub(uS, uC))));
+    const double2 Ycm = act ? Yc : z2;
+    // Y of the wave's halo column from the edge values of rows r-1, r, r+1 (zero off the grid)
+    const double2 eS = EG[m - 1], eC = EG[m], eN = EG[m + 1];
+    const double2 Yh = cmul(R1e, cfma(BN, csub(eN, eC), cmul(BS, csub(eS, eC))));
+    const double2 sw = shfl_up(Ycm), se = shfl_dn(Ycm);
+    const double2 Yw = lane == 0 ? (lw ? Yh : z2) : sw;
+    const double2 Ye = lane == kWave - 1 ? (le ? Yh : z2) : se;
+    const double2 W = cmul(AW, R2);
+    const double2 E = cmul(AE, R2);
+    const double2 S = cmul(BS, R1);
+    const double2 N = cmul(BN, R1);
+    const double2 M = cscale(cmul(OM, R1), IC[m - 1]);
+    const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
+    const double2 lap = cadd(Xc, Yc);
+    const double2 avg = cadd(cadd(Xm, Xp), cadd(Yw, Ye));
+    const double2 edges = cadd(Hc, cadd(uS, uN));
+    const double2 corners = cadd(Hm, Hp);
+    const double2 mix = cadd(cadd(cscale(uC, w.c), cscale(edges, w.d)), cscale(corners, w.e));
+    const double2 Au = cfma(M, mix, cadd(cscale(lap, w.alpha), cscale(avg, w.g)));
+    if (act && r < re) {
+      if constexpr (EPI == EPI_AX) store2(a.out0 + (size_t)r * n + ic_, cscale(Au, sin), NT);
+      else store2(a.out0 + (size_t)r * n + ic_, cscale(cdiv(Au, stencil9_diag(M, sum4, w)), sin), NT);
+    }
+    Xm = Xc;
+    Xc = Xp;
+    Hm = Hc;
+    Hc = Hp;
+  }
+}
+
 // Pointwise operations needing only the diagonal D (or D_beta) of a point.
 template <int OP, bool CONSTC>
 __global__ __launch_bounds__(kStencilThreads) void point_kernel(const PointArgs a) {
@@ -590,7 +697,8 @@ constexpr bool tile_variant_known(int v) {
 // kernel's speed (4096^2 cold: 119.3 vs 119.6 us, profiles/r01v_tune_stencil9.log).
 constexpr int kStencil9Variant = kSmallVariant;
 bool stencil9_variant_valid(int v) {
-  return v == 6 || v == kSmallVariant || v == kDefaultVariant || v == kSolveVariant;
+  return v == 6 || v == kSmallVariant || v == kDefaultVariant || v == kSolveVariant ||
+         (v >= kTileVariant && tile_variant_known(v));
 }
 
 // Variant table: V = XM + 3 (PF - 1) + 6 NT + 12 NTU + 24 (512-wide strips)  (0..47).
@@ -725,6 +833,10 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_
   const int rows = a.row_end - a.row_begin;
   int v = stencil_resolve_variant(epi, variant, a.n);
   // the 9-point operator has a subset of the shapes (launch_stencil_t): others take the default
+  // 9-point standalone apply: 5-row tiles on long rows only (4096^2: tile 127.7 vs marching
+  // 121.8 us; 8192^2: 479.9 vs 507.6 us; profiles/r01y_tune_tile9.log)
+  if (a.tab_r2x && variant == -1 && v >= kTileVariant)
+    v = a.n > kLongRow ? kTileVariant + 5 : kDefaultVariant;
   if (a.tab_r2x && !stencil9_variant_valid(v)) {
     v = stencil_resolve_variant(epi, -1, a.n);
     if (!stencil9_variant_valid(v))  // (the non-marching tile default is 5-point only)
@@ -745,7 +857,17 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_
       constexpr int E = decltype(ke)::value;
       constexpr int RR = decltype(kr)::value;
       const dim3 g(tiles), b(kStencilThreads);
-      if (const_c) {
+      if (a.tab_r2x) {  // 9-point operator
+        if (const_c) {
+          if (!nt) hipLaunchKernelGGL((tile9_kernel<E, true, RR, false, false>), g, b, 0, stream, a);
+          else if (ntu) hipLaunchKernelGGL((tile9_kernel<E, true, RR, true, true>), g, b, 0, stream, a);
+          else hipLaunchKernelGGL((tile9_kernel<E, true, RR, true, false>), g, b, 0, stream, a);
+        } else {
+          if (!nt) hipLaunchKernelGGL((tile9_kernel<E, false, RR, false, false>), g, b, 0, stream, a);
+          else if (ntu) hipLaunchKernelGGL((tile9_kernel<E, false, RR, true, true>), g, b, 0, stream, a);
+          else hipLaunchKernelGGL((tile9_kernel<E, false, RR, true, false>), g, b, 0, stream, a);
+        }
+      } else if (const_c) {
         if (!nt) hipLaunchKernelGGL((tile_kernel<E, true, RR, false, false>), g, b, 0, stream, a);
         else if (ntu) hipLaunchKernelGGL((tile_kernel<E, true, RR, true, true>), g, b, 0, stream, a);
         else hipLaunchKernelGGL((tile_kernel<E, true, RR, true, false>), g, b, 0, stream, a);

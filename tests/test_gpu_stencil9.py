@@ -201,3 +201,23 @@ def test_sweeping_refuses_9pt(ctx):
     A5.set_preconditioner(H._ffi.HH_PREC_SWEEP)
     with pytest.raises(H.HHError, match="5-point"):
         A5.set_stencil(9)
+
+
+@pytest.mark.parametrize("n,kind", [(700, "c1"), (2100, "c2")])
+def test_all_shapes_bit_identical(ctx, n, kind):
+    """marching (256/512-wide, cached/NT) and tile (2 .. 8 rows) shapes of the 9-point apply and
+    of its Jacobi-fused apply: identical numbers, and the oracle's"""
+    A, R = _op(n, kind, ctx)
+    x = rand_complex(n * n, 6)
+    yref = R @ x
+    first = firstj = None
+    for v in (6, 18, 30, 42, 98, 99, 100, 101, 102, 104, 116, 132):
+        A.tune(v, 0, 0)
+        y = A @ x
+        yj = A._apply_host(x, H._ffi.HH_APPLY_JACOBI_A)
+        assert relerr(y, yref) < TOL, v
+        first = y if first is None else first
+        firstj = yj if firstj is None else firstj
+        np.testing.assert_array_equal(y, first)
+        np.testing.assert_array_equal(yj, firstj)
+    A.tune(-1, 0, 0)

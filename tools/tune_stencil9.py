@@ -18,6 +18,7 @@ p.add_argument("--rounds", type=int, default=2)
 p.add_argument("--iters", type=int, default=50)
 p.add_argument("--rpbs", default="16,32,64")
 p.add_argument("--medium", default="marmousi")
+p.add_argument("--variants", default="")
 a = p.parse_args()
 n = a.n
 om, h, eta = H.problem_params(n, 12, 100.0, 2.0)
@@ -33,7 +34,7 @@ for k, v in enumerate(xs):
     x5[k].fill_hash(7 + k)
 bpp = A9.bytes_per_point
 ref = None
-shapes = [(v, r) for v in (6, 18, 30, 42) for r in [int(t) for t in a.rpbs.split(",")]]
+shapes = [(v, r) for v in ([int(t) for t in a.variants.split(",")] if a.variants else (6, 18, 30, 42)) for r in [int(t) for t in a.rpbs.split(",")]]
 for v, r in shapes:
     A9.tune(v, r)
     A9.apply_device(xs[0], ys[0])
