@@ -179,7 +179,23 @@ def cpu_baseline(args, n, omega, h, eta, c_mat):
         out["gmres_iters_per_s"] = round(args.cpu_gmres_iters / t_g, 4)
         out["gmres_sample"] = (f"{args.cpu_gmres_iters} scipy gmres inner iterations "
                                f"({args.precond} preconditioner), OpenBLAS threads={thr}")
+    out["host"] = host_description()
     return out
+
+
+def host_description():
+    """CPU model and logical CPUs of the host the CPU baseline ran on."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return f"{model}, {os.cpu_count()} logical CPUs (process affinity: " \
+           f"{len(os.sched_getaffinity(0))})"
 
 
 def main():
