@@ -1,4 +1,4 @@
-// Matrix-free complex 5-point PML Helmholtz stencil for gfx950 (MI355X).
+// Matrix-free complex 5-point (and 9-point) PML Helmholtz stencil for gfx950 (MI355X).
 //
 // Replaces the reference's assembled CSR operator and its scipy csr_matvec:
 //   coefficients  get_A_diag_block_coeffs  code.py:70-115 (W=c1, E=c2, S=c3, N=c4, D=c5)
@@ -22,14 +22,20 @@
 //   W : alpha W - g (Sm + Nm) + d M   C: c M - alpha (W + E + S + N)   E: alpha E - g (Sp + Np) + d M
 //   NW: g (Wp + Nm) + e M   N: alpha N - g (Wp + Ep) + d M   NE: g (Ep + Np) + e M
 // with g = (1 - alpha) / 2, M = OM R1 / c^2 at the centre, Wm/Em/Wp/Ep = AW/AE x R2 of rows
-// j-1 / j+1 and Sm/Nm/Sp/Np = BS/BN x R1 of columns i-1 / i+1.  Same HBM bytes as the 5-point
-// apply (40 B/pt): the diagonal neighbours come from a 4-row LDS ring.
+// j-1 / j+1 and Sm/Nm/Sp/Np = BS/BN x R1 of columns i-1 / i+1 (hh_stencil9.hpp).  The kernels
+// evaluate it in a separable form (see the S9 step of stencil_tile).  Same HBM bytes as the
+// 5-point apply (40 B/pt).
 //
-// Kernel shape: a block owns a 256-wide strip of i and marches a band of rows in j with a
-// three-row register window (u_{j-1}, u_j, u_{j+1}) plus a one-row prefetch, so every u is
-// read from HBM once; the W/E neighbours are exchanged through a double-buffered LDS row
-// with a one-point halo at each side (one barrier per row).  Tiles are dealt to XCDs in
-// contiguous bands so the band-edge halo rows of vertically adjacent tiles hit the same L2.
+// Two kernel shapes, bit-identical (the same per-point arithmetic):
+// * marching (stencil_tile): a block owns a 256- or 512-wide strip of i and marches a band of
+//   rows in j with a three-row register window (u_{j-1}, u_j, u_{j+1}) plus a one-row
+//   prefetch, so every u is read from HBM once; W/E neighbours go through a double-buffered
+//   LDS row (a 4-row ring for 9 points) with a one-point halo at each side (one barrier per
+//   row).  Tiles are dealt to XCDs in contiguous bands.  Every epilogue (Jacobi, residual,
+//   shifted-Laplace sweeps, norms); the shape used inside GMRES.
+// * non-marching tiles (tile_kernel / tile9_kernel): R rows x 256 columns per block, every
+//   load issued up front, wave-shuffle exchange, blocks in plain order -- the default
+//   standalone apply on large grids (see stencil_resolve_variant).
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
 #include "hh_stencil9.hpp"
