@@ -29,8 +29,10 @@ enum Epi : int {
 
 // W/E neighbour exchange of the stencil kernel (see stencil.hip).
 enum XMode : int { XM_LDS = 0, XM_DIRECT = 1, XM_SHFL = 2 };
-// Tuning variant = XM + 3 * (PF - 1) + 6 * NT + 12 * NTU + 24 * (512-wide strips)  (0..47;
-// the 512-wide set is instantiated for 24..27 and 30..33).
+// Tuning variant of the marching kernel = XM + 3 * (PF - 1) + 6 * NT + 12 * NTU + 24 * (512-wide
+// strips)  (0..47; the 512-wide set is instantiated for 24..27 and 30..33).  Variants 96 + R
+// (+ 16: NT u loads, + 32: cached 1/c^2 and plain stores) select the non-marching R-row tile
+// kernel (plain and Jacobi-fused apply; stencil.hip, tile_kernel / tile9_kernel).
 constexpr int kNumVariants = 48;
 
 // Pointwise (no-neighbour) operations that need only the diagonal.

@@ -193,9 +193,11 @@ int hh_gmres(hh_op* op, const hh_vec* b, hh_vec* x, double rtol, double atol,
 typedef void (*hh_gmres_cycle_callback)(void* user, long cycle);
 int hh_op_set_cycle_callback(hh_op* op, hh_gmres_cycle_callback cb, void* user);
 
-/* Performance tuning of the stencil kernel used by HH_APPLY_A: variant in [0, 24)
- * selects the W/E exchange (LDS row / direct cached loads / wave shuffle), prefetch
- * depth and load/store cache policy (-1 = built-in default); rows_per_block overrides
+/* Performance tuning of the stencil kernel used by HH_APPLY_A: variant in [0, 48) selects the
+ * marching kernel's W/E exchange (LDS row / direct cached loads / wave shuffle), prefetch depth,
+ * load/store cache policy and strip width, 96 + R (R = 2 .. 8 rows, + 16 / + 32 cache-policy
+ * bits) the non-marching tile kernel (-1 = built-in default: tiles for standalone applies on
+ * n >= 2048, marching inside hh_gmres and below); rows_per_block overrides
  * the band height one workgroup marches (0 = automatic); grid_blocks > 0 runs a
  * persistent grid of that many workgroups (0 = one per tile).  Results are identical
  * for every setting; only speed changes. */
