@@ -687,7 +687,9 @@ __global__ __launch_bounds__(kStencilThreads) void point_kernel(const PointArgs 
 // DESIGN.md "stencil variants"); the benchmark kernel (EPI_AX) can run all 12 variants.
 constexpr int kDefaultVariant = 30;  // XM_LDS, PF 1, NT stores + NT 1/c^2 loads, cached u, 512-wide
 constexpr int kSmallVariant = 18;    // 256-wide strips, NT u loads (grids below 2048)
-constexpr int kSmallCachedVariant = 6;  // 256-wide strips, cached u (plain apply below 2048)
+constexpr int kSmallCachedVariant = 8;  // 256-wide strips, wave-shuffle exchange, cached u
+                                        // (plain apply below 2048: 8.2 vs 8.5 us for the LDS
+                                        // exchange at 1024^2, profiles/r01w_tune_const_1024.log)
 constexpr int kSolveVariant = 42;    // kDefaultVariant with NT u loads: solve epilogues, rows <= kLongRow
 constexpr int kLongRow = 4608;
 // Non-marching tile variants (plain 5-point apply): kTileVariant + 0/16 (NT u loads: + 16) +
@@ -846,7 +848,7 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_
   if (a.tab_r2x && !stencil9_variant_valid(v)) {
     v = stencil_resolve_variant(epi, -1, a.n);
     if (!stencil9_variant_valid(v))  // (the non-marching tile default is 5-point only)
-      v = a.n < 2048 ? (epi == EPI_AX ? kSmallCachedVariant : kSmallVariant)
+      v = a.n < 2048 ? (epi == EPI_AX ? 6 : kSmallVariant)  // 6: LDS exchange, cached u
                      : (epi != EPI_AX && a.n <= kLongRow ? kSolveVariant : kDefaultVariant);
   }
   if (v >= kTileVariant && a.row_step > 0)  // spaced bands (halo rows): marching shape
