@@ -194,7 +194,6 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
                   hi_x ? in + sl.off + (size_t)(sl.nl - 1) * n : nullptr,
                   hi_x ? sl.halo_hi_buf : nullptr, 2 * sizeof(double) * (size_t)n, c->stream,
                   c->cstream, c->ev_in);
-    HIPC(hipEventRecord(c->ev_halo, c->cstream));
   }
 
   auto make_args = [&](int si) {
@@ -226,7 +225,8 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
   };
 
   int nparts = 0;
-  auto launch_rows = [&](int si, int r0, int r1, int rpb, int step = 0) {
+  auto launch_rows = [&](int si, int r0, int r1, int rpb, int step = 0,
+                         hipStream_t st = nullptr) {
     if (r1 <= r0) return;
     StencilArgs a = make_args(si);
     a.row_begin = r0;
@@ -240,7 +240,7 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
             "partials workspace too small for the stencil launch");
     int written = 0;
     const int variant = (op->variant < 0 && op->stop_flag) ? kVariantInSolve : op->variant;
-    launch_stencil(epi, op->const_c, a, &written, c->stream, variant);
+    launch_stencil(epi, op->const_c, a, &written, st ? st : c->stream, variant);
     nparts += written;
   };
 
@@ -256,17 +256,23 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
     first = false;
   }
   if (lo_x || hi_x) {
-    HIPC(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+    // The boundary rows run on the halo stream, right behind the exchange (which it ordered
+    // after everything the compute stream had queued), concurrently with the interior launch;
+    // they read the same input and write disjoint rows and partial slots.  The compute stream
+    // then waits for them.
+    hipStream_t hs = c->cstream;
     const Slab& s0 = op->slabs[0];
     const Slab& sl = op->slabs[S - 1];
     if (S == 1 && s0.nl == 1) {
-      launch_rows(0, 0, 1, 1);
+      launch_rows(0, 0, 1, 1, 0, hs);
     } else if (S == 1 && lo_x && hi_x) {
-      launch_rows(0, 0, s0.nl, 1, s0.nl - 1);  // rows 0 and nl-1: one launch of two bands
+      launch_rows(0, 0, s0.nl, 1, s0.nl - 1, hs);  // rows 0 and nl-1: one launch of two bands
     } else {
-      if (lo_x) launch_rows(0, 0, 1, 1);
-      if (hi_x) launch_rows(S - 1, sl.nl - 1, sl.nl, 1);
+      if (lo_x) launch_rows(0, 0, 1, 1, 0, hs);
+      if (hi_x) launch_rows(S - 1, sl.nl - 1, sl.nl, 1, 0, hs);
     }
+    HIPC(hipEventRecord(c->ev_halo, hs));
+    HIPC(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
   }
   HIPC(hipGetLastError());
   op->stats.spmv_count++;
