@@ -216,7 +216,9 @@ def main():
     omega, h, eta = H.problem_params(n, args.b, args.wave_num, args.alpha)
     j0, j1 = dist.slab_bounds(n, world, rank)
     t0 = time.perf_counter()
-    c_mat = make_medium(args.medium, n, (j0, j1))
+    # this rank's layers plus two on each side (the fused shifted-Laplace M A evaluates the
+    # first sweep on the neighbouring ranks' boundary layers)
+    c_mat = make_medium(args.medium, n, (j0 - 2, j1 + 2))
     A = H.build_A_matrix(args.b, args.C, eta, omega, h, n, c_mat, context=ctx,
                          stencil=args.stencil)
     t_init = time.perf_counter() - t0
@@ -319,7 +321,7 @@ def main():
         # stencil + sweep launches, 16 + 56 B per further sweep.
         js = [i % args.restart for i in range(its)]
         N = float(n) * n
-        fused = args.sl_sweeps == 2 and world == 1 and args.virtual_slabs == 1
+        fused = args.sl_sweeps == 2  # one launch per slab (plus the halo rows) on any layout
         sl_extra = 0 if fused else bpp + 16 + 56 * (args.sl_sweeps - 1)
         pre = {"sl": sl_extra, "jacobi": 0, "none": 0}[args.precond]
         gbytes = sum((bpp + pre) * N + 16 * (j + 2) * N + 16 * (j + 3) * N for j in js)

@@ -76,6 +76,11 @@ struct StencilArgs {
   // rows -1 .. nl ([nl + 2], entry r + 1 for row r) and the stencil weights (see stencil.hip)
   const double2* tab_r2x;
   Stencil9W w9;
+  // fused SL kernel only (sl_fused.hip): halo_lo / halo_hi point at TWO rows each (rows -2, -1
+  // and nl, nl+1), tab_j is valid for rows -2 .. nl+1, invc2_halo holds 1/c^2 of rows -2, -1,
+  // nl, nl+1, and j0 is the slab's first global layer (z1 vanishes only off the grid)
+  const double* invc2_halo;
+  int j0;
 };
 
 struct PointArgs {
@@ -128,8 +133,9 @@ int launch_probe_kind(int kind, int blocks, const double2* u, const double* ic, 
                       size_t len, hipStream_t s);
 int stencil_grid_blocks(int n, int rows, int rows_per_block, int row_step = 0);
 int stencil_bands(int rows, int rows_per_block, int row_step);  // tiles along j
-// Fused M A for the two-sweep shifted-Laplace M (sl_fused.hip): a.u = v, a.out0 = w; single
-// slab whose halo rows are zero rows; a.tab_r2x != nullptr selects the 9-point operator.
+// Fused M A for the two-sweep shifted-Laplace M (sl_fused.hip): a.u = v, a.out0 = w; two halo
+// rows per side and the extended tables (StencilArgs, fused SL fields); a.tab_r2x != nullptr
+// selects the 9-point operator.
 void launch_sl2(bool const_c, const StencilArgs& a, hipStream_t stream, int variant = -1);
 int stencil_rows_per_block(int n, int rows);
 void launch_point(int op, bool const_c, const PointArgs& a, int blocks, hipStream_t stream);

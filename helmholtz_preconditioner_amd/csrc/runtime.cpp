@@ -87,6 +87,12 @@ struct Slab {
   double2* tab_r2x = nullptr;  // 9-point only: R2 = 1/s2 of local rows -1 .. nl ([nl + 2])
   double2* halo_lo_buf = nullptr;
   double2* halo_hi_buf = nullptr;
+  // for the fused shifted-Laplace M A (sl_fused.hip) across slabs / ranks, which reads v two
+  // rows beyond the slab and evaluates the first sweep on the neighbours' boundary rows:
+  double2* tab_j_ext = nullptr;  // [nl + 4][4]: the tab_j rows of local rows -2 .. nl+1
+  double* invc2_halo = nullptr;  // [4][n]: 1/c^2 of local rows -2, -1, nl, nl+1 (0 off-grid)
+  double2* halo2_lo = nullptr;   // [2][n]: cross-rank v rows -2, -1
+  double2* halo2_hi = nullptr;   // [2][n]: cross-rank v rows nl, nl+1
   int rpb = 16;
 };
 }  // namespace
@@ -103,7 +109,8 @@ struct hh_op {
   size_t nloc = 0;
   std::vector<Slab> slabs;
   double2* tab_i = nullptr;
-  double2* zero_row = nullptr;
+  double2* zero_row = nullptr;   // two zero rows (the fused SL kernel reads two halo rows)
+  bool sl_ext_ok = true;          // every rank holds the medium two layers beyond its slab
   // preconditioner
   int pkind = HH_PREC_NONE;
   double beta = 0.5, damping = 1.0;
@@ -279,37 +286,81 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
   return nparts;
 }
 
-// w = M A (s v) for the two-sweep shifted-Laplace M in one launch (sl_fused.hip): T and the
-// first sweep never leave the chip.  Single slab of a single rank only (the fused band reads
-// v two rows beyond its own, which a cross-slab halo of one row does not carry).
+// w = M A (s v) for the two-sweep shifted-Laplace M in one launch per slab (sl_fused.hip): T
+// and the first sweep never leave the chip.  A band reads v two rows beyond its own rows and
+// evaluates the first sweep on its two halo rows, so the slab needs two halo rows per side
+// (exchanged here across ranks; read in place from a neighbouring slab on the same device) and
+// the medium and PML tables two layers beyond it (Slab::tab_j_ext, invc2_halo).
 bool sl_fused_applies(const hh_op* op) {
-  return op->sl_fuse && op->sweeps == 2 && op->slabs.size() == 1 && op->ctx->world == 1;
+  return op->sl_fuse && op->sweeps == 2 && op->sl_ext_ok;
 }
 void run_sl2(hh_op* op, const double2* v, const double* vs, double2* out) {
-  const Slab& s = op->slabs[0];
-  StencilArgs a{};
-  a.u = v + s.off;
-  a.halo_lo = op->zero_row;
-  a.halo_hi = op->zero_row;
-  a.invc2 = op->const_c ? nullptr : s.invc2;
-  a.invc2_const = op->invc2_const;
-  a.tab_i = op->tab_i;
-  a.tab_j = s.tab_j;
-  a.n = op->n;
-  a.nl = s.nl;
-  a.row_begin = 0;
-  a.row_end = s.nl;
-  a.rows_per_block = op->rpb_override > 0 ? std::min(op->rpb_override, s.nl) : s.rpb;
-  a.mshift = op->mshift;
-  a.damping = op->damping;
-  a.in_scale = vs;
-  a.out0 = out + s.off;
-  a.stop = op->stop_flag;
-  a.tab_r2x = op->points == 9 ? s.tab_r2x : nullptr;  // selects the 9-point kernel
-  a.w9 = op->w9;
-  if (op->tk0) HIPC(hipEventRecord(op->tk0, op->ctx->stream));
-  launch_sl2(op->const_c, a, op->ctx->stream, op->variant);
-  if (op->tk1) HIPC(hipEventRecord(op->tk1, op->ctx->stream));
+  hh_ctx* c = op->ctx;
+  const int n = op->n;
+  const int S = (int)op->slabs.size();
+  const bool lo_x = c->world > 1 && c->rank > 0;
+  const bool hi_x = c->world > 1 && c->rank < c->world - 1;
+  if (lo_x || hi_x) {
+    const Slab& s0 = op->slabs[0];
+    const Slab& sl = op->slabs[S - 1];
+    c->comm->halo(lo_x ? v + s0.off : nullptr, lo_x ? s0.halo2_lo : nullptr,
+                  hi_x ? v + sl.off + (size_t)(sl.nl - 2) * n : nullptr,
+                  hi_x ? sl.halo2_hi : nullptr, 2 * 2 * sizeof(double) * (size_t)n, c->stream,
+                  c->cstream, c->ev_in);
+  }
+  auto launch_rows = [&](int si, int r0, int r1, int rpb, int step, hipStream_t st) {
+    if (r1 <= r0) return;
+    const Slab& s = op->slabs[si];
+    StencilArgs a{};
+    a.u = v + s.off;
+    a.halo_lo = si > 0 ? v + op->slabs[si - 1].off + (size_t)(op->slabs[si - 1].nl - 2) * n
+                       : (lo_x ? s.halo2_lo : op->zero_row);
+    a.halo_hi = si < S - 1 ? v + op->slabs[si + 1].off : (hi_x ? s.halo2_hi : op->zero_row);
+    a.invc2 = op->const_c ? nullptr : s.invc2;
+    a.invc2_halo = s.invc2_halo;
+    a.invc2_const = op->invc2_const;
+    a.tab_i = op->tab_i;
+    a.tab_j = s.tab_j;  // row 0 of tab_j_ext: rows -2 .. nl+1 are valid
+    a.j0 = s.j0;
+    a.n = n;
+    a.nl = s.nl;
+    a.row_begin = r0;
+    a.row_end = r1;
+    a.row_step = step;
+    a.rows_per_block = (op->rpb_override > 0 && rpb > 2) ? std::min(op->rpb_override, r1 - r0) : rpb;
+    a.mshift = op->mshift;
+    a.damping = op->damping;
+    a.in_scale = vs;
+    a.out0 = out + s.off;
+    a.stop = op->stop_flag;
+    a.tab_r2x = op->points == 9 ? s.tab_r2x : nullptr;  // selects the 9-point kernel
+    a.w9 = op->w9;
+    launch_sl2(op->const_c, a, st, op->variant);
+  };
+  // interior rows (no cross-rank halo needed: a band reads two rows beyond itself) first
+  for (int si = 0; si < S; ++si) {
+    const Slab& s = op->slabs[si];
+    const int r0 = (si == 0 && lo_x) ? 2 : 0;
+    const int r1 = (si == S - 1 && hi_x) ? s.nl - 2 : s.nl;
+    if (si == 0 && op->tk0) HIPC(hipEventRecord(op->tk0, c->stream));
+    launch_rows(si, r0, r1, s.rpb, 0, c->stream);
+    if (si == 0 && op->tk1) HIPC(hipEventRecord(op->tk1, c->stream));
+  }
+  if (lo_x || hi_x) {
+    // the two rows next to each cross-rank boundary, on the halo stream behind the exchange
+    hipStream_t hs = c->cstream;
+    const Slab& s0 = op->slabs[0];
+    const Slab& sl = op->slabs[S - 1];
+    if (S == 1 && lo_x && hi_x) {
+      if (s0.nl < 4) launch_rows(0, 0, s0.nl, s0.nl, 0, hs);     // (no interior rows)
+      else launch_rows(0, 0, s0.nl, 2, s0.nl - 2, hs);          // rows 0-1 and nl-2 - nl-1
+    } else {
+      if (lo_x) launch_rows(0, 0, std::min(2, s0.nl), 2, 0, hs);
+      if (hi_x) launch_rows(S - 1, std::max(0, sl.nl - 2), sl.nl, 2, 0, hs);
+    }
+    HIPC(hipEventRecord(c->ev_halo, hs));
+    HIPC(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+  }
   HIPC(hipGetLastError());
   op->stats.spmv_count++;
 }
@@ -769,8 +820,8 @@ HH_API int hh_op_create(hh_ctx* c, int n, int b, double cconst, double eta, doub
     }
     op->tab_i = dalloc<double2>(3 * (size_t)n);
     HIPC(hipMemcpy(op->tab_i, ti.data(), ti.size() * sizeof(double2), hipMemcpyHostToDevice));
-    op->zero_row = dalloc<double2>(n);
-    HIPC(hipMemsetAsync(op->zero_row, 0, n * sizeof(double2), c->stream));
+    op->zero_row = dalloc<double2>(2 * (size_t)n);
+    HIPC(hipMemsetAsync(op->zero_row, 0, 2 * n * sizeof(double2), c->stream));
     // local slabs
     const int rows = op->je - op->jb;
     size_t off = 0;
@@ -783,17 +834,21 @@ HH_API int hh_op_create(hh_ctx* c, int n, int b, double cconst, double eta, doub
       sl.off = off;
       off += (size_t)sl.nl * n;
       sl.rpb = stencil_rows_per_block(n, sl.nl);
-      std::vector<double2> tj(4 * (size_t)sl.nl);
-      for (int jl = 0; jl < sl.nl; ++jl) {
+      // per-layer table of local rows -2 .. nl+1 (the fused SL kernel reads two rows beyond
+      // the slab); tab_j proper is rows 0 .. nl-1 of it
+      std::vector<double2> tj(4 * ((size_t)sl.nl + 4));
+      for (int jl = -2; jl < sl.nl + 2; ++jl) {
         const double j = sl.j0 + jl + 1;
         const cd r2 = 1.0 / s2(j * h, cconst, eta, om);
-        tj[4 * jl + 0] = d2(r2);
-        tj[4 * jl + 1] = d2(s2((j - .5) * h, cconst, eta, om) * ih2);
-        tj[4 * jl + 2] = d2(s2((j + .5) * h, cconst, eta, om) * ih2);
-        tj[4 * jl + 3] = d2(om2 * r2);
+        double2* t = &tj[4 * (size_t)(jl + 2)];
+        t[0] = d2(r2);
+        t[1] = d2(s2((j - .5) * h, cconst, eta, om) * ih2);
+        t[2] = d2(s2((j + .5) * h, cconst, eta, om) * ih2);
+        t[3] = d2(om2 * r2);
       }
-      sl.tab_j = dalloc<double2>(tj.size());
-      HIPC(hipMemcpy(sl.tab_j, tj.data(), tj.size() * sizeof(double2), hipMemcpyHostToDevice));
+      sl.tab_j_ext = dalloc<double2>(tj.size());
+      HIPC(hipMemcpy(sl.tab_j_ext, tj.data(), tj.size() * sizeof(double2), hipMemcpyHostToDevice));
+      sl.tab_j = sl.tab_j_ext + 8;  // row 0
       if (!op->const_c) {
         // invc2[jl][ii] = 1 / c_mat[ii, j-1]^2  (c_mat read as c_mat[i-1, j-1]: quirk Q3),
         // transposed once here so the kernel streams it along i with unit stride.
@@ -811,12 +866,48 @@ HH_API int hh_op_create(hh_ctx* c, int n, int b, double cconst, double eta, doub
             }
         sl.invc2 = dalloc<double>(buf.size());
         HIPC(hipMemcpy(sl.invc2, buf.data(), buf.size() * sizeof(double), hipMemcpyHostToDevice));
+        // 1/c^2 of the two layers on each side of the slab (0 off the grid): the fused SL
+        // kernel's first sweep on the neighbours' boundary rows.  A caller that filled only its
+        // own columns of c_mat (zero elsewhere) gets the two-launch path instead.
+        std::vector<double> hb(4 * (size_t)n, 0.0);
+        const int rows4[4] = {sl.j0 - 2, sl.j0 - 1, sl.j1, sl.j1 + 1};
+        for (int q = 0; q < 4; ++q) {
+          const int j = rows4[q];
+          if (j < 0 || j >= n) continue;
+          for (int ii = 0; ii < n; ++ii) {
+            const double cv = c_mat[(size_t)ii * ld + j];
+            if (!(cv > 0.0) || !std::isfinite(cv)) {
+              op->sl_ext_ok = false;
+              break;
+            }
+            hb[(size_t)q * n + ii] = 1.0 / (cv * cv);
+          }
+        }
+        sl.invc2_halo = dalloc<double>(hb.size());
+        HIPC(hipMemcpy(sl.invc2_halo, hb.data(), hb.size() * sizeof(double), hipMemcpyHostToDevice));
       }
+      sl.halo2_lo = dalloc<double2>(2 * (size_t)n);
+      sl.halo2_hi = dalloc<double2>(2 * (size_t)n);
+      HIPC(hipMemsetAsync(sl.halo2_lo, 0, 2 * n * sizeof(double2), c->stream));
+      HIPC(hipMemsetAsync(sl.halo2_hi, 0, 2 * n * sizeof(double2), c->stream));
       sl.halo_lo_buf = dalloc<double2>(n);
       sl.halo_hi_buf = dalloc<double2>(n);
       HIPC(hipMemsetAsync(sl.halo_lo_buf, 0, n * sizeof(double2), c->stream));
       HIPC(hipMemsetAsync(sl.halo_hi_buf, 0, n * sizeof(double2), c->stream));
       op->slabs.push_back(sl);
+    }
+    // The fused SL path exchanges two halo rows, the two-launch path one: every rank must take
+    // the same path, so the condition (medium known two layers beyond every slab, slabs of at
+    // least two layers) is agreed on by all ranks.
+    {
+      bool ok = op->sl_ext_ok;
+      for (const Slab& sl : op->slabs) ok = ok && sl.nl >= 2;
+      if (c->world > 1) {
+        double bad = ok ? 0.0 : 1.0;
+        host_allreduce(c, &bad, 1, true);
+        ok = bad == 0.0;
+      }
+      op->sl_ext_ok = ok;
     }
     // partial-sum workspace: stencil tiles (+ boundary rows) of every slab, or streaming blocks
     size_t tiles = 0;
@@ -847,8 +938,11 @@ static void op_release(hh_op* op) {
   (void)hipStreamSynchronize(op->ctx->stream);
   for (Slab& s : op->slabs) {
     dfree(s.invc2);
-    dfree(s.tab_j);
+    dfree(s.tab_j_ext);  // (tab_j points into it)
     dfree(s.tab_r2x);
+    dfree(s.invc2_halo);
+    dfree(s.halo2_lo);
+    dfree(s.halo2_hi);
     dfree(s.halo_lo_buf);
     dfree(s.halo_hi_buf);
   }

@@ -13,10 +13,12 @@
 // Shape: as stencil.hip's marching tile (XCD-aware band map, register rings, unconditional
 // clamped loads), with two changes.  (1) The second sweep needs z1 one row above and below,
 // so every band also computes the first sweep on its two halo rows (rows rb-1 and re; v rows
-// rb-2 .. re+1).  (2) It needs z1 one column to each side, so strips overlap: a block of TPB
-// threads computes the first sweep on TPB columns and writes w on the TPB-2 inner ones.  The
-// arithmetic is stencil.hip's, term for term (coefficients, FMA order), so w is bit-identical
-// to the two-launch path.
+// rb-2 .. re+1) -- for a band at a slab edge that is the neighbouring slab's (or rank's)
+// boundary row, with its 1/c^2 and PML tables (two halo rows per side, runtime.cpp run_sl2);
+// z1 vanishes only off the grid.  (2) It needs z1 one column to each side, so strips overlap:
+// a block of TPB threads computes the first sweep on TPB columns and writes w on the TPB-2
+// inner ones.  The arithmetic is stencil.hip's, term for term (coefficients, FMA order), so w
+// is bit-identical to the two-launch path on any slab decomposition.
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
 #include "hh_stencil9.hpp"
@@ -73,8 +75,10 @@ __device__ __forceinline__ void sl2_tile(const StencilArgs& a, const int t) {
   ie = min(max(ie, 0), n - 1);
   const double2 z2 = make_double2(0.0, 0.0);
 
+  // rows -2 .. nl+1: two halo rows on each side (StencilArgs, fused SL fields)
   auto rowp = [&](int r) -> const double2* {
-    return r < 0 ? a.halo_lo : (r >= nl ? a.halo_hi : a.u + (size_t)r * n);
+    return r < 0 ? a.halo_lo + (size_t)(r + 2) * n
+                 : (r >= nl ? a.halo_hi + (size_t)(r - nl) * n : a.u + (size_t)r * n);
   };
   auto load_v = [&](int r) -> double2 {
     const double2* p = rowp(r) + cc;
@@ -84,14 +88,19 @@ __device__ __forceinline__ void sl2_tile(const StencilArgs& a, const int t) {
       return *p;
   };
   auto load_in = [&](int r, RowIn& v) {
-    const int rc = min(max(r, 0), nl - 1);
-    if constexpr (!CONSTC) v.ic = __builtin_nontemporal_load(a.invc2 + (size_t)rc * n + cc);
-    else v.ic = a.invc2_const;
+    if constexpr (!CONSTC) {
+      const double* q = r < 0 ? a.invc2_halo + (size_t)(r + 2) * n
+                              : (r >= nl ? a.invc2_halo + (size_t)(r - nl + 2) * n
+                                         : a.invc2 + (size_t)r * n);
+      v.ic = __builtin_nontemporal_load(q + cc);
+    } else {
+      v.ic = a.invc2_const;
+    }
     v.e = rowp(r)[ie];
   };
   const cdouble_p tabj = (cdouble_p)(a.tab_j);
   auto load_tab = [&](int r, RowTab& tb) {
-    const int ru = __builtin_amdgcn_readfirstlane(min(max(r, 0), nl - 1));
+    const int ru = __builtin_amdgcn_readfirstlane(min(max(r, -2), nl + 1));  // tab_j_ext rows
     const cdouble_p q = tabj + 8 * ru;
     tb.R2 = make_double2(q[0], q[1]);
     tb.BS = make_double2(q[2], q[3]);
@@ -124,7 +133,7 @@ __device__ __forceinline__ void sl2_tile(const StencilArgs& a, const int t) {
     Au = cfma(E, uE, Au);
     Au = cfma(N, uN, Au);
     T = cscale(Au, sin);
-    z1 = csel(cin && s >= 0 && s < nl, cscale(cdiv(T, Db), a.damping), z2);
+    z1 = csel(cin && a.j0 + s >= 0 && a.j0 + s < n, cscale(cdiv(T, Db), a.damping), z2);
   };
   // second sweep on row r: w = z1 + damp (T - A_beta z1) / Db
   auto stage2 = [&](double2 zS, double2 zC, double2 zN, double2 T, const RowIn& in,
@@ -226,8 +235,10 @@ __device__ __forceinline__ void sl2_tile9(const StencilArgs& a, const int t) {
   const double2 z2 = make_double2(0.0, 0.0);
   const Stencil9W w = a.w9;
 
+  // rows -2 .. nl+1: two halo rows on each side (StencilArgs, fused SL fields)
   auto rowp = [&](int r) -> const double2* {
-    return r < 0 ? a.halo_lo : (r >= nl ? a.halo_hi : a.u + (size_t)r * n);
+    return r < 0 ? a.halo_lo + (size_t)(r + 2) * n
+                 : (r >= nl ? a.halo_hi + (size_t)(r - nl) * n : a.u + (size_t)r * n);
   };
   auto load_v = [&](int r) -> double2 {
     const double2* p = rowp(r) + cc;
@@ -237,14 +248,19 @@ __device__ __forceinline__ void sl2_tile9(const StencilArgs& a, const int t) {
       return *p;
   };
   auto load_in = [&](int r, RowIn& v) {
-    const int rc = min(max(r, 0), nl - 1);
-    if constexpr (!CONSTC) v.ic = __builtin_nontemporal_load(a.invc2 + (size_t)rc * n + cc);
-    else v.ic = a.invc2_const;
+    if constexpr (!CONSTC) {
+      const double* q = r < 0 ? a.invc2_halo + (size_t)(r + 2) * n
+                              : (r >= nl ? a.invc2_halo + (size_t)(r - nl + 2) * n
+                                         : a.invc2 + (size_t)r * n);
+      v.ic = __builtin_nontemporal_load(q + cc);
+    } else {
+      v.ic = a.invc2_const;
+    }
     v.e = rowp(r)[ie];
   };
   const cdouble_p tabj = (cdouble_p)(a.tab_j);
   auto load_tab = [&](int r, RowTab& tb) {
-    const int ru = __builtin_amdgcn_readfirstlane(min(max(r, 0), nl - 1));
+    const int ru = __builtin_amdgcn_readfirstlane(min(max(r, -2), nl + 1));  // tab_j_ext rows
     const cdouble_p q = tabj + 8 * ru;
     tb.R2 = make_double2(q[0], q[1]);
     tb.BS = make_double2(q[2], q[3]);
@@ -309,7 +325,7 @@ __device__ __forceinline__ void sl2_tile9(const StencilArgs& a, const int t) {
     const double2 M = cscale(cmul(tb.OM, R1), in.ic);
     const double2 Db = stencil9_diag(cmul(M, a.mshift), sum4_of(tb), w);
     T = cscale(op9(M, Xvm, Xvc, Xp, Yc, Yw, Ye, Hvm, Hvc, Hp, vS, vC, vN), sin);
-    z1 = csel(cin && s >= 0 && s < nl, cscale(cdiv(T, Db), a.damping), z2);
+    z1 = csel(cin && a.j0 + s >= 0 && a.j0 + s < n, cscale(cdiv(T, Db), a.damping), z2);
     Xvm = Xvc;
     Xvc = Xp;
     Hvm = Hvc;
@@ -460,7 +476,7 @@ void launch_sl2(bool const_c, const StencilArgs& a_in, hipStream_t stream, int v
     ntu = variant % 24 >= 12;
   }
   const int rows = a.row_end - a.row_begin;
-  a.row_step = a.rows_per_block;
+  if (a.row_step <= 0) a.row_step = a.rows_per_block;  // (> 0: spaced boundary bands)
   a.tiles_x = (n + (tpb - 2) - 1) / (tpb - 2);
   a.tiles_y = stencil_bands(rows, a.rows_per_block, a.row_step);
   a.tiles_per_xcd = (a.tiles_x * a.tiles_y + 7) / 8;

@@ -217,7 +217,8 @@ int hh_op_tune(hh_op* op, int variant, int rows_per_block, int grid_blocks);
 int hh_op_set_stencil(hh_op* op, int points, double alpha, double c, double d);
 /* Two-sweep shifted-Laplace M: apply M A in one fused launch (default 1) or as the stencil
  * + sweep pair (0).  Same results bit for bit; the fused form moves 40 instead of 112 B per
- * unknown.  It applies to a single slab of a single rank; elsewhere the pair runs. */
+ * unknown.  Any slab / rank layout (ranks exchange two halo rows for it); it needs the medium
+ * two layers beyond every slab in the c_mat given to hh_op_create, else the pair runs. */
 int hh_op_sl_fusion(hh_op* op, int enable);
 /* Sweeping preconditioner form (speed / memory only; results agree to rounding):
  *   mode -1 (default) dense transfer matrices when n <= 2048 and the n^3 x 16 B fit in HBM,

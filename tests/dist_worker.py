@@ -38,6 +38,10 @@ def main():
     y = A @ xg[j0:j1].ravel()
     f = H.init_f1_mat(.5, .125, om, n)[j0:j1].ravel()
     out = dict(j0=j0, j1=j1, y=y)
+    # the two-sweep shifted-Laplace M A (fused: two halo rows exchanged across ranks)
+    Msl = H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7)
+    Msl.configure()
+    out["ysl"] = A._apply_host(xg[j0:j1].ravel(), H._ffi.HH_APPLY_PREC_A)
     for name, M in () if a.apply_only else (("none", None), ("jacobi", "jacobi"),
                     ("sl", H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7))):
         x, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=50, M=M,

@@ -34,6 +34,9 @@ def _single_domain(n, stencil=5):
     rng = np.random.default_rng(5)
     xg = rng.standard_normal(n * n) + 1j * rng.standard_normal(n * n)
     res = dict(y=A @ xg)
+    M = H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7)
+    M.configure()
+    res["ysl"] = A._apply_host(xg, H._ffi.HH_APPLY_PREC_A)
     f = H.init_f1_mat(.5, .125, om, n).ravel()
     for name, M in (("none", None), ("jacobi", "jacobi"),
                     ("sl", H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7))):
@@ -72,6 +75,8 @@ def test_multiprocess_slabs_match_single_domain(tmp_path, world, slabs, stencil)
         assert a["j1"] == b["j0"]
     y = np.concatenate([p["y"] for p in parts])
     np.testing.assert_array_equal(y, ref["y"])
+    ysl = np.concatenate([p["ysl"] for p in parts])
+    np.testing.assert_array_equal(ysl, ref["ysl"])  # fused M A across ranks
     errs = []
     for name in ("none", "jacobi", "sl"):
         x = np.concatenate([p[f"x_{name}"] for p in parts])

@@ -204,3 +204,25 @@ def test_gmres_with_tile_shape_forced(ctx, M_kind):
     for x, hist in out[1:]:
         np.testing.assert_array_equal(hist, out[0][1])
         np.testing.assert_array_equal(x, out[0][0])
+
+
+@pytest.mark.parametrize("slabs,stencil", [(2, 5), (3, 5), (3, 9)])
+def test_fused_shifted_laplace_on_slabs(slabs, stencil):
+    """The fused M A across virtual slabs (two halo rows read in place from the neighbouring
+    slab, the first sweep evaluated on its boundary rows with its medium and tables):
+    bit-identical to the single domain's fused and two-launch results."""
+    n = 301
+    b, C, wn = 12, 81.0, 10.0
+    om, h, eta = O.problem_params(n, b, wn, 2.0)
+    cm = medium("c1", n)
+    x = rand_complex(n * n, 12)
+    outs = []
+    for s, fused in ((1, True), (1, False), (slabs, True), (slabs, False)):
+        c = H.Context(device=0, virtual_slabs=s)
+        A = H.build_A_matrix(b, C, eta, om, h, n, cm, context=c, stencil=stencil)
+        M = H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7)
+        A.sl_fusion(fused)
+        M.configure()
+        outs.append(A._apply_host(x, H._ffi.HH_APPLY_PREC_A))
+    for y in outs[1:]:
+        np.testing.assert_array_equal(y, outs[0])
