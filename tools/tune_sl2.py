@@ -19,10 +19,11 @@ p.add_argument("--rounds", type=int, default=2)
 p.add_argument("--iters", type=int, default=40)
 p.add_argument("--rpbs", default="8,16,32,64")
 p.add_argument("--variants", default="6,18,30,42")
+p.add_argument("--stencil", type=int, default=5, choices=[5, 9])
 a = p.parse_args()
 n = a.n
 om, h, eta = H.problem_params(n, 12, 100.0, 2.0)
-A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.marmousi_like_c_mat(n))
+A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.marmousi_like_c_mat(n), stencil=a.stencil)
 A.set_preconditioner(_ffi.HH_PREC_SHIFTED_LAPLACE, 0.5, 2, 0.7)
 xs = [A.vector() for _ in range(3)]
 ys = [A.vector() for _ in range(3)]
