@@ -340,11 +340,8 @@ def main():
 
     # ---------------- CPU baseline (rank 0, N=1) ----------------
     if world == 1 and not args.no_cpu_baseline and n <= 4096:
-        if args.medium == "marmousi":
-            c_full = c_mat  # N=1: the full field was generated
-        else:
-            c_full = c_mat
-        result["cpu_baseline"] = cpu_baseline(args, n, omega, h, eta, c_full)
+        # N=1: c_mat holds the full field (plus two layers beyond the grid on each side)
+        result["cpu_baseline"] = cpu_baseline(args, n, omega, h, eta, c_mat)
     elif world > 1:
         result["cpu_baseline"] = None
 
