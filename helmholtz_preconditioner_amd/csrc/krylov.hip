@@ -283,14 +283,21 @@ __global__ void gmres_solve_kernel(GivensState g, int col) {
   for (int k = 0; k <= col; ++k) g.ycoef[k] = cscale(y[k], g.vscale[k]);
 }
 
-// Krylov tuning knobs (hh_tune_krylov): non-temporal basis loads, streaming grid size.
-int g_krylov_nt = 1;  // measured +7.7% GMRES it/s at 4096^2 (profiles/r01_tune_krylov.log)
-int g_krylov_blocks = 1024;
+// Krylov tuning knobs (hh_tune_krylov): non-temporal basis loads, streaming grid size;
+// -1 / 0 = by vector length.  Measured (GMRES(20) it/s, profiles/r01_tune_krylov.log and
+// r01z3_tune_krylov_{1024,128}.log): at 4096^2 NT loads +7.7 % and 1024 blocks best; at
+// 1024^2 (a 21-vector basis of 352 MB, partly served by the 256 MB Infinity Cache) cached
+// loads +3 % and 512 blocks another +2 %; at 128^2 every setting within 1 % (launch-bound).
+int g_krylov_nt = -1;
+int g_krylov_blocks = 0;
+constexpr size_t kSmallKrylovLen = (size_t)2 << 20;  // rank-local unknowns
+
+bool krylov_nt(size_t len) { return g_krylov_nt < 0 ? len > kSmallKrylovLen : g_krylov_nt != 0; }
 
 template <int K>
 void md_launch(const double2* V, size_t ldv, const double2* w, size_t len, double* part,
                int blocks, hipStream_t s, const int* stop) {
-  if (g_krylov_nt)
+  if (krylov_nt(len))
     hipLaunchKernelGGL((multidot_kernel<K, true>), dim3(blocks), dim3(kT), 0, s, V, ldv, w, len,
                        part, stop);
   else
@@ -301,7 +308,7 @@ template <int K>
 void up_launch(const double2* V, size_t ldv, const double* raw, const double* scale,
                const double2* w, double2* wo, size_t len, double* part, int blocks,
                hipStream_t s, const int* stop) {
-  if (g_krylov_nt)
+  if (krylov_nt(len))
     hipLaunchKernelGGL((update_kernel<K, true>), dim3(blocks), dim3(kT), 0, s, V, ldv, raw, scale,
                        w, wo, len, part, stop);
   else
@@ -332,13 +339,15 @@ static_assert(kMaxProj == 32, "table covers 1..kMaxProj");
 }  // namespace
 
 void tune_krylov(int nt, int blocks) {
-  g_krylov_nt = nt;
-  g_krylov_blocks = blocks > 0 ? (blocks < kMaxStreamBlocks ? blocks : kMaxStreamBlocks) : 1024;
+  g_krylov_nt = nt < 0 ? -1 : (nt != 0);
+  g_krylov_blocks = blocks > 0 ? (blocks < kMaxStreamBlocks ? blocks : kMaxStreamBlocks) : 0;
 }
 
 int stream_blocks(size_t len) {
+  const size_t cap = g_krylov_blocks > 0 ? (size_t)g_krylov_blocks
+                                         : (len <= kSmallKrylovLen ? 512 : 1024);
   size_t b = (len + kT - 1) / kT;
-  if (b > (size_t)g_krylov_blocks) b = g_krylov_blocks;
+  if (b > cap) b = cap;
   if (b < 1) b = 1;
   return (int)b;
 }

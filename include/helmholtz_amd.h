@@ -228,7 +228,9 @@ int hh_op_sl_fusion(hh_op* op, int enable);
  * active (optional) receives 1 when the dense form is in use. */
 int hh_op_sweep_mode(hh_op* op, int mode, int* active);
 /* Process-wide tuning of the Krylov streaming kernels (multidot / update): non-temporal
- * basis loads on/off and the streaming grid size (0 = default 1024).  Speed only. */
+ * basis loads on (1) / off (0) / by vector length (-1, default: on above 2^21 rank-local
+ * unknowns) and the streaming grid size (0 = by vector length: 512 blocks up to 2^21
+ * unknowns, 1024 above).  Speed only. */
 int hh_tune_krylov(int nt_loads, int blocks);
 /* Streaming roofline probes (diagnostic only): the stencil's byte mix without neighbour
  * traffic in different access shapes (`kind`, see csrc/probe.hip), `blocks` workgroups,

@@ -10,15 +10,20 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import helmholtz_preconditioner_amd as H  # noqa: E402
 from helmholtz_preconditioner_amd import _ffi  # noqa: E402
 
+# usage: tune_krylov.py [n [config]]  -- config 3 (default): Marmousi-like, shifted-Laplace,
+# wn 100; config 2: constant medium, Jacobi, wn 64 (BASELINE.json)
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-om, h, eta = H.problem_params(n, 12, 100.0, 2.0)
-A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.marmousi_like_c_mat(n))
+config = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+om, h, eta = H.problem_params(n, 12, 100.0 if config == 3 else 64.0, 2.0)
+cm = H.marmousi_like_c_mat(n) if config == 3 else np.ones((n + 2, n + 2))
+A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm)
 f = A.vector(H.init_f1_mat(.5, .125, om, n).ravel())
-M = H.ShiftedLaplace(A, 0.5, 2, 0.7)
+M = H.ShiftedLaplace(A, 0.5, 2, 0.7) if config == 3 else "jacobi"
+grid = (1024, 2048, 4096, 8192) if n >= 2048 else (256, 512, 768, 1024, 2048, 4096)
 res = {}
 for rnd in range(3):
     for nt in (0, 1):
-        for blocks in (1024, 2048, 4096, 8192):
+        for blocks in grid:
             _ffi.check(_ffi.lib.hh_tune_krylov(nt, blocks))
             H.gmres(A, f, rtol=1e-14, restart=20, maxiter=2, M=M, callback=lambda r: None,
                     callback_type="legacy")
