@@ -186,9 +186,12 @@ struct GivensState {
 // exit test (iterative.py:792-795) on the device: presid <= ptol, breakdown, or
 // col == stop_col (the legacy maxiter cap) raises ctrl[0], which turns every kernel queued
 // after it in this cycle into a no-op.
+// With norm_partials non-null, |w_new|^2 is instead summed from the update kernel's
+// `norm_count` block partials inside this launch (bit-identical to launch_reduce; single rank
+// only -- across ranks the norm needs the allreduce in between).
 void launch_gmres_column(const GivensState& g, int col, const double* red_dots,
-                         const double* red_norm, double eps, double ptol, int stop_col,
-                         hipStream_t stream);
+                         const double* red_norm, const double* norm_partials, int norm_count,
+                         double eps, double ptol, int stop_col, hipStream_t stream);
 // Start of a cycle: S[0] = ||Mr||, vscale[0] = 1/||Mr|| from red[idx_m]; status[4] = ||r||.
 void launch_gmres_start(const GivensState& g, const double* red, int idx_r, int idx_m,
                         hipStream_t stream);

@@ -204,14 +204,44 @@ __device__ void zlartg(double2 f, double2 g, double* c, double2* s, double2* r) 
   *s = cmul(cconj(g), fd);
 }
 
+// |w|^2 from the update kernel's per-block partials (column 0 of `width`), summed by one
+// wave in exactly reduce_kernel's order: the 256 strided partial sums of its threads, then its
+// LDS tree (steps 128 and 64 inside each lane's four sums, 32 .. 1 by shuffles).  Every lane
+// returns; lane 0's value is the result, bit-identical to reduce_kernel's out[0].
+__device__ double wave_reduce_like_block(const double* partials, int count, int width) {
+  static_assert(kT == 4 * kWave, "four strided sums per lane emulate a 256-thread block");
+  const int l = threadIdx.x;
+  double s[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    double acc = 0.0;
+    for (int b = l + q * kWave; b < count; b += kT) acc += partials[(size_t)b * width];
+    s[q] = acc;
+  }
+  s[0] += s[2];  // off = 128: threads l and l + 64
+  s[1] += s[3];
+  s[0] += s[1];  // off = 64
+  double x = s[0];
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) x += __shfl_down(x, off);
+  return x;
+}
+
 __global__ void gmres_column_kernel(GivensState g, int col, const double* rd, const double* rn,
-                                    double eps, double ptol, int stop_col) {
-  if (threadIdx.x != 0 || g.ctrl[0]) return;
+                                    const double* npart, int ncount, double eps, double ptol,
+                                    int stop_col) {
+  if (g.ctrl[0]) return;
+  double rn0;
+  if (npart) {
+    rn0 = wave_reduce_like_block(npart, ncount, kMaxNorms);
+  }
+  if (threadIdx.x != 0) return;
+  if (!npart) rn0 = rn[0];
   const int R1 = g.restart + 1;
   double2* h = g.H + (size_t)col * R1;
   for (int k = 0; k <= col; ++k) h[k] = cscale(make_double2(rd[2 * k], rd[2 * k + 1]), g.vscale[k]);
   const double h0 = sqrt(rd[2 * (col + 1)]);
-  const double h1 = sqrt(rn[0]);
+  const double h1 = sqrt(rn0);
   h[col + 1] = make_double2(h1, 0.0);
   double brk = 0.0;
   if (h1 <= eps * h0) {
@@ -391,10 +421,10 @@ void launch_scale_copy(const double2* in, double2* out, size_t len, double s,
 }
 
 void launch_gmres_column(const GivensState& g, int col, const double* red_dots,
-                         const double* red_norm, double eps, double ptol, int stop_col,
-                         hipStream_t stream) {
+                         const double* red_norm, const double* norm_partials, int norm_count,
+                         double eps, double ptol, int stop_col, hipStream_t stream) {
   hipLaunchKernelGGL(gmres_column_kernel, dim3(1), dim3(kWave), 0, stream, g, col, red_dots,
-                     red_norm, eps, ptol, stop_col);
+                     red_norm, norm_partials, norm_count, eps, ptol, stop_col);
 }
 
 void launch_gmres_start(const GivensState& g, const double* red, int idx_r, int idx_m,

@@ -1572,9 +1572,14 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       launch_multidot(V, ldv, K, w, L, op->partials, blocks, s, stp);
       launch_reduce(op->partials, blocks, 2 * K + 2, 2 * K + 1, op->red + 16, s, stp);
       allreduce_sum_dev(op, op->red + 16, 2 * K + 1);
+      // single rank: the column kernel sums the update's norm partials itself (one launch
+      // fewer per iteration); across ranks they are reduced and allreduced first
+      const bool fold = c->world == 1;
       launch_update(V, ldv, K, op->red + 16, g.vscale, w, w, L, op->partials, blocks, s, stp);
-      launch_reduce(op->partials, blocks, kMaxNorms, 1, op->red + 8, s, stp);
-      allreduce_sum_dev(op, op->red + 8, 1);
+      if (!fold) {  // (with reorth this norm is superseded by the second pass's)
+        launch_reduce(op->partials, blocks, kMaxNorms, 1, op->red + 8, s, stp);
+        allreduce_sum_dev(op, op->red + 8, 1);
+      }
       if (reorth) {
         // CGS2: project once more; the H column is the sum of both passes' dots, h0 stays
         // the first pass's |w| (scipy's h0 is taken before orthogonalisation).
@@ -1582,11 +1587,14 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         launch_reduce(op->partials, blocks, 2 * K + 2, 2 * K, op->red + 96, s, stp);
         allreduce_sum_dev(op, op->red + 96, 2 * K);
         launch_update(V, ldv, K, op->red + 96, g.vscale, w, w, L, op->partials, blocks, s, stp);
-        launch_reduce(op->partials, blocks, kMaxNorms, 1, op->red + 8, s, stp);
-        allreduce_sum_dev(op, op->red + 8, 1);
+        if (!fold) {
+          launch_reduce(op->partials, blocks, kMaxNorms, 1, op->red + 8, s, stp);
+          allreduce_sum_dev(op, op->red + 8, 1);
+        }
         launch_add_small(op->red + 96, op->red + 16, 2 * K, s, stp);
       }
-      launch_gmres_column(g, c2, op->red + 16, op->red + 8, eps, ptol, stop_col, s);
+      launch_gmres_column(g, c2, op->red + 16, op->red + 8, fold ? op->partials : nullptr, blocks,
+                          eps, ptol, stop_col, s);
       HIPC(hipGetLastError());
     }
     op->stop_flag = nullptr;
