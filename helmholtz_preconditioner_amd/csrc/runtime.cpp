@@ -72,7 +72,7 @@ struct hh_ctx {
   int device = 0, rank = 0, world = 1, vslabs = 1, transport = 0;
   std::unique_ptr<hh::Comm> comm;  // null at world == 1
   hipStream_t stream = nullptr;   // compute
-  hipStream_t cstream = nullptr;  // halo exchange
+  hipStream_t cstream = nullptr;  // halo exchange + boundary rows (highest priority)
   hipEvent_t ev_in = nullptr, ev_halo = nullptr;
   double* dscratch = nullptr;     // device scratch for host collectives
   double* hpinned = nullptr;      // pinned host staging
@@ -683,7 +683,13 @@ HH_API int hh_ctx_create_ex(int device, int rank, int world, const unsigned char
   c->transport = transport;
   try {
     HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIPC(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    // The halo stream runs the exchange (RCCL send/recv kernels) and the boundary rows
+    // concurrently with the interior stencil launch, which alone fills every CU: give it the
+    // highest priority so the dispatcher places its few blocks first instead of behind the
+    // interior grid.
+    int prio_least = 0, prio_greatest = 0;
+    HIPC(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
+    HIPC(hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, prio_greatest));
     HIPC(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
     HIPC(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
     c->dscratch = dalloc<double>(256);
