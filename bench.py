@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--gmres-iters", type=int, default=40, help="timed inner GMRES iterations")
     p.add_argument("--restart", type=int, default=20)
     p.add_argument("--no-gmres", action="store_true")
+    p.add_argument("--const-steps", type=int, default=200,
+                   help="timed applies of the same grid with a constant medium (reported as "
+                        "spmv_constant_medium; 0 = skip; not run when --medium const)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-gmres-iters", type=int, default=4)
     p.add_argument("--virtual-slabs", type=int, default=1)
@@ -294,6 +297,36 @@ def main():
         "bytes_per_launch": bpp * interior_rows * n,
     }
     del x, y
+
+    # ---------------- the same apply on a constant medium (same grid and ranks) ----------------
+    # The north star reports constant-k next to Marmousi-like grids at every GPU count: one
+    # extra operator (no 1/c^2 stream: 32 B per unknown), timed exactly like the steps above.
+    if args.medium != "const" and args.const_steps > 0:
+        Ac = H.build_A_matrix(args.b, args.C, eta, omega, h, n,
+                              np.broadcast_to(1.0, (n + 2, n + 2)), context=ctx,
+                              stencil=args.stencil)
+        if args.variant >= 0:
+            Ac.tune(args.variant)
+        xc, yc = [Ac.vector() for _ in range(R)], [Ac.vector() for _ in range(R)]
+        for k, v in enumerate(xc):
+            v.fill_hash(2024 + k)
+        if args.warmup > 0:
+            Ac.time_apply(xc, yc, args.warmup)
+        ctx.barrier()
+        t0 = time.perf_counter()
+        Ac.time_apply(xc, yc, args.const_steps)
+        ctx.barrier()
+        tc = float(ctx.allreduce_max([time.perf_counter() - t0])[0])
+        vc = Ac.bytes_per_point * float(n) * n * args.const_steps / tc / 1e9
+        result["spmv_constant_medium"] = {
+            "value": round(vc, 2), "unit": "GB/s", "steps": args.const_steps,
+            "ms_per_step": round(tc * 1e3 / args.const_steps, 5),
+            "bytes_per_unknown": Ac.bytes_per_point,
+            "pct_hbm_peak": round(100.0 * vc / (HBM_PEAK_GBPS * world), 2)}
+        for v in xc + yc:
+            v.close()
+        Ac.close()
+        del xc, yc, Ac
 
     # ---------------- GMRES(restart): timed inner iterations ----------------
     if not args.no_gmres and args.gmres_iters > 0:

@@ -110,6 +110,8 @@ def test_bench_two_ranks_rehearsal(tmp_path):
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["config"]["n"] == 768 and res["value"] > 0
     assert res["gmres"]["iterations"] == 6
+    assert res["spmv_constant_medium"]["value"] > 0
+    assert res["spmv_constant_medium"]["bytes_per_unknown"] == 32
 
 
 @pytest.mark.parametrize("world", [2, 3])
