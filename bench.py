@@ -38,7 +38,10 @@ def parse():
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200, help="timed operator applies")
-    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=200,
+                   help="untimed applies before each timed leg: the GPU's clocks ramp up over "
+                        "the first ~tens of ms of load (4096^2: 121 us per apply after 20 "
+                        "warm-up applies, 116 us after 200 or 1000, profiles/r01z3_warmup.log)")
     p.add_argument("--grid", type=int, default=0, help="global grid size n (default 4096*sqrt(N))")
     p.add_argument("--medium", default="marmousi", choices=["marmousi", "const", "c1"])
     p.add_argument("--wave-num", type=float, default=100.0)

@@ -22,11 +22,11 @@ rocm-smi --showproductname > "$OUT/smi.log" 2>&1 || true
 step pytest_gpu 480 python -m pytest tests -m gpu -q -x "$@"
 step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 300 python bench.py
-step rocprof 240 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline --gmres-iters 40
+step rocprof 240 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --gmres-iters 40
 step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 tools/prof_stencil.py --iters 20
 step pmc_write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 tools/prof_stencil.py --iters 20
 step bench9 300 python bench.py --stencil 9
-step rocprof9 240 rocprofv3 --kernel-trace --stats -d "$OUT/prof9" -o run --output-format csv -- python3 bench.py --stencil 9 --steps 100 --warmup 10 --no-cpu-baseline --gmres-iters 40
+step rocprof9 240 rocprofv3 --kernel-trace --stats -d "$OUT/prof9" -o run --output-format csv -- python3 bench.py --stencil 9 --no-cpu-baseline --gmres-iters 40
 step pmc_fetch9 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch9" -o run --output-format csv -- python3 tools/prof_stencil.py --iters 20 --stencil 9
 step pmc_write9 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write9" -o run --output-format csv -- python3 tools/prof_stencil.py --iters 20 --stencil 9
 step sweep 300 python tools/bench_sweep.py --form dense 127 255 511 1023
