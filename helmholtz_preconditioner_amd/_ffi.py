@@ -46,6 +46,7 @@ SIGNATURES = [
     ("hh_last_error", ctypes.c_char_p, []),
     ("hh_device_count", c_int, [c_ip]),
     ("hh_comm_unique_id", c_int, [c_ubp]),
+    ("hh_comm_selftest", c_int, [c_int, c_dp, c_dp]),
     ("hh_ctx_create", c_int, [c_int, c_int, c_int, c_ubp, c_int, PP]),
     ("hh_ctx_create_ex", c_int, [c_int, c_int, c_int, c_ubp, c_int, c_int, PP]),
     ("hh_ctx_destroy", c_int, [c_void_p]),

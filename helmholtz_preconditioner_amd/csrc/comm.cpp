@@ -11,9 +11,11 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <cstring>
 #include <new>
 #include <thread>
+#include <vector>
 
 #include "hh_error.hpp"
 
@@ -209,6 +211,57 @@ std::unique_ptr<Comm> make_rccl_comm(int rank, int world, const unsigned char id
 std::unique_ptr<Comm> make_shm_comm(int rank, int world, const unsigned char id[128]) {
   return std::make_unique<ShmComm>(rank, world, id);
 }
+void rccl_selftest(int device, double* allreduce_err, double* p2p_err) {
+  // The RCCL calls RcclComm makes, in one process: a 1-rank communicator, an in-place
+  // float64 sum on the compute stream, and a grouped send/recv pair (to itself) on a second,
+  // highest-priority stream ordered behind the compute stream by an event -- the halo pattern.
+  constexpr int kCount = 4096;
+  HIPC(hipSetDevice(device));
+  struct Res {
+    ncclComm_t comm = nullptr;
+    hipStream_t s = nullptr, hs = nullptr;
+    hipEvent_t ev = nullptr;
+    double* d = nullptr;
+    ~Res() {
+      if (d) (void)hipFree(d);
+      if (ev) (void)hipEventDestroy(ev);
+      if (hs) (void)hipStreamDestroy(hs);
+      if (s) (void)hipStreamDestroy(s);
+      if (comm) ncclCommDestroy(comm);
+    }
+  } r;
+  ncclUniqueId id;
+  NCCLC(ncclGetUniqueId(&id));
+  NCCLC(ncclCommInitRank(&r.comm, 1, id, 0));
+  int lo = 0, hi = 0;
+  HIPC(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  HIPC(hipStreamCreateWithFlags(&r.s, hipStreamNonBlocking));
+  HIPC(hipStreamCreateWithPriority(&r.hs, hipStreamNonBlocking, hi));
+  HIPC(hipEventCreateWithFlags(&r.ev, hipEventDisableTiming));
+  HIPC(hipMalloc(reinterpret_cast<void**>(&r.d), 3 * kCount * sizeof(double)));
+  std::vector<double> h(3 * kCount);
+  for (int k = 0; k < kCount; ++k) h[k] = h[kCount + k] = 0.5 + k * 1e-3;
+  for (int k = 0; k < kCount; ++k) h[2 * kCount + k] = -1.0;
+  HIPC(hipMemcpyAsync(r.d, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, r.s));
+  NCCLC(ncclAllReduce(r.d, r.d, kCount, ncclFloat64, ncclSum, r.comm, r.s));
+  HIPC(hipEventRecord(r.ev, r.s));
+  HIPC(hipStreamWaitEvent(r.hs, r.ev, 0));
+  NCCLC(ncclGroupStart());
+  NCCLC(ncclRecv(r.d + 2 * kCount, kCount, ncclFloat64, 0, r.comm, r.hs));
+  NCCLC(ncclSend(r.d + kCount, kCount, ncclFloat64, 0, r.comm, r.hs));
+  NCCLC(ncclGroupEnd());
+  HIPC(hipStreamSynchronize(r.hs));
+  std::vector<double> o(3 * kCount);
+  HIPC(hipMemcpy(o.data(), r.d, o.size() * sizeof(double), hipMemcpyDeviceToHost));
+  double ea = 0.0, ep = 0.0;
+  for (int k = 0; k < kCount; ++k) {
+    ea = std::max(ea, std::abs(o[k] - h[k]));
+    ep = std::max(ep, std::abs(o[2 * kCount + k] - h[kCount + k]));
+  }
+  *allreduce_err = ea;
+  *p2p_err = ep;
+}
+
 void rccl_unique_id(unsigned char out[128]) {
   ncclUniqueId id;
   NCCLC(ncclGetUniqueId(&id));

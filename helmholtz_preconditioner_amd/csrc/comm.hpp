@@ -34,5 +34,6 @@ class Comm {
 std::unique_ptr<Comm> make_rccl_comm(int rank, int world, const unsigned char id[128]);
 std::unique_ptr<Comm> make_shm_comm(int rank, int world, const unsigned char id[128]);
 void rccl_unique_id(unsigned char out[128]);
+void rccl_selftest(int device, double* allreduce_err, double* p2p_err);
 
 }  // namespace hh

@@ -662,6 +662,16 @@ HH_API int hh_comm_unique_id(unsigned char id_out[128]) {
   GUARD_END
 }
 
+HH_API int hh_comm_selftest(int device, double* allreduce_err, double* p2p_err) {
+  GUARD_BEGIN
+  REQUIRE(allreduce_err && p2p_err, "null output");
+  int ndev = 0;
+  HIPC(hipGetDeviceCount(&ndev));
+  REQUIRE(device >= 0 && device < ndev, "device %d not present (%d devices)", device, ndev);
+  rccl_selftest(device, allreduce_err, p2p_err);
+  GUARD_END
+}
+
 HH_API int hh_ctx_create_ex(int device, int rank, int world, const unsigned char* id,
                             int virtual_slabs, int transport, hh_ctx** out) {
   GUARD_BEGIN

@@ -73,6 +73,12 @@ int hh_device_count(int* count);
 /* RCCL bootstrap: rank 0 calls this and ships the 128 bytes to the others. */
 int hh_comm_unique_id(unsigned char id_out[128]);
 
+/* Diagnostic (no reference counterpart): the RCCL calls of the row-slab transport in one
+ * process on `device` -- a 1-rank communicator, an in-place allreduce and a grouped
+ * send/recv to itself on a second stream ordered by an event.  Writes the max abs error of
+ * each (0 when RCCL works). */
+int hh_comm_selftest(int device, double* allreduce_err, double* p2p_err);
+
 /* Create a context on HIP device `device` as rank `rank` of `world` ranks
  * (one process per GPU).  world == 1: nccl_id may be NULL.  `virtual_slabs`
  * >= 1 splits this rank's rows into that many slabs on the same device, with

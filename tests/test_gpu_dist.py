@@ -144,3 +144,15 @@ def test_multiprocess_apply_large_grid(tmp_path, world):
         assert p.returncode == 0, p.stdout.read().decode()[-3000:]
     y = np.concatenate([np.load(o)["y"] for _, o in procs])
     np.testing.assert_array_equal(y, yref)
+
+
+def test_rccl_calls_in_one_process():
+    """The RCCL calls the production transport makes (RcclComm), on this box's RCCL: a 1-rank
+    communicator, an in-place allreduce and the grouped send/recv on the halo stream.  (Two
+    ranks cannot share one GPU under RCCL; the N > 1 orchestration is covered above with the
+    SHM transport.)"""
+    import ctypes
+    from helmholtz_preconditioner_amd import _ffi
+    ea, ep = ctypes.c_double(-1.0), ctypes.c_double(-1.0)
+    _ffi.check(_ffi.lib.hh_comm_selftest(0, ctypes.byref(ea), ctypes.byref(ep)))
+    assert ea.value == 0.0 and ep.value == 0.0
