@@ -23,6 +23,7 @@ step pytest_gpu 480 python -m pytest tests -m gpu -q -x "$@"
 step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 300 python bench.py
 step rocprof 240 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --gmres-iters 40
+python3 tools/rocprof_timed_avg.py "$OUT/prof/run_kernel_trace.csv" "void hh::(anonymous namespace)::tile_kernel<0, false, 4" 200 > "$OUT/rocprof_timed.log" 2>&1 || true
 step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 tools/prof_stencil.py --iters 20
 step pmc_write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 tools/prof_stencil.py --iters 20
 step bench9 300 python bench.py --stencil 9
