@@ -15,7 +15,15 @@ region (max over ranks); algorithmic bytes = 40 B per unknown (read u 16 + write
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
 one process per GPU, row-slab decomposition with RCCL halo exchange overlapped
 with the interior stencil; weak scaling -- the grid grows to n = 4096 sqrt(N)
-(rounded to 32) so every GPU keeps ~4096^2 unknowns.
+(rounded to 32) so every GPU keeps ~4096^2 unknowns.  The same job then also runs the
+fixed BASELINE grid (4096^2, or 16384^2 under --config 5) on all N ranks and, on rank 0
+alone, on one GPU: the `same_n` block carries the same-N speedup and per-GPU fraction of
+HBM peak the north star grades (strong scaling).
+
+Every rank runs a watchdog thread: each phase (communicator init, first halo exchange,
+first allreduce, first GMRES cycle, ...) has a time bound, and a phase that overruns it
+prints the phase and rank and ends the process with status 3 -- a stalled collective
+becomes a diagnosable non-zero exit instead of a hang.
 """
 from __future__ import annotations
 
@@ -25,6 +33,7 @@ import math
 import os
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -32,6 +41,49 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+
+
+class Watchdog:
+    """Per-rank phase timer: `phase(name, bound_s)` starts a phase; a
+    daemon thread ends the process with status 3 (os._exit: no re-exec, no cleanup that could
+    block on the stalled collective) when the current phase overruns its bound, after
+    printing the phase and rank.  ctypes releases the GIL inside the native calls, so the
+    thread runs while the main thread is blocked in RCCL or a stream synchronize.
+    HH_WATCHDOG_SCALE multiplies every bound (tests shorten them); HH_BENCH_STALL=rank:phase
+    makes that rank hang at the start of the phase whose name starts with `phase` (the
+    stalled-rank rehearsal)."""
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.scale = float(os.environ.get("HH_WATCHDOG_SCALE", "1"))
+        self.name, self.deadline, self.t0 = "startup", None, time.monotonic()
+        self.lock = threading.Lock()
+        stall = os.environ.get("HH_BENCH_STALL", "")
+        self.stall = tuple(stall.split(":", 1)) if ":" in stall else None
+        threading.Thread(target=self._run, daemon=True).start()
+
+    def phase(self, name, bound_s):
+        with self.lock:
+            self.name, self.t0 = name, time.monotonic()
+            self.deadline = self.t0 + bound_s * self.scale
+        if self.stall and int(self.stall[0]) == self.rank and name.startswith(self.stall[1]):
+            while True:  # simulated stalled rank: only the watchdog ends it
+                time.sleep(1)
+
+    def done(self):
+        with self.lock:
+            self.name, self.deadline = "done", None
+
+    def _run(self):
+        while True:
+            time.sleep(0.5)
+            with self.lock:
+                late = self.deadline is not None and time.monotonic() > self.deadline
+                name, el = self.name, time.monotonic() - self.t0
+            if late:
+                print(f"[bench watchdog] rank {self.rank}: phase '{name}' stalled for {el:.0f} s "
+                      f"(bound exceeded); exiting with status 3", file=sys.stderr, flush=True)
+                os._exit(3)
 
 
 def parse():
@@ -67,6 +119,10 @@ def parse():
                    help="distinct (x, y) vector pairs the timed applies cycle through: like the "
                         "applies of a solve, none re-reads lines an earlier one left in the "
                         "256 MiB Infinity Cache (1 = the same x every step)")
+    p.add_argument("--same-n", type=int, default=-1,
+                   help="N > 1: also time this fixed grid on all ranks and on one GPU (rank 0) "
+                        "for the same-N speedup (-1 = 4096, or 16384 under --config 5; 0 = skip)")
+    p.add_argument("--same-n-steps", type=int, default=100)
     p.add_argument("--config", type=int, default=0, choices=[0, 1, 2, 3, 4, 5],
                    help="BASELINE.json config preset (fixed grid => strong scaling); "
                         "0 = config 3 workload with weak scaling (default)")
@@ -204,6 +260,125 @@ def host_description():
            f"{len(os.sched_getaffinity(0))})"
 
 
+def timed_applies(A, ctx, R, steps, warmup):
+    """`steps` timed applies over R rotating (x, y) pairs after `warmup` untimed ones:
+    (wall s of the timed region, max over ranks; device ms; average interior-kernel ms)."""
+    x, y = [A.vector() for _ in range(R)], [A.vector() for _ in range(R)]
+    for k, v in enumerate(x):
+        v.fill_hash(2024 + k)
+    if warmup > 0:
+        A.time_apply(x, y, warmup)
+    ctx.barrier()
+    t0 = time.perf_counter()
+    dev_ms, kern_ms = A.time_apply(x, y, steps)
+    ctx.barrier()
+    elapsed = float(ctx.allreduce_max([time.perf_counter() - t0])[0])
+    for v in x + y:
+        v.close()
+    return elapsed, dev_ms, kern_ms
+
+
+def make_precond(H, A, kind, sweeps):
+    if kind == "sl":
+        return H.ShiftedLaplace(A, beta=0.5, sweeps=sweeps, damping=0.7)
+    return H.Jacobi(A) if kind == "jacobi" else None
+
+
+def timed_gmres(H, A, ctx, f_host, args, iters, wd=None):
+    """Warm-up (two iterations: the first restart cycle, first allreduces), then `iters`
+    timed legacy-counted inner iterations: (iterations, wall s max over ranks, history)."""
+    f = A.vector(f_host)
+    M = make_precond(H, A, args.precond, args.sl_sweeps)
+    if wd:
+        wd.phase("gmres warm-up (first restart cycle, first in-solve allreduces)", 180)
+    H.gmres(A, f, rtol=1e-14, restart=args.restart, maxiter=2, M=M,
+            callback=lambda r: None, callback_type="legacy")
+    ctx.barrier()
+    if wd:
+        wd.phase("timed gmres", 120 + 0.5 * iters)
+    t0 = time.perf_counter()
+    xs, info, hist = H.gmres(A, f, rtol=1e-14, restart=args.restart, maxiter=iters,
+                             M=M, callback=lambda r: None, callback_type="legacy",
+                             return_history=True)
+    ctx.barrier()
+    tg = float(ctx.allreduce_max([time.perf_counter() - t0])[0])
+    f.close()
+    xs.close()
+    return len(hist), tg, hist
+
+
+def gmres_bytes(args, its, bpp, N):
+    """algorithmic bytes of `its` GMRES inner iterations (CGS, lazy normalisation): SpMV 40N +
+    projection 16(j+2)N + update 16(j+3)N (SURVEY 8d style), + the preconditioner's own
+    traffic: none for Jacobi (fused into the SpMV) and for the two-sweep shifted-Laplace M
+    (M A in one launch, csrc/sl_fused.hip: 40 B/unknown in all); otherwise the stencil + sweep
+    launches, 16 + 56 B per further sweep."""
+    js = [i % args.restart for i in range(its)]
+    fused = args.sl_sweeps == 2
+    sl_extra = 0 if fused else bpp + 16 + 56 * (args.sl_sweeps - 1)
+    pre = {"sl": sl_extra, "jacobi": 0, "none": 0}[args.precond]
+    return sum((bpp + pre) * N + 16 * (j + 2) * N + 16 * (j + 3) * N for j in js), fused
+
+
+def same_n_leg(H, dist, args, ctx, rank, world, wd):
+    """Strong scaling at the fixed BASELINE grid in the same job: the grid on all `world`
+    ranks, then on rank 0 alone with a world-1 context on its own GPU (the other ranks wait at
+    a barrier).  Returns the `same_n` block (rank 0) -- speedups are 1-GPU time / N-GPU time
+    of the same work."""
+    import numpy as np
+    n = args.same_n
+    omega, h, eta = H.problem_params(n, args.b, args.wave_num, args.alpha)
+    R = max(1, args.rotate)
+    steps = args.same_n_steps
+    its = min(args.gmres_iters, 20)
+
+    def measure(c, r, w):
+        j0, j1 = dist.slab_bounds(n, w, r)
+        c_mat = make_medium(args.medium, n, (j0 - 2, j1 + 2))
+        A = H.build_A_matrix(args.b, args.C, eta, omega, h, n, c_mat, context=c,
+                             stencil=args.stencil)
+        del c_mat
+        el, _, kern = timed_applies(A, c, R, steps, min(args.warmup, 100))
+        out = {"spmv_ms_per_step": el * 1e3 / steps, "kernel_ms": kern,
+               "bytes_per_unknown": A.bytes_per_point}
+        if not args.no_gmres and its > 0:
+            k, tg, _ = timed_gmres(H, A, c, local_f1(omega, n, j0, j1), args, its)
+            out["gmres_iters_per_s"] = k / tg
+        A.close()
+        return out
+
+    wd.phase(f"same-N leg: {n}^2 on {world} ranks", 600)
+    multi = measure(ctx, rank, world)
+    single = None
+    wd.phase(f"same-N leg: {n}^2 on rank 0's GPU alone (other ranks wait)", 900)
+    if rank == 0:
+        c1 = H.Context(device=ctx.device)
+        single = measure(c1, 0, 1)
+        c1.close()
+    ctx.barrier()
+    if rank != 0:
+        return None
+    bpp = multi["bytes_per_unknown"]
+    agg = bpp * float(n) * n / (multi["spmv_ms_per_step"] * 1e-3) / 1e9
+    one = bpp * float(n) * n / (single["spmv_ms_per_step"] * 1e-3) / 1e9
+    block = {
+        "n": n, "medium": args.medium, "steps": steps, "scaling": "strong",
+        "spmv": {"value": round(agg, 2), "unit": "GB/s",
+                 "ms_per_step": round(multi["spmv_ms_per_step"], 5),
+                 "per_gpu_frac": round(agg / (HBM_PEAK_GBPS * world), 4),
+                 "single_gpu_value": round(one, 2),
+                 "single_gpu_ms_per_step": round(single["spmv_ms_per_step"], 5),
+                 "speedup_same_n": round(single["spmv_ms_per_step"] / multi["spmv_ms_per_step"], 3)},
+    }
+    if "gmres_iters_per_s" in multi:
+        block["gmres"] = {"iterations": its, "precond": args.precond,
+                          "iters_per_s": round(multi["gmres_iters_per_s"], 3),
+                          "single_gpu_iters_per_s": round(single["gmres_iters_per_s"], 3),
+                          "speedup_same_n": round(multi["gmres_iters_per_s"]
+                                                  / single["gmres_iters_per_s"], 3)}
+    return block
+
+
 def main():
     args = parse()
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -215,12 +390,16 @@ def main():
     from helmholtz_preconditioner_amd import dist
 
     rank, world, _ = dist.env_rank_world()
+    wd = Watchdog(rank)
+    transport = os.environ.get("HH_TRANSPORT", "rccl") if world > 1 else "none"
+    wd.phase("context + communicator init (ncclCommInitRank)", 240)
     ctx = dist.init_from_env(virtual_slabs=args.virtual_slabs)
     H.set_default_context(ctx)
 
     n = args.grid or int(round(4096 * math.sqrt(world) / 32) * 32)
     omega, h, eta = H.problem_params(n, args.b, args.wave_num, args.alpha)
     j0, j1 = dist.slab_bounds(n, world, rank)
+    wd.phase("operator build", 300)
     t0 = time.perf_counter()
     # this rank's layers plus two on each side (the fused shifted-Laplace M A evaluates the
     # first sweep on the neighbouring ranks' boundary layers)
@@ -239,12 +418,15 @@ def main():
     # solve.  (The same x every step lets part of it survive on the die between launches:
     # +13 % at 4096^2, profiles/r01l_*.)
     R = max(1, args.rotate)
+    wd.phase("first applies (first halo exchange) + warm-up", 120 + 0.05 * args.warmup)
     x, y = [A.vector() for _ in range(R)], [A.vector() for _ in range(R)]
     for k, v in enumerate(x):
         v.fill_hash(2024 + k)
     if args.warmup > 0:
         A.time_apply(x, y, args.warmup)
+    wd.phase("first host allreduce (barrier)", 60)
     ctx.barrier()
+    wd.phase("timed applies", 120 + 0.05 * args.steps)
     t0 = time.perf_counter()
     dev_ms, kern_ms = A.time_apply(x, y, args.steps)
     ctx.barrier()
@@ -256,6 +438,8 @@ def main():
         - (1 if (world > 1 and rank < world - 1) else 0)
     achieved = bpp * float(interior_rows) * n / (kern_ms * 1e-3) / 1e9
     achieved_min = float(ctx.allreduce_max([-achieved])[0]) * -1.0
+    medium_desc = {"marmousi": "Marmousi-like layered velocity (seeded generator)",
+                   "const": "constant velocity c = 1", "c1": "init_c1_mat(.5, .5) velocity"}
 
     result = {
         "metric": METRIC,
@@ -269,7 +453,7 @@ def main():
         "scaling": "strong" if args.config and world > 1 else "weak",
         "vs_baseline": None,
         "dtype": "complex128",
-        "data": f"synthetic: {args.medium}-like velocity (seeded), hash-filled complex input, "
+        "data": f"synthetic: {medium_desc[args.medium]}, hash-filled complex input, "
                 f"{R} rotating vector pairs",
         "config": {
             "workload": f"config{args.config or 3}: {n}x{n} {args.medium} velocity, matrix-free "
@@ -277,7 +461,9 @@ def main():
                         f"(+ GMRES({args.restart}) {args.precond}-preconditioned)",
             "n": n, "unknowns": n * n, "wave_num": args.wave_num, "b": args.b, "C": args.C,
             "alpha": args.alpha, "bytes_per_unknown": bpp, "stencil_points": args.stencil,
-            "parallelism": f"row-slab x{world} (RCCL halo)" if world > 1 else "single GPU",
+            "parallelism": (f"row-slab x{world} ({'RCCL' if transport == 'rccl' else 'host-staged SHM'}"
+                            f" halo{', all ranks on one GPU' if os.environ.get('HH_FORCE_DEVICE') else ''})"
+                            if world > 1 else "single GPU"),
         },
         "pct_hbm_peak": round(100.0 * value / (HBM_PEAK_GBPS * world), 2),
         "device_ms_per_step": round(dev_ms / args.steps, 5),
@@ -299,68 +485,35 @@ def main():
         "kernel_ms": round(kern_ms, 5),
         "bytes_per_launch": bpp * interior_rows * n,
     }
+    for v in x + y:
+        v.close()
     del x, y
 
     # ---------------- the same apply on a constant medium (same grid and ranks) ----------------
     # The north star reports constant-k next to Marmousi-like grids at every GPU count: one
     # extra operator (no 1/c^2 stream: 32 B per unknown), timed exactly like the steps above.
     if args.medium != "const" and args.const_steps > 0:
+        wd.phase("constant-medium applies", 180 + 0.05 * (args.warmup + args.const_steps))
         Ac = H.build_A_matrix(args.b, args.C, eta, omega, h, n,
                               np.broadcast_to(1.0, (n + 2, n + 2)), context=ctx,
                               stencil=args.stencil)
         if args.variant >= 0:
             Ac.tune(args.variant)
-        xc, yc = [Ac.vector() for _ in range(R)], [Ac.vector() for _ in range(R)]
-        for k, v in enumerate(xc):
-            v.fill_hash(2024 + k)
-        if args.warmup > 0:
-            Ac.time_apply(xc, yc, args.warmup)
-        ctx.barrier()
-        t0 = time.perf_counter()
-        Ac.time_apply(xc, yc, args.const_steps)
-        ctx.barrier()
-        tc = float(ctx.allreduce_max([time.perf_counter() - t0])[0])
+        tc, _, _ = timed_applies(Ac, ctx, R, args.const_steps, args.warmup)
         vc = Ac.bytes_per_point * float(n) * n * args.const_steps / tc / 1e9
         result["spmv_constant_medium"] = {
             "value": round(vc, 2), "unit": "GB/s", "steps": args.const_steps,
             "ms_per_step": round(tc * 1e3 / args.const_steps, 5),
             "bytes_per_unknown": Ac.bytes_per_point,
             "pct_hbm_peak": round(100.0 * vc / (HBM_PEAK_GBPS * world), 2)}
-        for v in xc + yc:
-            v.close()
         Ac.close()
-        del xc, yc, Ac
+        del Ac
 
     # ---------------- GMRES(restart): timed inner iterations ----------------
     if not args.no_gmres and args.gmres_iters > 0:
-        f = A.vector(local_f1(omega, n, j0, j1))
-        if args.precond == "sl":
-            M = H.ShiftedLaplace(A, beta=0.5, sweeps=args.sl_sweeps, damping=0.7)
-        elif args.precond == "jacobi":
-            M = H.Jacobi(A)
-        else:
-            M = None
-        H.gmres(A, f, rtol=1e-14, restart=args.restart, maxiter=2, M=M,
-                callback=lambda r: None, callback_type="legacy")  # warm-up
-        ctx.barrier()
-        t0 = time.perf_counter()
-        xs, info, hist = H.gmres(A, f, rtol=1e-14, restart=args.restart, maxiter=args.gmres_iters,
-                                 M=M, callback=lambda r: None, callback_type="legacy",
-                                 return_history=True)
-        ctx.barrier()
-        tg = float(ctx.allreduce_max([time.perf_counter() - t0])[0])
-        its = len(hist)
-        # algorithmic bytes / iteration (CGS, lazy normalisation): SpMV 40N + projection
-        # 16(j+2)N + update 16(j+3)N (SURVEY 8d style), + the preconditioner's own traffic:
-        # none for Jacobi (fused into the SpMV) and for the two-sweep shifted-Laplace M on one
-        # slab (M A in one launch, csrc/sl_fused.hip: 40 B/unknown in all); otherwise the
-        # stencil + sweep launches, 16 + 56 B per further sweep.
-        js = [i % args.restart for i in range(its)]
-        N = float(n) * n
-        fused = args.sl_sweeps == 2  # one launch per slab (plus the halo rows) on any layout
-        sl_extra = 0 if fused else bpp + 16 + 56 * (args.sl_sweeps - 1)
-        pre = {"sl": sl_extra, "jacobi": 0, "none": 0}[args.precond]
-        gbytes = sum((bpp + pre) * N + 16 * (j + 2) * N + 16 * (j + 3) * N for j in js)
+        its, tg, hist = timed_gmres(H, A, ctx, local_f1(omega, n, j0, j1), args,
+                                    args.gmres_iters, wd)
+        gbytes, fused = gmres_bytes(args, its, bpp, float(n) * n)
         result["gmres"] = {
             "iters_per_s": round(its / tg, 3),
             "iterations": its,
@@ -372,10 +525,20 @@ def main():
             "algorithmic_GBps": round(gbytes / tg / 1e9, 1),
             "final_rel_presid": float(hist[-1]) if its else None,
         }
-        del f, xs
+    A.close()
+
+    # ---------------- same-N strong scaling (N > 1): the north star's speedup ----------------
+    if world > 1:
+        if args.same_n < 0:
+            args.same_n = 16384 if args.config == 5 else 4096
+        if args.same_n > 0:
+            block = same_n_leg(H, dist, args, ctx, rank, world, wd)
+            if rank == 0:
+                result["same_n"] = block
 
     # ---------------- CPU baseline (rank 0, N=1) ----------------
     if world == 1 and not args.no_cpu_baseline and n <= 4096:
+        wd.phase("cpu baseline", 900)
         # N=1: c_mat holds the full field (plus two layers beyond the grid on each side)
         result["cpu_baseline"] = cpu_baseline(args, n, omega, h, eta, c_mat)
     elif world > 1:
@@ -383,7 +546,9 @@ def main():
 
     if rank == 0:
         print(json.dumps(result), flush=True)
+    wd.phase("final barrier", 120)
     ctx.barrier()
+    wd.done()
 
 
 if __name__ == "__main__":

@@ -31,8 +31,11 @@ HH_PREC_NONE, HH_PREC_JACOBI, HH_PREC_SHIFTED_LAPLACE, HH_PREC_SWEEP, HH_PREC_SW
 HH_APPLY_A, HH_APPLY_JACOBI_A, HH_APPLY_PREC, HH_APPLY_PREC_A = 0, 1, 2, 3
 HH_TRANSPORT_RCCL, HH_TRANSPORT_SHM = 0, 1
 
-GMRES_CALLBACK = ctypes.CFUNCTYPE(None, c_void_p, c_long, c_double)
-GMRES_CYCLE_CALLBACK = ctypes.CFUNCTYPE(None, c_void_p, c_long)
+# callbacks return 0 to continue, non-zero to stop the solve (hh_gmres -> HH_ERR_ABORTED)
+GMRES_CALLBACK = ctypes.CFUNCTYPE(c_int, c_void_p, c_long, c_double)
+GMRES_CYCLE_CALLBACK = ctypes.CFUNCTYPE(c_int, c_void_p, c_long)
+HH_ERR_ABORTED = -6
+ABI_VERSION = 2
 
 
 class HHStats(ctypes.Structure):
@@ -91,7 +94,7 @@ for _name, _res, _args in SIGNATURES:
     _fn.restype = _res
     _fn.argtypes = _args
 
-if lib.hh_abi_version() != 1:
+if lib.hh_abi_version() != ABI_VERSION:
     raise ImportError("libhelmholtz_amd.so ABI version mismatch")
 
 

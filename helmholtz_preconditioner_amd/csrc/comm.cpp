@@ -59,7 +59,10 @@ class RcclComm final : public Comm {
 
 // -------------------------------------------------------------------------- SHM
 constexpr size_t kShmSlotDoubles = 256;          // allreduce slot per rank
-constexpr size_t kShmHaloBytes = 65536 * 16;     // one row of up to n = 65536 complex
+// the fused shifted-Laplace M A exchanges TWO complex rows per side (run_sl2), the plain
+// stencil one: slots hold two rows of up to n = 65536
+constexpr size_t kShmMaxRow = 65536;
+constexpr size_t kShmHaloBytes = 2 * kShmMaxRow * 16;
 constexpr uint64_t kShmMagic = 0x48484d5348574d31ull;
 constexpr double kShmTimeoutS = 300.0;
 
@@ -152,7 +155,8 @@ class ShmComm final : public Comm {
   }
   void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi, size_t bytes,
             hipStream_t compute, hipStream_t, hipEvent_t) override {
-    REQUIRE(bytes <= kShmHaloBytes, "shm halo row too large (n > 65536)");
+    REQUIRE(bytes <= kShmHaloBytes, "shm halo of %zu bytes exceeds the slot (two rows of n <= %zu)",
+            bytes, kShmMaxRow);
     // Device <-> shared memory goes through this rank's pinned staging rows: DMA copies to /
     // from pinned memory on `compute` (ordered after the kernels that produced `send_*` and
     // before the boundary-row kernels that read `recv_*`), completed by a stream sync, and

@@ -43,8 +43,8 @@ struct Error {
   do {                                                                                    \
     ncclResult_t r_ = (expr);                                                             \
     if (r_ != ncclSuccess)                                                                \
-      ::hh::fail(HH_ERR_RCCL, "%s:%d %s -> %s", __FILE__, __LINE__, #expr,                \
-                 ncclGetErrorString(r_));                                                 \
+      ::hh::fail(HH_ERR_RCCL, "%s:%d %s -> %s (%s)", __FILE__, __LINE__, #expr,           \
+                 ncclGetErrorString(r_), ncclGetLastError(nullptr));                      \
   } while (0)
 
 #define REQUIRE(cond, ...)                                                                \

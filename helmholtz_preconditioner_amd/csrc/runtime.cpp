@@ -1496,6 +1496,19 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
   HIPC(hipSetDevice(c->device));
   hipStream_t s = c->stream;
   const auto t_start = std::chrono::steady_clock::now();
+  // In-solve state (the cycle's stop flag every queued kernel polls, the as-is sweep's
+  // constant M b) must not outlive this call on ANY exit path -- an error, an SHM timeout or a
+  // callback abort included: a later plain apply would otherwise poll a raised stop flag and
+  // return a stale buffer.  The stream is drained first so no queued kernel still reads them.
+  struct SolveScope {
+    hh_op* op;
+    ~SolveScope() {
+      (void)hipStreamSynchronize(op->ctx->stream);
+      op->stop_flag = nullptr;
+      dfree(op->sw_const);
+      op->sw_const = nullptr;
+    }
+  } scope{op};
   op->stats = hh_stats{};
   if (restart > (long)op->n * op->n) restart = (int)((long)op->n * op->n);
   ensure_gmres(op, restart);
@@ -1613,7 +1626,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
                           eps, ptol, stop_col, s);
       HIPC(hipGetLastError());
     }
-    op->stop_flag = nullptr;
+    op->stop_flag = nullptr;  // (the SolveScope also clears it if anything above throws)
     // one sync: per-iteration statuses + the last column executed
     HIPC(hipMemcpyAsync(op->status_h, g.status_it, 4 * (size_t)restart * sizeof(double),
                         hipMemcpyDeviceToHost, s));
@@ -1628,7 +1641,10 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       const double pr = op->status_h[4 * k];
       inner += 1;
       if (hist && inner - 1 < hist_cap) hist[inner - 1] = pr / bnrm2;
-      if (cb) cb(user, inner, pr / bnrm2);
+      if (cb && cb(user, inner, pr / bnrm2) != 0) {
+        finish(inner, -1, 0.0);
+        fail(HH_ERR_ABORTED, "gmres stopped by the per-iteration callback at iteration %ld", inner);
+      }
     }
     presid = op->status_h[4 * col];
     breakdown = op->status_h[4 * col + 1] != 0.0;
@@ -1640,11 +1656,13 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     rnorm = std::sqrt(st[0]);
     if (legacy && inner == maxiter) {
       finish(inner, rnorm <= atol ? 0 : (int)std::min<long>(maxiter, 0x7fffffff), rnorm);
-      dfree(op->sw_const);
-      op->sw_const = nullptr;
       return HH_OK;
     }
-    if (op->cycle_cb) op->cycle_cb(op->cycle_user, op->stats.restarts);
+    if (op->cycle_cb && op->cycle_cb(op->cycle_user, op->stats.restarts) != 0) {
+      finish(inner, -1, rnorm);
+      fail(HH_ERR_ABORTED, "gmres stopped by the cycle callback after cycle %ld",
+           op->stats.restarts);
+    }
     if (rnorm <= atol) break;
     else if (breakdown) break;
     else if (presid <= ptol) ptol_max_factor = std::max(eps, 0.25 * ptol_max_factor);
@@ -1652,7 +1670,5 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     ptol = presid * std::min(ptol_max_factor, atol / rnorm);
   }
   finish(inner, rnorm <= atol ? 0 : (int)std::min<long>(maxiter, 0x7fffffff), rnorm);
-  dfree(op->sw_const);
-  op->sw_const = nullptr;
   GUARD_END
 }

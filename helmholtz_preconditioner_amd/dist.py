@@ -73,11 +73,19 @@ def init_from_env(virtual_slabs: int = 1) -> Context:
     communicator when WORLD_SIZE > 1.
 
     Test rehearsal knobs (single-GPU machine): HH_TRANSPORT=shm selects the host-staged
-    shared-memory transport and HH_FORCE_DEVICE=0 puts every rank on device 0.
+    shared-memory transport, HH_FORCE_DEVICE=0 puts every rank on device 0, and
+    HH_RCCL_HOSTID_PER_RANK=1 lets RCCL itself run with every rank on that one device.
     """
     rank, world, local = env_rank_world()
     device = int(os.environ.get("HH_FORCE_DEVICE", local if "LOCAL_RANK" in os.environ else 0))
     transport = os.environ.get("HH_TRANSPORT", "rccl")
+    if world > 1 and transport == "rccl" and os.environ.get("HH_RCCL_HOSTID_PER_RANK") == "1":
+        # RCCL rehearsal with every rank on one GPU (HH_FORCE_DEVICE): RCCL refuses two ranks
+        # on one device of one host, so each rank poses as its own host and the ranks talk
+        # through RCCL's socket transport over loopback.  Set before the first RCCL call.
+        os.environ["NCCL_HOSTID"] = f"hh-rank-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     if world == 1:
         return Context(device=device, virtual_slabs=virtual_slabs)
     make_id = unique_id if transport == "rccl" else (lambda: os.urandom(128))

@@ -333,7 +333,7 @@ class ShiftedLaplace(DevicePreconditioner):
 
     kind = _ffi.HH_PREC_SHIFTED_LAPLACE
 
-    def __init__(self, A: DeviceOperator, beta=0.5, sweeps=4, damping=0.7):
+    def __init__(self, A: DeviceOperator, beta=0.5, sweeps=2, damping=0.7):
         super().__init__(A, beta, sweeps, damping)
 
 

@@ -61,12 +61,15 @@ def gmres(A, b, x0=None, *, rtol=1e-5, atol=0., restart=None, maxiter=None, M=No
         raise ValueError(f"Unknown callback_type: {callback_type!r}")
     if callback is None:
         callback_type = None
-    n = A.shape[0]
+    # scipy's defaults are taken on the GLOBAL system size N = n^2 (iterative.py: n =
+    # len(b)), not on this rank's slab: every rank then runs the same number of cycles and
+    # collectives, whatever the slab sizes.
+    N = int(A.n) * int(A.n)
     if restart is None:
         restart = 20
-    restart = min(restart, n)
+    restart = min(restart, N)
     if maxiter is None:
-        maxiter = n * 10
+        maxiter = N * 10
     legacy = callback_type == 'legacy'
 
     _resolve_precond(A, M)
@@ -84,21 +87,38 @@ def gmres(A, b, x0=None, *, rtol=1e-5, atol=0., restart=None, maxiter=None, M=No
     hist = np.zeros(max(cap, 1), dtype=np.float64)
     cb = _ffi.GMRES_CALLBACK(0)
     ccb = _ffi.GMRES_CYCLE_CALLBACK(0)
+    # An exception raised by the user's callback propagates out of gmres, as in scipy: the
+    # trampoline stores it and returns non-zero, hh_gmres stops at once (HH_ERR_ABORTED), and
+    # the stored exception is re-raised here (ctypes would otherwise print and drop it).
+    raised = []
     if callback is not None and callback_type in ('legacy', 'pr_norm'):
         def _cb(_user, _it, rel):
-            callback(rel)
+            try:
+                callback(rel)
+            except BaseException as e:  # noqa: BLE001 -- re-raised after hh_gmres returns
+                raised.append(e)
+                return 1
+            return 0
         cb = _ffi.GMRES_CALLBACK(_cb)
     elif callback is not None:  # 'x': the iterate after every restart cycle (downloaded for
         def _ccb(_user, _cycle):  # numpy b, the DeviceVector itself otherwise)
-            callback(xv.download() if host_in else xv)
+            try:
+                callback(xv.download() if host_in else xv)
+            except BaseException as e:  # noqa: BLE001
+                raised.append(e)
+                return 1
+            return 0
         ccb = _ffi.GMRES_CYCLE_CALLBACK(_ccb)
     iters, info, rnorm, bnorm = ctypes.c_long(), ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
     check(lib.hh_op_set_cycle_callback(A.handle, ccb, None))
     try:
-        check(lib.hh_gmres(A.handle, bv.handle, xv.handle, float(rtol), float(atol),
-                           int(restart), int(maxiter), int(legacy), int(bool(reorth)),
-                           _ffi.dptr(hist), cap, cb, None, ctypes.byref(iters),
-                           ctypes.byref(info), ctypes.byref(rnorm), ctypes.byref(bnorm)))
+        rc = lib.hh_gmres(A.handle, bv.handle, xv.handle, float(rtol), float(atol),
+                          int(restart), int(maxiter), int(legacy), int(bool(reorth)),
+                          _ffi.dptr(hist), cap, cb, None, ctypes.byref(iters),
+                          ctypes.byref(info), ctypes.byref(rnorm), ctypes.byref(bnorm))
+        if rc == _ffi.HH_ERR_ABORTED and raised:
+            raise raised[0]
+        check(rc)
     finally:
         check(lib.hh_op_set_cycle_callback(A.handle, _ffi.GMRES_CYCLE_CALLBACK(0), None))
     A.last_solve = dict(iterations=iters.value, info=info.value, rnorm=rnorm.value,

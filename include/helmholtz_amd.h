@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define HH_ABI_VERSION 1
+#define HH_ABI_VERSION 2
 
 typedef enum {
   HH_OK = 0,
@@ -36,7 +36,8 @@ typedef enum {
   HH_ERR_HIP = -2,       /* HIP runtime failure                                 */
   HH_ERR_RCCL = -3,      /* RCCL failure                                        */
   HH_ERR_ALLOC = -4,     /* device / host allocation failure                    */
-  HH_ERR_STATE = -5      /* call not valid in this state (e.g. wrong context)   */
+  HH_ERR_STATE = -5,     /* call not valid in this state (e.g. wrong context)   */
+  HH_ERR_ABORTED = -6    /* a hh_gmres callback returned non-zero: solve stopped */
 } hh_err;
 
 /* Preconditioner kinds filling the reference's M slot (code.py:510-511). */
@@ -186,8 +187,12 @@ int hh_op_time_apply_set(hh_op* op, const hh_vec* const* xs, hh_vec* const* ys, 
  *   b, x: device vectors (x holds x0 on entry, the solution on exit).
  *   hist: optional host array of length >= maxiter*restart (legacy: maxiter)
  *         receiving presid/||b|| per inner iteration.
- *   cb:   optional per-iteration callback(user, iteration, presid/||b||). */
-typedef void (*hh_gmres_callback)(void* user, long iteration, double rel_presid);
+ *   cb:   optional per-iteration callback(user, iteration, presid/||b||); returns 0 to
+ *         continue, non-zero to stop the solve at once (hh_gmres then returns
+ *         HH_ERR_ABORTED; scipy propagates a callback's exception the same way).
+ * On every exit path -- success, error or abort -- the operator is left ready for plain
+ * applies (no stale in-solve state). */
+typedef int (*hh_gmres_callback)(void* user, long iteration, double rel_presid);
 int hh_gmres(hh_op* op, const hh_vec* b, hh_vec* x, double rtol, double atol,
              int restart, long maxiter, int legacy_maxiter, int reorth,
              double* hist, long hist_cap, hh_gmres_callback cb, void* user,
@@ -195,8 +200,9 @@ int hh_gmres(hh_op* op, const hh_vec* b, hh_vec* x, double rtol, double atol,
 /* Per-restart-cycle hook of the following hh_gmres calls on `op` (NULL removes it): called
  * after each cycle's x update and true residual, where scipy calls callback(x) for
  * callback_type='x' (iterative.py, after `r = b - matvec(x)`; not after the legacy exit);
- * x is complete on the device, so the hook may download it (hh_vec_download). */
-typedef void (*hh_gmres_cycle_callback)(void* user, long cycle);
+ * x is complete on the device, so the hook may download it (hh_vec_download).  Returns 0
+ * to continue, non-zero to stop (HH_ERR_ABORTED). */
+typedef int (*hh_gmres_cycle_callback)(void* user, long cycle);
 int hh_op_set_cycle_callback(hh_op* op, hh_gmres_cycle_callback cb, void* user);
 
 /* Performance tuning of the stencil kernel used by HH_APPLY_A: variant in [0, 48) selects the

@@ -293,7 +293,7 @@ def jacobi_preconditioner(A):
                                               dtype=np.complex128)
 
 
-def shifted_laplace_jacobi(b, const, eta, omega, h, n, c_mat, beta=0.5, sweeps=4,
+def shifted_laplace_jacobi(b, const, eta, omega, h, n, c_mat, beta=0.5, sweeps=2,
                            damping=0.7):
     """Shifted-Laplace preconditioner M ~= A_beta^-1 (BASELINE config 3).
 
@@ -302,7 +302,9 @@ def shifted_laplace_jacobi(b, const, eta, omega, h, n, c_mat, beta=0.5, sweeps=4
     is approximated by ``sweeps`` damped-Jacobi sweeps from a zero guess:
         z_0 = 0,  z_{k+1} = z_k + damping * D_beta^-1 (r - A_beta z_k).
     The first sweep is just damping*D^-1 r.  Must match the device kernel
-    sequence in csrc/precond.hip (same recurrence, same order).
+    sequence (csrc/stencil.hip EPI_SL_FIRST / EPI_SL_SWEEP, and the fused two-sweep
+    M A of csrc/sl_fused.hip): same recurrence, same order.  Default 2 sweeps, as in
+    every graded path (BASELINE config 3, bench.py, driver.run_solver).
     """
     Ab = build_A_matrix(b, const, eta, omega, h, n, np.asarray(c_mat) / np.sqrt(1 + 1j * beta))
     dinv = 1.0 / Ab.diagonal()

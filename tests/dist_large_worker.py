@@ -1,0 +1,57 @@
+"""One rank of a BASELINE config-4 run (8192^2 constant medium, used by
+tests/test_gpu_configs.py): every rank sits on device 0 with the shared-memory transport.
+
+The input is the hash fill (hh_vec_fill_hash: a pure function of the global index, identical
+for any slab decomposition), so nothing of size N crosses the process boundary on the way in;
+the parent's single-domain results are memory-mapped from .npy files and compared here, rank
+by rank, and only small summaries come back.
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import helmholtz_preconditioner_amd as H  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rank", type=int)
+    p.add_argument("--world", type=int)
+    p.add_argument("--id")
+    p.add_argument("--out")
+    p.add_argument("--n", type=int)
+    p.add_argument("--wave-num", type=float)
+    p.add_argument("--iters", type=int)
+    p.add_argument("--ref-dir")
+    a = p.parse_args()
+    ctx = H.Context(device=0, rank=a.rank, world=a.world, nccl_id=bytes.fromhex(a.id),
+                    transport="shm")
+    n = a.n
+    om, h, eta = H.problem_params(n, 12, a.wave_num, 2.0)
+    A = H.build_A_matrix(12, 81.0, eta, om, h, n, np.broadcast_to(1.0, (n + 2, n + 2)),
+                         context=ctx)
+    j0, j1 = A.row_begin, A.row_end
+    x, y = A.vector(), A.vector()
+    x.fill_hash(7)
+    A.apply_device(x, y)
+    yl = y.download()
+    yref = np.load(os.path.join(a.ref_dir, "y.npy"), mmap_mode="r")[j0 * n:j1 * n]
+    out = dict(j0=j0, j1=j1, y_mismatch=int(np.count_nonzero(yl != yref)))
+    del yl, yref
+    f = H.init_f1_mat(.5, .125, om, n)[j0:j1].ravel()
+    xs, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=a.iters, M="jacobi",
+                             callback=lambda r: None, callback_type="legacy",
+                             return_history=True)
+    xref = np.load(os.path.join(a.ref_dir, "x.npy"), mmap_mode="r")[j0 * n:j1 * n]
+    out.update(info=info, hist=hist, dx2=float(np.sum(np.abs(xs - xref) ** 2)),
+               x2=float(np.sum(np.abs(xref) ** 2)))
+    np.savez(a.out, **out)
+    ctx.barrier()
+
+
+if __name__ == "__main__":
+    main()

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     bound = {name for name, _, _ in _ffi.SIGNATURES}
     assert set(declared_symbols()) <= bound, set(declared_symbols()) - bound
-    assert lib.hh_abi_version() == 1
+    assert lib.hh_abi_version() == _ffi.ABI_VERSION == 2
 
 
 def test_library_is_gfx950_code():

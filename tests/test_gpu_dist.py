@@ -1,9 +1,10 @@
 """GPU tier, N > 1: row-slab decomposition across processes.
 
-RCCL refuses two ranks on one GPU, so these tests run W processes on device 0 with the
-host-staged shared-memory transport (csrc/comm.cpp ShmComm) -- the same orchestration as
-the RCCL production path (slab ownership, one-row halo exchange, rank-ordered global
-reductions), checked against the single-domain result on the same GPU:
+The box has one GPU, so these tests run W processes on device 0, over the host-staged
+shared-memory transport (csrc/comm.cpp ShmComm) and over the production RCCL transport
+(RcclComm; one NCCL_HOSTID per rank, see rccl_rank_env) -- slab ownership, the halo
+exchange, rank-ordered global reductions -- checked against the single-domain result on
+the same GPU:
   * the operator apply: bit-identical slabs;
   * GMRES (none / Jacobi / shifted-Laplace): residual history and field to 1e-8 (the
     reductions sum partials in a different order; the contract is 1e-6);
@@ -26,7 +27,39 @@ pytestmark = pytest.mark.gpu
 WORKER = os.path.join(ROOT, "tests", "dist_worker.py")
 
 
-def _single_domain(n, stencil=5):
+def rccl_rank_env(rank):
+    """RCCL on one GPU: a distinct NCCL_HOSTID per rank makes every rank its own "host"
+    (RCCL refuses two ranks on one device of one host), connected by RCCL's socket
+    transport over loopback."""
+    return dict(NCCL_HOSTID=f"hh-rank-{rank}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1",
+                HH_FORCE_DEVICE="0")
+
+
+def _run_workers(tmp_path, world, n, extra=(), transport="shm", timeout=240):
+    tok = os.urandom(128).hex()
+    procs = []
+    for r in range(world):
+        out = tmp_path / f"r{r}.npz"
+        env = dict(os.environ, **(rccl_rank_env(r) if transport == "rccl" else {}),
+                   TMPDIR=str(tmp_path))
+        procs.append((subprocess.Popen([sys.executable, WORKER, "--rank", str(r), "--world",
+                                        str(world), "--id", tok, "--out", str(out), "--n", str(n),
+                                        "--transport", transport] + list(extra),
+                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env),
+                      out))
+    try:
+        for p, _ in procs:
+            p.wait(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        for q, _ in procs:
+            q.kill()
+        raise
+    for p, _ in procs:
+        assert p.returncode == 0, p.stdout.read().decode()[-3000:]
+    return [np.load(o) for _, o in procs]
+
+
+def _single_domain(n, stencil=5, default_limits=False):
     ctx = H.Context(device=0)
     om, h, eta = H.problem_params(n, 12, 6.0, 2.0)
     A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.init_c1_mat(.5, .5, n), context=ctx,
@@ -44,32 +77,20 @@ def _single_domain(n, stencil=5):
                                 callback=lambda r: None, callback_type="legacy",
                                 return_history=True)
         res[f"x_{name}"], res[f"info_{name}"], res[f"hist_{name}"] = x, info, hist
+    if default_limits:
+        res["x_default"], res["info_default"] = H.gmres(A, f, rtol=1e-3, M="jacobi")
     return res
 
 
 @pytest.mark.parametrize("world,slabs,stencil", [(2, 1, 5), (3, 1, 5), (2, 2, 5), (4, 1, 5),
                                                 (3, 2, 5), (3, 1, 9), (2, 2, 9)])
 def test_multiprocess_slabs_match_single_domain(tmp_path, world, slabs, stencil):
-    n = 150
-    ref = _single_domain(n, stencil)
-    tok = os.urandom(128).hex()
-    procs = []
-    for r in range(world):
-        out = tmp_path / f"r{r}.npz"
-        procs.append((subprocess.Popen([sys.executable, WORKER, "--rank", str(r), "--world",
-                                        str(world), "--id", tok, "--out", str(out), "--n", str(n),
-                                        "--slabs", str(slabs), "--stencil", str(stencil)],
-                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT), out))
-    for p, _ in procs:
-        try:
-            p.wait(timeout=240)
-        except subprocess.TimeoutExpired:
-            for q, _ in procs:
-                q.kill()
-            raise
-    for p, _ in procs:
-        assert p.returncode == 0, p.stdout.read().decode()[-3000:]
-    parts = [np.load(o) for _, o in procs]
+    _check_against_single_domain(
+        _run_workers(tmp_path, world, 150, ["--slabs", str(slabs), "--stencil", str(stencil)]),
+        _single_domain(150, stencil), world, 150)
+
+
+def _check_against_single_domain(parts, ref, world, n):
     assert parts[0]["j0"] == 0 and parts[-1]["j1"] == n
     for a, b in zip(parts, parts[1:]):
         assert a["j1"] == b["j0"]
@@ -91,27 +112,81 @@ def test_multiprocess_slabs_match_single_domain(tmp_path, world, slabs, stencil)
     bad = [e for e in errs if e[2] != e[3] or e[4] != e[5] or not e[6] < 1e-8]
     assert not bad, "\n".join(map(str, errs))
     assert all(float(p["maxrank"]) == world - 1 for p in parts)
+    if "x_default" in ref:
+        x = np.concatenate([p["x_default"] for p in parts])
+        assert all(int(p["info_default"]) == int(ref["info_default"]) for p in parts)
+        assert np.linalg.norm(x - ref["x_default"]) <= 1e-8 * np.linalg.norm(ref["x_default"])
 
 
-def test_bench_two_ranks_rehearsal(tmp_path):
+def test_uneven_slabs_default_limits(tmp_path):
+    """n = 151 over 3 ranks (50 / 50 / 51 layers) with scipy's default restart and maxiter:
+    the defaults come from the global N = n^2 on every rank (a rank-local N would give the
+    ranks different maxiter and desynchronise their collectives)."""
+    n = 151
+    _check_against_single_domain(_run_workers(tmp_path, 3, n, ["--default-limits"]),
+                                 _single_domain(n, default_limits=True), 3, n)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rccl_transport_ranks_match_single_domain(tmp_path, world):
+    """The production RCCL transport (RcclComm) with world > 1: ncclCommInitRank across
+    processes, the grouped halo send/recv on the highest-priority stream overlapped with the
+    interior launch, and the in-solve allreduces -- apply and fused M A bit-identical to the
+    single domain, GMRES (none / Jacobi / shifted-Laplace) to 1e-8.  All ranks share device 0
+    (see rccl_rank_env)."""
+    n = 150
+    _check_against_single_domain(_run_workers(tmp_path, world, n, transport="rccl", timeout=180),
+                                 _single_domain(n), world, n)
+
+
+def _torchrun_bench(tmp_path, world, bench_args, env_extra, timeout=400):
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    env = dict(os.environ, HH_TRANSPORT="shm", HH_FORCE_DEVICE="0", TMPDIR=str(tmp_path))
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--grid", "768", "--steps", "10",
-           "--warmup", "2", "--gmres-iters", "6", "--no-cpu-baseline"]
-    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=400, cwd=ROOT)
+    env = dict(os.environ, HH_FORCE_DEVICE="0", TMPDIR=str(tmp_path), **env_extra)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "bench.py"), "--gpus", str(world)] + bench_args
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+
+
+BENCH_SMALL = ["--grid", "768", "--steps", "10", "--warmup", "2", "--gmres-iters", "6",
+               "--no-cpu-baseline", "--same-n", "1024", "--same-n-steps", "10"]
+
+
+@pytest.mark.parametrize("transport", ["shm", "rccl"])
+def test_bench_two_ranks_rehearsal(tmp_path, transport):
+    """`bench.py --gpus 2` end to end under torch.distributed.run (both ranks on device 0):
+    one JSON line with the weak-scaling aggregate, the same-N strong-scaling block (the grid
+    on 2 ranks and on rank 0 alone) and the transport actually used in `parallelism`."""
+    extra = {"HH_TRANSPORT": transport}
+    if transport == "rccl":  # RCCL's own per-rank env (NCCL_HOSTID ...) is per process here:
+        extra["HH_RCCL_HOSTID_PER_RANK"] = "1"  # bench sets it from LOCAL_RANK
+    out = _torchrun_bench(tmp_path, 2, BENCH_SMALL, extra)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["config"]["n"] == 768 and res["value"] > 0
+    assert ("RCCL" if transport == "rccl" else "SHM") in res["config"]["parallelism"]
     assert res["gmres"]["iterations"] == 6
     assert res["spmv_constant_medium"]["value"] > 0
     assert res["spmv_constant_medium"]["bytes_per_unknown"] == 32
+    sn = res["same_n"]
+    assert sn["n"] == 1024 and sn["spmv"]["speedup_same_n"] > 0
+    assert sn["spmv"]["single_gpu_value"] > 0 and 0 < sn["spmv"]["per_gpu_frac"] < 1
+    assert sn["gmres"]["speedup_same_n"] > 0
+
+
+def test_bench_stalled_rank_exits_with_the_phase_named(tmp_path):
+    """A rank that stalls (simulated: HH_BENCH_STALL makes rank 1 hang when its first applies
+    start) must end the job with a non-zero status and the stalled phase named, not hang."""
+    out = _torchrun_bench(tmp_path, 2, BENCH_SMALL,
+                          {"HH_TRANSPORT": "shm", "HH_WATCHDOG_SCALE": "0.1",
+                           "HH_BENCH_STALL": "1:first applies"}, timeout=180)
+    assert out.returncode != 0
+    assert "[bench watchdog] rank 1: phase 'first applies" in out.stderr, out.stderr[-3000:]
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -125,25 +200,8 @@ def test_multiprocess_apply_large_grid(tmp_path, world):
     A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.init_c1_mat(.5, .5, n), context=ctx)
     rng = np.random.default_rng(5)
     yref = A @ (rng.standard_normal(n * n) + 1j * rng.standard_normal(n * n))
-    tok = os.urandom(128).hex()
-    procs = []
-    for r in range(world):
-        out = tmp_path / f"r{r}.npz"
-        procs.append((subprocess.Popen([sys.executable, WORKER, "--rank", str(r), "--world",
-                                        str(world), "--id", tok, "--out", str(out), "--n", str(n),
-                                        "--apply-only"],
-                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT), out))
-    for p, _ in procs:
-        try:
-            p.wait(timeout=240)
-        except subprocess.TimeoutExpired:
-            for q, _ in procs:
-                q.kill()
-            raise
-    for p, _ in procs:
-        assert p.returncode == 0, p.stdout.read().decode()[-3000:]
-    y = np.concatenate([np.load(o)["y"] for _, o in procs])
-    np.testing.assert_array_equal(y, yref)
+    parts = _run_workers(tmp_path, world, n, ["--apply-only"])
+    np.testing.assert_array_equal(np.concatenate([p["y"] for p in parts]), yref)
 
 
 def test_rccl_calls_in_one_process():

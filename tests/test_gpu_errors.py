@@ -116,3 +116,67 @@ def test_sweeping_needs_one_slab():
         H.gmres(A, np.ones(n * n, complex), M=H.Sweeping(A), maxiter=2)
     R = O.build_A_matrix(6, 81.0, eta, om, h, n, medium("c1", n))
     _still_works(A, R)
+
+
+class _Stop(Exception):
+    pass
+
+
+def _raise_at(k):
+    calls = []
+
+    def cb(r):
+        calls.append(r)
+        if len(calls) == k:
+            raise _Stop(f"stop at {k}")
+    return cb, calls
+
+
+@pytest.mark.parametrize("callback_type", ["legacy", "pr_norm", "x"])
+def test_callback_exception_propagates(op, callback_type):
+    """scipy propagates an exception raised by the callback out of gmres (users rely on it
+    to stop a solve early); the device solve stops at once and re-raises it."""
+    A, R, _ = op
+    f = np.ones(A.shape[0], complex)
+    cb, calls = _raise_at(3 if callback_type != "x" else 1)
+    with pytest.raises(_Stop):
+        H.gmres(A, f, rtol=1e-12, restart=5, maxiter=50, callback=cb, callback_type=callback_type)
+    assert len(calls) == (3 if callback_type != "x" else 1)
+    # nothing of the aborted solve is left behind: plain applies and a new solve are exact
+    _still_works(A, R)
+    x, info, hist = H.gmres(A, f, rtol=1e-3, maxiter=5, callback=lambda r: None,
+                            callback_type="legacy", return_history=True)
+    xr, infor, histr, _ = O.gmres_reference(R, f, rtol=1e-3, maxiter=5)
+    assert info == infor and np.max(np.abs(hist - histr) / histr) < 1e-6
+
+
+def test_aborted_asis_sweep_leaves_no_constant_map(ctx):
+    """Sweeping(reference=True) makes M a constant map (algo2_4(b), quirk Q1) for the
+    duration of a solve only: after a solve aborted by its callback, a plain M x is
+    algo2_4(x) again (the in-solve state is released on every exit path)."""
+    n, b, C = 37, 6, 61.0
+    om, h, eta = O.problem_params(n, b, 3.0, 2.0)
+    cm = medium("c2", n)
+    A = H.build_A_matrix(b, C, eta, om, h, n, cm, context=ctx)
+    M = H.Sweeping(A, reference=True)
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    cb, _ = _raise_at(1)
+    with pytest.raises(_Stop):
+        H.gmres(A, f, rtol=1e-12, maxiter=50, M=M, callback=cb, callback_type="legacy")
+    st = O.SweepState(b, C, eta, om, h, n, cm)
+    x = rand_complex(n * n, 5)
+    want = st.apply(x)
+    got = M @ x
+    assert np.linalg.norm(got - want) <= 1e-10 * np.linalg.norm(want)
+    R = O.build_A_matrix(b, C, eta, om, h, n, cm)
+    _still_works(A, R)
+
+
+def test_default_maxiter_and_restart_follow_the_global_size(op):
+    """scipy's defaults restart = min(20, N) and maxiter = 10 N use the global N = n^2."""
+    A, R, _ = op
+    f = np.ones(A.shape[0], complex)
+    x, info = H.gmres(A, f, rtol=1e-3)
+    xr, infor = scipy.sparse.linalg.gmres(R, f, rtol=1e-3)
+    assert info == infor
+    assert np.linalg.norm(x - xr) <= 1e-6 * np.linalg.norm(xr)

@@ -2,39 +2,84 @@
 
 Runs scipy gmres exactly as code.py:516 calls it (oracle.gmres_reference) twice -- on f and
 on f perturbed by 1e-15 relative -- and prints how far the presid history, the field and the
-true residual drift apart.  Where the reference drifts by more than the 1e-6 contract, no
-implementation can be held to it; DESIGN.md 6 uses this to choose the parity cases.
-usage: python tools/gmres_sensitivity.py [n] [wave_num]
+true residual drift apart, per iteration count K.  Where the reference drifts by more than
+the 1e-6 contract, no implementation can be held to it; DESIGN.md 6 uses this to choose the
+parity horizons of the GPU tests.
+
+usage:
+  python tools/gmres_sensitivity.py [n] [wave_num]                 # c1 medium, all M, K 6/12/30
+  python tools/gmres_sensitivity.py --config 2 --iters 10,20,40,100  # a BASELINE config exactly
 """
+import argparse
 import os
 import sys
+import time
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 from oracle import helmholtz_oracle as O  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 600
-wn = float(sys.argv[2]) if len(sys.argv) > 2 else 12.0
-b, C, al = 12, 81.0, 2.0
-cm = O.init_c1_mat(.5, .5, n)
-om, h, eta = O.problem_params(n, b, wn, al)
-A = O.build_A_matrix(b, C, eta, om, h, n, cm)
-f = O.init_f1_mat(.5, .125, om, n).ravel()
-fp = f * (1 + 1e-15 * np.random.default_rng(1).standard_normal(f.size))
-precs = (("none", None), ("jacobi", O.jacobi_preconditioner(A)),
-         ("sl", O.shifted_laplace_jacobi(b, C, eta, om, h, n, cm, beta=0.5, sweeps=2,
-                                         damping=0.7)[0]))
-print(f"n={n} wave_num={wn}: drift between scipy gmres on f and on f(1 + 1e-15 N(0,1))")
-for name, M in precs:
-    for x0s in (None, 1e-6):
-        for K in (6, 12, 30):
-            x0 = None if x0s is None else x0s * f
-            x1, _, h1, r1 = O.gmres_reference(A, f, M=M, rtol=1e-3, restart=20, maxiter=K,
-                                              x0=None if x0 is None else x0.copy())
-            x2, _, h2, r2 = O.gmres_reference(A, fp, M=M, rtol=1e-3, restart=20, maxiter=K,
-                                              x0=None if x0 is None else x0.copy())
-            print(f"M={name:6s} x0={'0' if x0s is None else '1e-6 f':7s} iters={K:2d}: "
-                  f"presid {np.max(np.abs(h1 - h2) / h1):.1e}  "
-                  f"field {np.linalg.norm(x1 - x2) / np.linalg.norm(x1):.1e}  "
-                  f"true relres {abs(r1 - r2) / r1:.1e}", flush=True)
+# BASELINE.json configs (SURVEY 8d): n, medium, wave_num, preconditioner
+CONFIGS = {1: (128, "const", 8.0, "none"), 2: (1024, "const", 64.0, "jacobi"),
+           3: (4096, "marmousi", 100.0, "sl"), 4: (8192, "const", 256.0, "jacobi")}
+
+
+def medium(kind, n):
+    if kind == "c1":
+        return O.init_c1_mat(.5, .5, n)
+    if kind == "const":
+        return np.ones((n + 2, n + 2))
+    from helmholtz_preconditioner_amd import media  # the seeded Marmousi-like generator
+    return media.marmousi_like_c_mat(n)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("n", nargs="?", type=int, default=600)
+    p.add_argument("wave_num", nargs="?", type=float, default=12.0)
+    p.add_argument("--config", type=int, default=0)
+    p.add_argument("--medium", default="c1")
+    p.add_argument("--precond", default="all")
+    p.add_argument("--iters", default="6,12,30")
+    p.add_argument("--x0", action="store_true", help="also x0 = 1e-6 f")
+    a = p.parse_args()
+    n, med, wn, pcs = a.n, a.medium, a.wave_num, a.precond
+    if a.config:
+        n, med, wn, pcs = CONFIGS[a.config]
+    b, C, al = 12, 81.0, 2.0
+    cm = medium(med, n)
+    om, h, eta = O.problem_params(n, b, wn, al)
+    t0 = time.perf_counter()
+    A = O.build_A_matrix(b, C, eta, om, h, n, cm)
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    fp = f * (1 + 1e-15 * np.random.default_rng(1).standard_normal(f.size))
+    precs = {"none": lambda: None, "jacobi": lambda: O.jacobi_preconditioner(A),
+             "sl": lambda: O.shifted_laplace_jacobi(b, C, eta, om, h, n, cm, beta=0.5, sweeps=2,
+                                                    damping=0.7)[0]}
+    names = list(precs) if pcs == "all" else pcs.split(",")
+    print(f"n={n} medium={med} wave_num={wn} (setup {time.perf_counter() - t0:.1f} s): drift "
+          f"between scipy gmres on f and on f(1 + 1e-15 N(0,1)), rtol=1e-3, restart=20",
+          flush=True)
+    for name in names:
+        M = precs[name]()
+        for x0s in ((None, 1e-6) if a.x0 else (None,)):
+            for K in [int(k) for k in a.iters.split(",")]:
+                x0 = None if x0s is None else x0s * f
+                t0 = time.perf_counter()
+                x1, i1, h1, r1 = O.gmres_reference(A, f, M=M, rtol=1e-3, restart=20, maxiter=K,
+                                                   x0=None if x0 is None else x0.copy())
+                x2, _, h2, r2 = O.gmres_reference(A, fp, M=M, rtol=1e-3, restart=20, maxiter=K,
+                                                  x0=None if x0 is None else x0.copy())
+                m = min(len(h1), len(h2))
+                print(f"M={name:6s} x0={'0' if x0s is None else '1e-6 f':7s} iters={K:3d} "
+                      f"(ran {len(h1)}/{len(h2)}, info {i1}): presid "
+                      f"{np.max(np.abs(h1[:m] - h2[:m]) / h1[:m]):.1e}  field "
+                      f"{np.linalg.norm(x1 - x2) / np.linalg.norm(x1):.1e}  true relres "
+                      f"{abs(r1 - r2) / r1:.1e} (relres {r1:.3e}; {time.perf_counter() - t0:.1f} s)",
+                      flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,29 @@
+#!/bin/bash
+# Round-2 session A: the new tests first (callback abort, RCCL ranks on one GPU, BASELINE-config
+# parity), then the whole GPU suite, smoke and the default bench line.
+# Every GPU step has its own time limit; a fault/abort/timeout stops the session.
+set -u
+TAG=${1:-r02a}
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+fatal() { case $1 in 124|137|134|139) return 0;; *) return 1;; esac; }
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -4 "$OUT/$name.log"
+  if fatal $rc; then echo "FATAL rc=$rc in $name: stopping"; exit $rc; fi
+  return 0
+}
+PYT="python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu"
+step t_errors 200 $PYT tests/test_gpu_errors.py
+step t_rccl 300 $PYT tests/test_gpu_dist.py -k "rccl or uneven or stalled or rehearsal"
+step t_configs 600 $PYT tests/test_gpu_configs.py
+step t_all 900 python -u -m pytest -q -x --timeout 300 --timeout-method thread -m gpu tests \
+  --deselect tests/test_gpu_configs.py
+step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 300 python bench.py
+echo done
