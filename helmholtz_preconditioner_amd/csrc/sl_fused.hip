@@ -199,6 +199,311 @@ __device__ __forceinline__ void sl2_tile(const StencilArgs& a, const int t) {
   __syncthreads();  // LDS reuse by the block's next tile
 }
 
+// sl2_tile with ONE barrier per row instead of two.  Iteration r publishes v row r+1 (the
+// first sweep's W/E input) and z1 row r (the second sweep's, computed one iteration earlier)
+// into the LDS buffers of parity r, then a single barrier, then both stages.  Double buffering
+// makes this safe: a thread writing parity p at iteration r+2 has passed the barrier of r+1,
+// which every thread reaches only after its reads of iteration r.  Same arithmetic: bit-identical.
+template <bool CONSTC, bool NTU, int TPB>
+__device__ __forceinline__ void sl2_tile_1b(const StencilArgs& a, const int t) {
+  constexpr int WO = TPB - 2;  // output columns per strip
+  __shared__ double2 lv[2][TPB + 2];
+  __shared__ double2 lz[2][TPB + 2];
+  const int tx = t % a.tiles_x;
+  const int ty = t / a.tiles_x;
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int n = a.n, nl = a.nl;
+  const int i0 = tx * WO;
+  const int c = i0 + tid - 1;  // this lane's column
+  const bool cin = c >= 0 && c < n;
+  const int cc = min(max(c, 0), n - 1);
+  const bool outl = tid >= 1 && tid <= TPB - 2 && cin;
+  const int rb = __builtin_amdgcn_readfirstlane(a.row_begin + ty * a.row_step);
+  const int re = __builtin_amdgcn_readfirstlane(min(rb + a.rows_per_block, a.row_end));
+  int ie = lane < kWave / 2 ? i0 - 2 : i0 + TPB - 1;
+  const bool lw = tid == 0 && i0 - 2 >= 0;
+  const bool le = tid == TPB - 1 && i0 + TPB - 1 < n;
+  ie = min(max(ie, 0), n - 1);
+  const double2 z2 = make_double2(0.0, 0.0);
+
+  auto rowp = [&](int r) -> const double2* {
+    return r < 0 ? a.halo_lo + (size_t)(r + 2) * n
+                 : (r >= nl ? a.halo_hi + (size_t)(r - nl) * n : a.u + (size_t)r * n);
+  };
+  auto load_v = [&](int r) -> double2 {
+    const double2* p = rowp(r) + cc;
+    if constexpr (NTU)
+      return make_double2(__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y));
+    else
+      return *p;
+  };
+  auto load_in = [&](int r, RowIn& v) {
+    if constexpr (!CONSTC) {
+      const double* q = r < 0 ? a.invc2_halo + (size_t)(r + 2) * n
+                              : (r >= nl ? a.invc2_halo + (size_t)(r - nl + 2) * n
+                                         : a.invc2 + (size_t)r * n);
+      v.ic = __builtin_nontemporal_load(q + cc);
+    } else {
+      v.ic = a.invc2_const;
+    }
+    v.e = rowp(r)[ie];
+  };
+  const cdouble_p tabj = (cdouble_p)(a.tab_j);
+  auto load_tab = [&](int r, RowTab& tb) {
+    const int ru = __builtin_amdgcn_readfirstlane(min(max(r, -2), nl + 1));  // tab_j_ext rows
+    const cdouble_p q = tabj + 8 * ru;
+    tb.R2 = make_double2(q[0], q[1]);
+    tb.BS = make_double2(q[2], q[3]);
+    tb.BN = make_double2(q[4], q[5]);
+    tb.OM = make_double2(q[6], q[7]);
+  };
+  const double2 AW = a.tab_i[cc], AE = a.tab_i[n + cc], R1 = a.tab_i[2 * n + cc];
+  const double sin = a.in_scale ? *a.in_scale : 1.0;
+
+  // v row (centre + the strip's halo columns) into LDS buffer p
+  auto put_v = [&](int p, double2 uC, const RowIn& in) __attribute__((always_inline)) {
+    lv[p][tid + 1] = csel(cin, uC, z2);
+    if (tid == 0) lv[p][0] = csel(lw, in.e, z2);
+    if (tid == TPB - 1) lv[p][TPB + 1] = csel(le, in.e, z2);
+  };
+  // first sweep on row s from LDS buffer p (same arithmetic as sl2_tile's stage1)
+  auto stage1 = [&](int s, int p, double2 uS, double2 uC, double2 uN, const RowIn& in,
+                    const RowTab& tb, double2& T, double2& z1) __attribute__((always_inline)) {
+    const double2 uW = lv[p][tid], uE = lv[p][tid + 2];
+    const double2 W = cmul(AW, tb.R2);
+    const double2 E = cmul(AE, tb.R2);
+    const double2 S = cmul(tb.BS, R1);
+    const double2 N = cmul(tb.BN, R1);
+    const double2 M = cscale(cmul(tb.OM, R1), in.ic);
+    const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
+    const double2 D = csub(M, sum4);
+    const double2 Db = csub(cmul(M, a.mshift), sum4);
+    double2 Au = cmul(S, uS);
+    Au = cfma(W, uW, Au);
+    Au = cfma(D, uC, Au);
+    Au = cfma(E, uE, Au);
+    Au = cfma(N, uN, Au);
+    T = cscale(Au, sin);
+    z1 = csel(cin && a.j0 + s >= 0 && a.j0 + s < n, cscale(cdiv(T, Db), a.damping), z2);
+  };
+  auto stage2 = [&](int p, double2 zS, double2 zC, double2 zN, double2 T, const RowIn& in,
+                    const RowTab& tb) __attribute__((always_inline)) -> double2 {
+    const double2 zW = lz[p][tid], zE = lz[p][tid + 2];
+    const double2 W = cmul(AW, tb.R2);
+    const double2 E = cmul(AE, tb.R2);
+    const double2 S = cmul(tb.BS, R1);
+    const double2 N = cmul(tb.BN, R1);
+    const double2 M = cscale(cmul(tb.OM, R1), in.ic);
+    const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
+    const double2 Db = csub(cmul(M, a.mshift), sum4);
+    double2 Au = cmul(S, zS);
+    Au = cfma(W, zW, Au);
+    Au = cfma(Db, zC, Au);
+    Au = cfma(E, zE, Au);
+    Au = cfma(N, zN, Au);
+    return cadd(zC, cscale(cdiv(csub(T, Au), Db), a.damping));
+  };
+
+  double2 V[4], Z[4], TT[4];
+  RowIn IN[4];
+  RowTab TB[4];
+  if (tid == 0) {  // z1 halo slots: never stored by a lane (outputs there are not written)
+    lz[0][0] = z2;
+    lz[1][0] = z2;
+  }
+  if (tid == TPB - 1) {
+    lz[0][TPB + 1] = z2;
+    lz[1][TPB + 1] = z2;
+  }
+  V[0] = load_v(rb - 2);
+  V[1] = load_v(rb - 1);
+  V[2] = load_v(rb);
+  V[3] = load_v(rb + 1);
+  load_in(rb - 1, IN[1]);
+  load_in(rb, IN[2]);
+  load_in(rb + 1, IN[3]);
+  load_tab(rb - 1, TB[1]);
+  load_tab(rb, TB[2]);
+  load_tab(rb + 1, TB[3]);
+  // prologue: first sweep on rows rb-1 (buffer 1) and rb (buffer 0), one barrier each
+  put_v(1, V[1], IN[1]);
+  __syncthreads();
+  stage1(rb - 1, 1, V[0], V[1], V[2], IN[1], TB[1], TT[1], Z[1]);
+  V[0] = load_v(rb + 2);
+  put_v(0, V[2], IN[2]);
+  __syncthreads();
+  stage1(rb, 0, V[1], V[2], V[3], IN[2], TB[2], TT[2], Z[2]);
+
+  for (int r0 = rb; r0 < re; r0 += 4) {
+    unroll<0, 4>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      constexpr int p = (k + 1) & 1;  // parity of this iteration's buffers
+      const int r = r0 + k;
+      const bool live = r < re;
+      V[(k + 1) & 3] = load_v(min(r + 3, re + 1));
+      load_in(min(r + 2, re), IN[k & 3]);
+      load_tab(min(r + 2, re), TB[k & 3]);
+      put_v(p, V[(k + 3) & 3], IN[(k + 3) & 3]);  // v row r+1
+      lz[p][tid + 1] = Z[(k + 2) & 3];            // z1 row r
+      __syncthreads();
+      stage1(r + 1, p, V[(k + 2) & 3], V[(k + 3) & 3], V[k & 3], IN[(k + 3) & 3],
+             TB[(k + 3) & 3], TT[(k + 3) & 3], Z[(k + 3) & 3]);
+      const double2 w = stage2(p, Z[(k + 1) & 3], Z[(k + 2) & 3], Z[(k + 3) & 3], TT[(k + 2) & 3],
+                               IN[(k + 2) & 3], TB[(k + 2) & 3]);
+      if (outl && live) {
+        double2* q = a.out0 + (size_t)r * n + c;
+        __builtin_nontemporal_store(w.x, &q->x);
+        __builtin_nontemporal_store(w.y, &q->y);
+      }
+    });
+  }
+  __syncthreads();  // LDS reuse by the block's next tile
+}
+
+// Barrier-free form: every WAVE is an independent overlapping strip -- its 64 lanes compute the
+// first sweep on 64 columns and write w on the inner 62 -- so all W/E exchanges are wave
+// shuffles (no LDS, no barrier: a wave never waits for another).  The two v columns beyond the
+// strip come from one broadcast load per row (lanes 0-31: column i0-2, lanes 32-63: i0+63).
+// Costs 64/62 lanes of arithmetic; same per-point arithmetic as sl2_tile: bit-identical.
+template <bool CONSTC, bool NTU>
+__device__ __forceinline__ void sl2_wave(const StencilArgs& a, const int t) {
+  constexpr int WO = kWave - 2;
+  const int wave = threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int n = a.n, nl = a.nl;
+  const int strips = (n + WO - 1) / WO;
+  const int tx = t % a.tiles_x;
+  const int ty = t / a.tiles_x;
+  const int strip = tx * (kStencilThreads / kWave) + wave;
+  if (strip >= strips) return;  // (wave-uniform; no barrier in this shape)
+  const int i0 = strip * WO;
+  const int c = i0 + lane - 1;
+  const bool cin = c >= 0 && c < n;
+  const int cc = min(max(c, 0), n - 1);
+  const bool outl = lane >= 1 && lane <= kWave - 2 && cin;
+  const int rb = __builtin_amdgcn_readfirstlane(a.row_begin + ty * a.row_step);
+  const int re = __builtin_amdgcn_readfirstlane(min(rb + a.rows_per_block, a.row_end));
+  int ie = lane < kWave / 2 ? i0 - 2 : i0 + kWave - 1;
+  const bool lw = lane == 0 && i0 - 2 >= 0;
+  const bool le = lane == kWave - 1 && i0 + kWave - 1 < n;
+  ie = min(max(ie, 0), n - 1);
+  const double2 z2 = make_double2(0.0, 0.0);
+
+  auto rowp = [&](int r) -> const double2* {
+    return r < 0 ? a.halo_lo + (size_t)(r + 2) * n
+                 : (r >= nl ? a.halo_hi + (size_t)(r - nl) * n : a.u + (size_t)r * n);
+  };
+  auto load_v = [&](int r) -> double2 {
+    const double2* p = rowp(r) + cc;
+    if constexpr (NTU)
+      return make_double2(__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y));
+    else
+      return *p;
+  };
+  auto load_in = [&](int r, RowIn& v) {
+    if constexpr (!CONSTC) {
+      const double* q = r < 0 ? a.invc2_halo + (size_t)(r + 2) * n
+                              : (r >= nl ? a.invc2_halo + (size_t)(r - nl + 2) * n
+                                         : a.invc2 + (size_t)r * n);
+      v.ic = __builtin_nontemporal_load(q + cc);
+    } else {
+      v.ic = a.invc2_const;
+    }
+    v.e = rowp(r)[ie];
+  };
+  const cdouble_p tabj = (cdouble_p)(a.tab_j);
+  auto load_tab = [&](int r, RowTab& tb) {
+    const int ru = __builtin_amdgcn_readfirstlane(min(max(r, -2), nl + 1));
+    const cdouble_p q = tabj + 8 * ru;
+    tb.R2 = make_double2(q[0], q[1]);
+    tb.BS = make_double2(q[2], q[3]);
+    tb.BN = make_double2(q[4], q[5]);
+    tb.OM = make_double2(q[6], q[7]);
+  };
+  const double2 AW = a.tab_i[cc], AE = a.tab_i[n + cc], R1 = a.tab_i[2 * n + cc];
+  const double sin = a.in_scale ? *a.in_scale : 1.0;
+  auto shup = [](double2 v) { return make_double2(__shfl_up(v.x, 1), __shfl_up(v.y, 1)); };
+  auto shdn = [](double2 v) { return make_double2(__shfl_down(v.x, 1), __shfl_down(v.y, 1)); };
+
+  auto stage1 = [&](int s, double2 uS, double2 uC, double2 uN, const RowIn& in,
+                    const RowTab& tb, double2& T, double2& z1) __attribute__((always_inline)) {
+    const double2 uCm = csel(cin, uC, z2);
+    const double2 sw = shup(uCm), se = shdn(uCm);
+    const double2 uW = lane == 0 ? csel(lw, in.e, z2) : sw;
+    const double2 uE = lane == kWave - 1 ? csel(le, in.e, z2) : se;
+    const double2 W = cmul(AW, tb.R2);
+    const double2 E = cmul(AE, tb.R2);
+    const double2 S = cmul(tb.BS, R1);
+    const double2 N = cmul(tb.BN, R1);
+    const double2 M = cscale(cmul(tb.OM, R1), in.ic);
+    const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
+    const double2 D = csub(M, sum4);
+    const double2 Db = csub(cmul(M, a.mshift), sum4);
+    double2 Au = cmul(S, uS);
+    Au = cfma(W, uW, Au);
+    Au = cfma(D, uC, Au);
+    Au = cfma(E, uE, Au);
+    Au = cfma(N, uN, Au);
+    T = cscale(Au, sin);
+    z1 = csel(cin && a.j0 + s >= 0 && a.j0 + s < n, cscale(cdiv(T, Db), a.damping), z2);
+  };
+  auto stage2 = [&](double2 zS, double2 zC, double2 zN, double2 T, const RowIn& in,
+                    const RowTab& tb) __attribute__((always_inline)) -> double2 {
+    const double2 zW = shup(zC), zE = shdn(zC);  // (lanes 0 and 63 write no output)
+    const double2 W = cmul(AW, tb.R2);
+    const double2 E = cmul(AE, tb.R2);
+    const double2 S = cmul(tb.BS, R1);
+    const double2 N = cmul(tb.BN, R1);
+    const double2 M = cscale(cmul(tb.OM, R1), in.ic);
+    const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
+    const double2 Db = csub(cmul(M, a.mshift), sum4);
+    double2 Au = cmul(S, zS);
+    Au = cfma(W, zW, Au);
+    Au = cfma(Db, zC, Au);
+    Au = cfma(E, zE, Au);
+    Au = cfma(N, zN, Au);
+    return cadd(zC, cscale(cdiv(csub(T, Au), Db), a.damping));
+  };
+
+  double2 V[4], Z[4], TT[4];
+  RowIn IN[4];
+  RowTab TB[4];
+  V[0] = load_v(rb - 2);
+  V[1] = load_v(rb - 1);
+  V[2] = load_v(rb);
+  V[3] = load_v(rb + 1);
+  load_in(rb - 1, IN[1]);
+  load_in(rb, IN[2]);
+  load_in(rb + 1, IN[3]);
+  load_tab(rb - 1, TB[1]);
+  load_tab(rb, TB[2]);
+  load_tab(rb + 1, TB[3]);
+  stage1(rb - 1, V[0], V[1], V[2], IN[1], TB[1], TT[1], Z[1]);
+  V[0] = load_v(rb + 2);
+  stage1(rb, V[1], V[2], V[3], IN[2], TB[2], TT[2], Z[2]);
+
+  for (int r0 = rb; r0 < re; r0 += 4) {
+    unroll<0, 4>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      const int r = r0 + k;
+      const bool live = r < re;
+      V[(k + 1) & 3] = load_v(min(r + 3, re + 1));
+      load_in(min(r + 2, re), IN[k & 3]);
+      load_tab(min(r + 2, re), TB[k & 3]);
+      stage1(r + 1, V[(k + 2) & 3], V[(k + 3) & 3], V[k & 3], IN[(k + 3) & 3], TB[(k + 3) & 3],
+             TT[(k + 3) & 3], Z[(k + 3) & 3]);
+      const double2 w = stage2(Z[(k + 1) & 3], Z[(k + 2) & 3], Z[(k + 3) & 3], TT[(k + 2) & 3],
+                               IN[(k + 2) & 3], TB[(k + 2) & 3]);
+      if (outl && live) {
+        double2* q = a.out0 + (size_t)r * n + c;
+        __builtin_nontemporal_store(w.x, &q->x);
+        __builtin_nontemporal_store(w.y, &q->y);
+      }
+    });
+  }
+}
+
 // The same fused M A for the 9-point operator, in stencil.hip's separable form
 // term for term (so w is bit-identical to the two-launch path): with X(r) the x second
 // difference of row r, Y(i) the y one of column i and H(r) = u_W + u_E of row r,
@@ -434,7 +739,9 @@ __device__ __forceinline__ void sl2_tile9(const StencilArgs& a, const int t) {
   __syncthreads();  // LDS reuse by the block's next tile
 }
 
-template <bool CONSTC, bool NTU, int TPB, bool S9>
+// SHAPE (5-point): 0 = sl2_tile (two barriers per row), 1 = sl2_tile_1b (one barrier per row),
+// 2 = sl2_wave (wave strips, no barrier).  The 9-point operator has sl2_tile9 only.
+template <bool CONSTC, bool NTU, int TPB, bool S9, int SHAPE = 0>
 __global__ __launch_bounds__(TPB) void sl2_kernel(const StencilArgs a) {
   if (a.stop && *a.stop) return;  // queued GMRES cycle already stopped
   const int L = blockIdx.x;
@@ -444,19 +751,21 @@ __global__ __launch_bounds__(TPB) void sl2_kernel(const StencilArgs a) {
     const int t = (L & 7) * a.tiles_per_xcd + tt;
     if (t >= ntiles) break;  // uniform per block
     if constexpr (S9) sl2_tile9<CONSTC, NTU, TPB>(a, t);
+    else if constexpr (SHAPE == 1) sl2_tile_1b<CONSTC, NTU, TPB>(a, t);
+    else if constexpr (SHAPE == 2) sl2_wave<CONSTC, NTU>(a, t);
     else sl2_tile<CONSTC, NTU, TPB>(a, t);
   }
 }
 
-template <int TPB, bool NTU>
+template <int TPB, bool NTU, int SHAPE = 0>
 void launch_t(bool const_c, const StencilArgs& a, int blocks, hipStream_t s) {
   const bool s9 = a.tab_r2x != nullptr;  // 9-point operator (the tables themselves are unused)
   if (const_c) {
     if (s9) hipLaunchKernelGGL((sl2_kernel<true, NTU, TPB, true>), dim3(blocks), dim3(TPB), 0, s, a);
-    else hipLaunchKernelGGL((sl2_kernel<true, NTU, TPB, false>), dim3(blocks), dim3(TPB), 0, s, a);
+    else hipLaunchKernelGGL((sl2_kernel<true, NTU, TPB, false, SHAPE>), dim3(blocks), dim3(TPB), 0, s, a);
   } else {
     if (s9) hipLaunchKernelGGL((sl2_kernel<false, NTU, TPB, true>), dim3(blocks), dim3(TPB), 0, s, a);
-    else hipLaunchKernelGGL((sl2_kernel<false, NTU, TPB, false>), dim3(blocks), dim3(TPB), 0, s, a);
+    else hipLaunchKernelGGL((sl2_kernel<false, NTU, TPB, false, SHAPE>), dim3(blocks), dim3(TPB), 0, s, a);
   }
 }
 
@@ -471,17 +780,35 @@ void launch_sl2(bool const_c, const StencilArgs& a_in, hipStream_t stream, int v
   // picks the strip width (>= 24: 512) and NT v loads (% 24 >= 12)
   int tpb = 256;
   bool ntu = n <= 4608;
+  int shape = 0;
   if (variant == 6 || variant == 18 || variant == 30 || variant == 42) {
     tpb = variant >= 24 ? 512 : 256;
     ntu = variant % 24 >= 12;
+  } else if (sl2_variant(variant)) {  // kSl2Variant + shape (1, 2) + 4 NT v loads
+    shape = (variant - kSl2Variant) & 3;
+    ntu = ((variant - kSl2Variant) & 4) != 0;
   }
+  if (a.tab_r2x) shape = 0;  // the 9-point operator has the LDS marching shape only
   const int rows = a.row_end - a.row_begin;
   if (a.row_step <= 0) a.row_step = a.rows_per_block;  // (> 0: spaced boundary bands)
-  a.tiles_x = (n + (tpb - 2) - 1) / (tpb - 2);
+  // output columns per tile: TPB - 2 (strip shapes) or 4 wave strips of 62 (shape 2)
+  const int wo = shape == 2 ? (kWave - 2) * (kStencilThreads / kWave) : tpb - 2;
+  if (shape == 2) {
+    const int strips = (n + kWave - 3) / (kWave - 2);
+    a.tiles_x = (strips + 3) / 4;
+  } else {
+    a.tiles_x = (n + wo - 1) / wo;
+  }
   a.tiles_y = stencil_bands(rows, a.rows_per_block, a.row_step);
   a.tiles_per_xcd = (a.tiles_x * a.tiles_y + 7) / 8;
   const int blocks = a.tiles_per_xcd * 8;
-  if (tpb == 256) {
+  if (shape == 1) {
+    if (ntu) launch_t<256, true, 1>(const_c, a, blocks, stream);
+    else launch_t<256, false, 1>(const_c, a, blocks, stream);
+  } else if (shape == 2) {
+    if (ntu) launch_t<256, true, 2>(const_c, a, blocks, stream);
+    else launch_t<256, false, 2>(const_c, a, blocks, stream);
+  } else if (tpb == 256) {
     if (ntu) launch_t<256, true>(const_c, a, blocks, stream);
     else launch_t<256, false>(const_c, a, blocks, stream);
   } else {

@@ -806,7 +806,7 @@ int stencil_resolve_variant(int epi, int requested, int n) {
   if (n < 2048) autov = epi == EPI_AX ? kSmallCachedVariant : kSmallVariant;
   else if (epi != EPI_AX && n <= kLongRow) autov = kSolveVariant;
   else if (epi == EPI_AX && requested != kVariantInSolve) autov = kTileDefault;
-  if (requested < 0) return autov;
+  if (requested < 0 || sl2_variant(requested)) return autov;
   if (epi == EPI_AX) return stencil_variant_valid(requested) ? requested : autov;
   if (epi == EPI_JAC && requested >= kTileVariant && stencil_variant_valid(requested))
     return requested;  // the tile shape has the Jacobi-fused apply too
@@ -831,7 +831,7 @@ int stencil_grid_blocks(int n, int rows, int rows_per_block, int row_step) {
 
 int stencil_default_variant() { return kDefaultVariant; }
 bool stencil_variant_valid(int v) {
-  return (v >= 0 && v <= 27) || (v >= 30 && v <= 33) || (v >= 42 && v <= 45) ||
+  return (v >= 0 && v <= 27) || (v >= 30 && v <= 33) || (v >= 42 && v <= 45) || sl2_variant(v) ||
          (v >= kTileVariant && v < kTileVariant + 64 && tile_variant_known(v));
 }
 

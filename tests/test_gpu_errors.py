@@ -176,7 +176,14 @@ def test_default_maxiter_and_restart_follow_the_global_size(op):
     """scipy's defaults restart = min(20, N) and maxiter = 10 N use the global N = n^2."""
     A, R, _ = op
     f = np.ones(A.shape[0], complex)
-    x, info = H.gmres(A, f, rtol=1e-3)
-    xr, infor = scipy.sparse.linalg.gmres(R, f, rtol=1e-3)
-    assert info == infor
-    assert np.linalg.norm(x - xr) <= 1e-6 * np.linalg.norm(xr)
+    c, cr = [], []
+    x, info = H.gmres(A, f, rtol=1e-3, callback=c.append, callback_type="legacy")
+    xr, infor = scipy.sparse.linalg.gmres(R, f, rtol=1e-3, callback=cr.append,
+                                          callback_type="legacy")
+    # this solve runs for hundreds of iterations, far past the horizon where scipy's own run is
+    # reproducible to 1e-6 (DESIGN 6): both must converge the same way, not bit for bit
+    assert info == infor == 0 and abs(len(c) - len(cr)) <= 2, (len(c), len(cr))
+    for u in (x, xr):
+        assert np.linalg.norm(f - R @ u) <= 1e-3 * np.linalg.norm(f)
+    assert np.linalg.norm(x - xr) <= 1e-3 * np.linalg.norm(xr)
+    np.testing.assert_allclose(c[:10], cr[:10], rtol=1e-6)

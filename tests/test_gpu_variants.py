@@ -226,3 +226,44 @@ def test_fused_shifted_laplace_on_slabs(slabs, stencil):
         outs.append(A._apply_host(x, H._ffi.HH_APPLY_PREC_A))
     for y in outs[1:]:
         np.testing.assert_array_equal(y, outs[0])
+
+
+SL2_SHAPES = [160, 161, 162, 164, 165, 166]  # kSl2Variant + shape (0/1/2) + 4 (NT v loads)
+
+
+@pytest.mark.parametrize("n,kind,rpb,slabs", [(97, "c2", 0, 1), (700, "c1", 13, 1),
+                                              (1100, "const", 0, 1), (2100, "c1", 0, 1),
+                                              (301, "c1", 0, 3), (63, "c1", 0, 1),
+                                              (125, "c2", 5, 2)])
+def test_fused_shifted_laplace_shapes_bit_identical(n, kind, rpb, slabs):
+    """Every shape of the fused M A (two barriers per row, one barrier per row, barrier-free
+    wave strips of 62 columns; cached / NT v loads) gives the two-launch path's result bit for
+    bit: ragged n (strip counts not a multiple of 4, rows shorter than a wave strip), odd band
+    heights, virtual slabs."""
+    b, C, wn = 12, 81.0, 10.0
+    om, h, eta = O.problem_params(n, b, wn, 2.0)
+    cm = medium(kind, n)
+    c = H.Context(device=0, virtual_slabs=slabs)
+    A = H.build_A_matrix(b, C, eta, om, h, n, cm, context=c)
+    M = H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7)
+    x = rand_complex(n * n, 21)
+    A.sl_fusion(False)
+    M.configure()
+    ref = A._apply_host(x, H._ffi.HH_APPLY_PREC_A)
+    A.sl_fusion(True)
+    for v in SL2_SHAPES:
+        A.tune(v, rpb, 0)
+        M.configure()
+        np.testing.assert_array_equal(A._apply_host(x, H._ffi.HH_APPLY_PREC_A), ref, err_msg=str(v))
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    out = []
+    for v in (-1, 162, 165):
+        A.tune(v, rpb, 0)
+        xs, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=12, M=M,
+                                 callback=lambda r: None, callback_type="legacy",
+                                 return_history=True)
+        out.append((xs, hist))
+    A.tune(-1, 0, 0)
+    for xs, hist in out[1:]:
+        np.testing.assert_array_equal(hist, out[0][1])
+        np.testing.assert_array_equal(xs, out[0][0])
