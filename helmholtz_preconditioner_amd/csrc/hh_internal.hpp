@@ -35,10 +35,12 @@ enum XMode : int { XM_LDS = 0, XM_DIRECT = 1, XM_SHFL = 2 };
 // kernel (plain and Jacobi-fused apply; stencil.hip, tile_kernel / tile9_kernel).
 constexpr int kNumVariants = 48;
 // Shapes of the fused two-sweep shifted-Laplace M A (sl_fused.hip, hh_op_tune): kSl2Variant +
-// shape (0: two barriers per row, 1: one barrier per row, 2: barrier-free wave strips) + 4 (NT v
-// loads).  The plain stencil launches ignore them (they take their default shape).
+// shape (0: two barriers per row, 1: one barrier per row, 2: barrier-free wave strips, 3:
+// sl2_tile_v2) + 4 (NT v
+// loads; shape 3: one barrier per row, LDS tables, mask-free interior tiles).  The plain stencil
+// launches ignore them (they take their default shape).
 constexpr int kSl2Variant = 160;
-constexpr bool sl2_variant(int v) { return v >= kSl2Variant && v < kSl2Variant + 8 && (v & 3) != 3; }
+constexpr bool sl2_variant(int v) { return v >= kSl2Variant && v < kSl2Variant + 8; }
 
 // Pointwise (no-neighbour) operations that need only the diagonal.
 enum PointOp : int {

@@ -268,8 +268,13 @@ __device__ __forceinline__ void sl2_tile_1b(const StencilArgs& a, const int t) {
     if (tid == TPB - 1) lv[p][TPB + 1] = csel(le, in.e, z2);
   };
   // first sweep on row s from LDS buffer p (same arithmetic as sl2_tile's stage1)
+  // The shifted diagonal Db of a row and the reciprocal 1/|Db|^2 of cdiv (hh_complex.hpp) are
+  // formed once, by the first sweep, and kept for the second sweep on the same row one
+  // iteration later: the same values cdiv would recompute, so the result is unchanged bit for
+  // bit, with one IEEE division per point instead of two and no second mass term.
   auto stage1 = [&](int s, int p, double2 uS, double2 uC, double2 uN, const RowIn& in,
-                    const RowTab& tb, double2& T, double2& z1) __attribute__((always_inline)) {
+                    const RowTab& tb, double2& T, double2& z1, double2& Dbo, double& invo)
+      __attribute__((always_inline)) {
     const double2 uW = lv[p][tid], uE = lv[p][tid + 2];
     const double2 W = cmul(AW, tb.R2);
     const double2 E = cmul(AE, tb.R2);
@@ -285,27 +290,33 @@ __device__ __forceinline__ void sl2_tile_1b(const StencilArgs& a, const int t) {
     Au = cfma(E, uE, Au);
     Au = cfma(N, uN, Au);
     T = cscale(Au, sin);
-    z1 = csel(cin && a.j0 + s >= 0 && a.j0 + s < n, cscale(cdiv(T, Db), a.damping), z2);
+    const double inv = 1.0 / fma(Db.x, Db.x, Db.y * Db.y);  // = cdiv(T, Db), split
+    const double2 q = make_double2(fma(T.x, Db.x, T.y * Db.y) * inv,
+                                   fma(T.y, Db.x, -T.x * Db.y) * inv);
+    z1 = csel(cin && a.j0 + s >= 0 && a.j0 + s < n, cscale(q, a.damping), z2);
+    Dbo = Db;
+    invo = inv;
   };
-  auto stage2 = [&](int p, double2 zS, double2 zC, double2 zN, double2 T, const RowIn& in,
+  auto stage2 = [&](int p, double2 zS, double2 zC, double2 zN, double2 T, double2 Db, double inv,
                     const RowTab& tb) __attribute__((always_inline)) -> double2 {
     const double2 zW = lz[p][tid], zE = lz[p][tid + 2];
     const double2 W = cmul(AW, tb.R2);
     const double2 E = cmul(AE, tb.R2);
     const double2 S = cmul(tb.BS, R1);
     const double2 N = cmul(tb.BN, R1);
-    const double2 M = cscale(cmul(tb.OM, R1), in.ic);
-    const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
-    const double2 Db = csub(cmul(M, a.mshift), sum4);
     double2 Au = cmul(S, zS);
     Au = cfma(W, zW, Au);
     Au = cfma(Db, zC, Au);
     Au = cfma(E, zE, Au);
     Au = cfma(N, zN, Au);
-    return cadd(zC, cscale(cdiv(csub(T, Au), Db), a.damping));
+    const double2 d = csub(T, Au);
+    const double2 q = make_double2(fma(d.x, Db.x, d.y * Db.y) * inv,
+                                   fma(d.y, Db.x, -d.x * Db.y) * inv);
+    return cadd(zC, cscale(q, a.damping));
   };
 
-  double2 V[4], Z[4], TT[4];
+  double2 V[4], Z[4], TT[4], DB[4];
+  double INV[4];
   RowIn IN[4];
   RowTab TB[4];
   if (tid == 0) {  // z1 halo slots: never stored by a lane (outputs there are not written)
@@ -329,11 +340,11 @@ __device__ __forceinline__ void sl2_tile_1b(const StencilArgs& a, const int t) {
   // prologue: first sweep on rows rb-1 (buffer 1) and rb (buffer 0), one barrier each
   put_v(1, V[1], IN[1]);
   __syncthreads();
-  stage1(rb - 1, 1, V[0], V[1], V[2], IN[1], TB[1], TT[1], Z[1]);
+  stage1(rb - 1, 1, V[0], V[1], V[2], IN[1], TB[1], TT[1], Z[1], DB[1], INV[1]);
   V[0] = load_v(rb + 2);
   put_v(0, V[2], IN[2]);
   __syncthreads();
-  stage1(rb, 0, V[1], V[2], V[3], IN[2], TB[2], TT[2], Z[2]);
+  stage1(rb, 0, V[1], V[2], V[3], IN[2], TB[2], TT[2], Z[2], DB[2], INV[2]);
 
   for (int r0 = rb; r0 < re; r0 += 4) {
     unroll<0, 4>([&](auto kc) {
@@ -348,9 +359,188 @@ __device__ __forceinline__ void sl2_tile_1b(const StencilArgs& a, const int t) {
       lz[p][tid + 1] = Z[(k + 2) & 3];            // z1 row r
       __syncthreads();
       stage1(r + 1, p, V[(k + 2) & 3], V[(k + 3) & 3], V[k & 3], IN[(k + 3) & 3],
-             TB[(k + 3) & 3], TT[(k + 3) & 3], Z[(k + 3) & 3]);
+             TB[(k + 3) & 3], TT[(k + 3) & 3], Z[(k + 3) & 3], DB[(k + 3) & 3], INV[(k + 3) & 3]);
       const double2 w = stage2(p, Z[(k + 1) & 3], Z[(k + 2) & 3], Z[(k + 3) & 3], TT[(k + 2) & 3],
-                               IN[(k + 2) & 3], TB[(k + 2) & 3]);
+                               DB[(k + 2) & 3], INV[(k + 2) & 3], TB[(k + 2) & 3]);
+      if (outl && live) {
+        double2* q = a.out0 + (size_t)r * n + c;
+        __builtin_nontemporal_store(w.x, &q->x);
+        __builtin_nontemporal_store(w.y, &q->y);
+      }
+    });
+  }
+  __syncthreads();  // LDS reuse by the block's next tile
+}
+
+// sl2_tile_1b with the instruction count cut (the kernel is VALU-issue-bound: ~200 vector
+// instructions per point-row against ~80 for the plain stencil):
+//  * the band's PML row tables (rows rb-2 .. re+1) are staged in LDS once per tile and read
+//    with broadcast ds_read_b128 right before use -- no four-row ring of table values in SGPRs
+//    (which spilled to VGPR lanes: ~130 v_readlane / v_writelane per four rows);
+//  * Db and 1/|Db|^2 of a row come from its first sweep into the second (one division per
+//    point, no second mass term) -- the values cdiv would recompute, so nothing changes;
+//  * tiles whose columns and rows all lie on the grid (all but the strips at the two side
+//    edges and the bands at the top / bottom of the grid) skip every mask (EDGE = false).
+// Same arithmetic, term for term: bit-identical to the two-launch path.
+constexpr int kSl2MaxBand = 60;  // band rows per tile for this shape (LDS table capacity)
+struct Sl2Lds {  // one LDS block shared by both instantiations of sl2_tile_v2
+  double2 lv[2][kStencilThreads + 2];
+  double2 lz[2][kStencilThreads + 2];
+  double2 ltab[kSl2MaxBand + 4][4];
+};
+template <bool CONSTC, bool NTU, bool EDGE>
+__device__ __forceinline__ void sl2_tile_v2(const StencilArgs& a, const int t, Sl2Lds& L) {
+  constexpr int TPB = kStencilThreads;
+  constexpr int WO = TPB - 2;
+  auto& lv = L.lv;
+  auto& lz = L.lz;
+  auto& ltab = L.ltab;
+  const int tx = t % a.tiles_x;
+  const int ty = t / a.tiles_x;
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int n = a.n, nl = a.nl;
+  const int i0 = tx * WO;
+  const int c = i0 + tid - 1;
+  const bool cin = !EDGE || (c >= 0 && c < n);
+  const int cc = EDGE ? min(max(c, 0), n - 1) : c;
+  const bool outl = tid >= 1 && tid <= TPB - 2 && cin;
+  const int rb = __builtin_amdgcn_readfirstlane(a.row_begin + ty * a.row_step);
+  const int re = __builtin_amdgcn_readfirstlane(min(rb + a.rows_per_block, a.row_end));
+  int ie = lane < kWave / 2 ? i0 - 2 : i0 + TPB - 1;
+  const bool lw = !EDGE || i0 - 2 >= 0;
+  const bool le = !EDGE || i0 + TPB - 1 < n;
+  if constexpr (EDGE) ie = min(max(ie, 0), n - 1);
+  const double2 z2 = make_double2(0.0, 0.0);
+
+  auto rowp = [&](int r) -> const double2* {
+    return r < 0 ? a.halo_lo + (size_t)(r + 2) * n
+                 : (r >= nl ? a.halo_hi + (size_t)(r - nl) * n : a.u + (size_t)r * n);
+  };
+  auto load_v = [&](int r) -> double2 {
+    const double2* p = rowp(r) + cc;
+    if constexpr (NTU)
+      return make_double2(__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y));
+    else
+      return *p;
+  };
+  auto load_in = [&](int r, RowIn& v) {
+    if constexpr (!CONSTC) {
+      const double* q = r < 0 ? a.invc2_halo + (size_t)(r + 2) * n
+                              : (r >= nl ? a.invc2_halo + (size_t)(r - nl + 2) * n
+                                         : a.invc2 + (size_t)r * n);
+      v.ic = __builtin_nontemporal_load(q + cc);
+    } else {
+      v.ic = a.invc2_const;
+    }
+    v.e = rowp(r)[ie];
+  };
+  // PML row tables of the band (tab_j_ext rows rb-2 .. re+1) into LDS
+  {
+    const int cnt = (re - rb + 4) * 4;
+    for (int k = tid; k < cnt; k += TPB) {
+      const int rr = min(rb - 2 + k / 4, nl + 1);
+      (&ltab[0][0])[k] = a.tab_j[4 * rr + (k & 3)];
+    }
+  }
+  auto tab = [&](int r) -> const double2* { return ltab[r - rb + 2]; };
+  const double2 AW = a.tab_i[cc], AE = a.tab_i[n + cc], R1 = a.tab_i[2 * n + cc];
+  const double sin = a.in_scale ? *a.in_scale : 1.0;
+
+  auto put_v = [&](int p, double2 uC, const RowIn& in) __attribute__((always_inline)) {
+    lv[p][tid + 1] = EDGE ? csel(cin, uC, z2) : uC;
+    if (tid == 0) lv[p][0] = EDGE ? csel(lw, in.e, z2) : in.e;
+    if (tid == TPB - 1) lv[p][TPB + 1] = EDGE ? csel(le, in.e, z2) : in.e;
+  };
+  auto stage1 = [&](int s, int p, double2 uS, double2 uC, double2 uN, const RowIn& in,
+                    double2& T, double2& z1, double2& Dbo, double& invo)
+      __attribute__((always_inline)) {
+    const double2* tb = tab(s);
+    const double2 R2 = tb[0], BS = tb[1], BN = tb[2], OM = tb[3];
+    const double2 uW = lv[p][tid], uE = lv[p][tid + 2];
+    const double2 W = cmul(AW, R2);
+    const double2 E = cmul(AE, R2);
+    const double2 S = cmul(BS, R1);
+    const double2 N = cmul(BN, R1);
+    const double2 M = cscale(cmul(OM, R1), in.ic);
+    const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
+    const double2 D = csub(M, sum4);
+    const double2 Db = csub(cmul(M, a.mshift), sum4);
+    double2 Au = cmul(S, uS);
+    Au = cfma(W, uW, Au);
+    Au = cfma(D, uC, Au);
+    Au = cfma(E, uE, Au);
+    Au = cfma(N, uN, Au);
+    T = cscale(Au, sin);
+    const double inv = 1.0 / fma(Db.x, Db.x, Db.y * Db.y);  // = cdiv(T, Db), split
+    const double2 q = cscale(make_double2(fma(T.x, Db.x, T.y * Db.y) * inv,
+                                          fma(T.y, Db.x, -T.x * Db.y) * inv), a.damping);
+    if constexpr (EDGE) z1 = csel(cin && a.j0 + s >= 0 && a.j0 + s < n, q, z2);
+    else z1 = q;
+    Dbo = Db;
+    invo = inv;
+  };
+  auto stage2 = [&](int r, int p, double2 zS, double2 zC, double2 zN, double2 T, double2 Db,
+                    double inv) __attribute__((always_inline)) -> double2 {
+    const double2* tb = tab(r);
+    const double2 R2 = tb[0], BS = tb[1], BN = tb[2];
+    const double2 zW = lz[p][tid], zE = lz[p][tid + 2];
+    const double2 W = cmul(AW, R2);
+    const double2 E = cmul(AE, R2);
+    const double2 S = cmul(BS, R1);
+    const double2 N = cmul(BN, R1);
+    double2 Au = cmul(S, zS);
+    Au = cfma(W, zW, Au);
+    Au = cfma(Db, zC, Au);
+    Au = cfma(E, zE, Au);
+    Au = cfma(N, zN, Au);
+    const double2 d = csub(T, Au);
+    const double2 q = make_double2(fma(d.x, Db.x, d.y * Db.y) * inv,
+                                   fma(d.y, Db.x, -d.x * Db.y) * inv);
+    return cadd(zC, cscale(q, a.damping));
+  };
+
+  double2 V[4], Z[4], TT[4], DB[4];
+  double INV[4];
+  RowIn IN[4];
+  if (tid == 0) {
+    lz[0][0] = z2;
+    lz[1][0] = z2;
+  }
+  if (tid == TPB - 1) {
+    lz[0][TPB + 1] = z2;
+    lz[1][TPB + 1] = z2;
+  }
+  V[0] = load_v(rb - 2);
+  V[1] = load_v(rb - 1);
+  V[2] = load_v(rb);
+  V[3] = load_v(rb + 1);
+  load_in(rb - 1, IN[1]);
+  load_in(rb, IN[2]);
+  load_in(rb + 1, IN[3]);
+  put_v(1, V[1], IN[1]);
+  __syncthreads();  // (also publishes the table rows)
+  stage1(rb - 1, 1, V[0], V[1], V[2], IN[1], TT[1], Z[1], DB[1], INV[1]);
+  V[0] = load_v(rb + 2);
+  put_v(0, V[2], IN[2]);
+  __syncthreads();
+  stage1(rb, 0, V[1], V[2], V[3], IN[2], TT[2], Z[2], DB[2], INV[2]);
+
+  for (int r0 = rb; r0 < re; r0 += 4) {
+    unroll<0, 4>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      constexpr int p = (k + 1) & 1;
+      const int r = r0 + k;
+      const bool live = r < re;
+      V[(k + 1) & 3] = load_v(min(r + 3, re + 1));
+      load_in(min(r + 2, re), IN[k & 3]);
+      put_v(p, V[(k + 3) & 3], IN[(k + 3) & 3]);  // v row r+1
+      lz[p][tid + 1] = Z[(k + 2) & 3];            // z1 row r
+      __syncthreads();
+      stage1(min(r + 1, re), p, V[(k + 2) & 3], V[(k + 3) & 3], V[k & 3], IN[(k + 3) & 3],
+             TT[(k + 3) & 3], Z[(k + 3) & 3], DB[(k + 3) & 3], INV[(k + 3) & 3]);
+      const double2 w = stage2(min(r, re), p, Z[(k + 1) & 3], Z[(k + 2) & 3], Z[(k + 3) & 3],
+                               TT[(k + 2) & 3], DB[(k + 2) & 3], INV[(k + 2) & 3]);
       if (outl && live) {
         double2* q = a.out0 + (size_t)r * n + c;
         __builtin_nontemporal_store(w.x, &q->x);
@@ -740,7 +930,8 @@ __device__ __forceinline__ void sl2_tile9(const StencilArgs& a, const int t) {
 }
 
 // SHAPE (5-point): 0 = sl2_tile (two barriers per row), 1 = sl2_tile_1b (one barrier per row),
-// 2 = sl2_wave (wave strips, no barrier).  The 9-point operator has sl2_tile9 only.
+// 2 = sl2_wave (wave strips, no barrier), 3 = sl2_tile_v2 (one barrier, LDS tables, mask-free
+// interior tiles).  The 9-point operator has sl2_tile9 only.
 template <bool CONSTC, bool NTU, int TPB, bool S9, int SHAPE = 0>
 __global__ __launch_bounds__(TPB) void sl2_kernel(const StencilArgs a) {
   if (a.stop && *a.stop) return;  // queued GMRES cycle already stopped
@@ -753,6 +944,19 @@ __global__ __launch_bounds__(TPB) void sl2_kernel(const StencilArgs a) {
     if constexpr (S9) sl2_tile9<CONSTC, NTU, TPB>(a, t);
     else if constexpr (SHAPE == 1) sl2_tile_1b<CONSTC, NTU, TPB>(a, t);
     else if constexpr (SHAPE == 2) sl2_wave<CONSTC, NTU>(a, t);
+    else if constexpr (SHAPE == 3) {
+      // interior tile: every column c = i0-1 .. i0+TPB-2 (+ the halo columns) and every first-
+      // sweep row rb-1 .. re on the grid -> the mask-free instantiation (block-uniform branch)
+      const int tx = t % a.tiles_x, ty = t / a.tiles_x;
+      const int i0 = tx * (TPB - 2);
+      const int rb = a.row_begin + ty * a.row_step;
+      const int re = min(rb + a.rows_per_block, a.row_end);
+      const bool interior = i0 - 2 >= 0 && i0 + TPB - 1 < a.n && a.j0 + rb - 1 >= 0 &&
+                            a.j0 + re < a.n;
+      __shared__ Sl2Lds lds;
+      if (interior) sl2_tile_v2<CONSTC, NTU, false>(a, t, lds);
+      else sl2_tile_v2<CONSTC, NTU, true>(a, t, lds);
+    }
     else sl2_tile<CONSTC, NTU, TPB>(a, t);
   }
 }
@@ -790,6 +994,11 @@ void launch_sl2(bool const_c, const StencilArgs& a_in, hipStream_t stream, int v
   }
   if (a.tab_r2x) shape = 0;  // the 9-point operator has the LDS marching shape only
   const int rows = a.row_end - a.row_begin;
+  if (shape == 3 && a.rows_per_block > kSl2MaxBand) {  // LDS table capacity of the shape
+    if (a.row_step == a.rows_per_block) a.row_step = kSl2MaxBand;
+    if (a.row_step <= 0 || a.row_step > kSl2MaxBand) shape = 1;  // (spaced bands: keep)
+    else a.rows_per_block = kSl2MaxBand;
+  }
   if (a.row_step <= 0) a.row_step = a.rows_per_block;  // (> 0: spaced boundary bands)
   // output columns per tile: TPB - 2 (strip shapes) or 4 wave strips of 62 (shape 2)
   const int wo = shape == 2 ? (kWave - 2) * (kStencilThreads / kWave) : tpb - 2;
@@ -805,6 +1014,9 @@ void launch_sl2(bool const_c, const StencilArgs& a_in, hipStream_t stream, int v
   if (shape == 1) {
     if (ntu) launch_t<256, true, 1>(const_c, a, blocks, stream);
     else launch_t<256, false, 1>(const_c, a, blocks, stream);
+  } else if (shape == 3) {
+    if (ntu) launch_t<256, true, 3>(const_c, a, blocks, stream);
+    else launch_t<256, false, 3>(const_c, a, blocks, stream);
   } else if (shape == 2) {
     if (ntu) launch_t<256, true, 2>(const_c, a, blocks, stream);
     else launch_t<256, false, 2>(const_c, a, blocks, stream);
