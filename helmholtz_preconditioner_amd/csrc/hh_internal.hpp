@@ -40,7 +40,9 @@ constexpr int kNumVariants = 48;
 // loads; shape 3: one barrier per row, LDS tables, mask-free interior tiles).  The plain stencil
 // launches ignore them (they take their default shape).
 constexpr int kSl2Variant = 160;
-constexpr bool sl2_variant(int v) { return v >= kSl2Variant && v < kSl2Variant + 8; }
+constexpr bool sl2_variant(int v) {  // (+ 8: prefetch distance 2, shape 3 only)
+  return v >= kSl2Variant && v < kSl2Variant + 16 && (v < kSl2Variant + 8 || (v & 3) == 3);
+}
 
 // Pointwise (no-neighbour) operations that need only the diagonal.
 enum PointOp : int {

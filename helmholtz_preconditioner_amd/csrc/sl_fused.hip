@@ -388,8 +388,11 @@ struct Sl2Lds {  // one LDS block shared by both instantiations of sl2_tile_v2
   double2 lz[2][kStencilThreads + 2];
   double2 ltab[kSl2MaxBand + 4][4];
 };
-template <bool CONSTC, bool NTU, bool EDGE>
+// PF: rows of prefetch distance of the v and 1/c^2 streams (1, or 2 with rings of 8 and the
+// row loop unrolled by 8): more bytes in flight per wave.
+template <bool CONSTC, bool NTU, bool EDGE, int PF>
 __device__ __forceinline__ void sl2_tile_v2(const StencilArgs& a, const int t, Sl2Lds& L) {
+  constexpr int RS = PF == 1 ? 4 : 8;  // ring slots: slot(row) = (row - rb + 2) % RS
   constexpr int TPB = kStencilThreads;
   constexpr int WO = TPB - 2;
   auto& lv = L.lv;
@@ -500,9 +503,9 @@ __device__ __forceinline__ void sl2_tile_v2(const StencilArgs& a, const int t, S
     return cadd(zC, cscale(q, a.damping));
   };
 
-  double2 V[4], Z[4], TT[4], DB[4];
-  double INV[4];
-  RowIn IN[4];
+  double2 V[RS], Z[RS], TT[RS], DB[RS];
+  double INV[RS];
+  RowIn IN[RS];
   if (tid == 0) {
     lz[0][0] = z2;
     lz[1][0] = z2;
@@ -511,36 +514,39 @@ __device__ __forceinline__ void sl2_tile_v2(const StencilArgs& a, const int t, S
     lz[0][TPB + 1] = z2;
     lz[1][TPB + 1] = z2;
   }
-  V[0] = load_v(rb - 2);
-  V[1] = load_v(rb - 1);
-  V[2] = load_v(rb);
-  V[3] = load_v(rb + 1);
-  load_in(rb - 1, IN[1]);
-  load_in(rb, IN[2]);
-  load_in(rb + 1, IN[3]);
+  // rows rb-2 .. rb+1+PF of v and rb-1 .. rb+PF of 1/c^2 (slot = row - rb + 2)
+  unroll<0, 4 + PF>([&](auto kc) {
+    constexpr int m = decltype(kc)::value;
+    V[m] = load_v(min(rb - 2 + m, re + 1));
+  });
+  unroll<1, 2 + PF + 1>([&](auto kc) {
+    constexpr int m = decltype(kc)::value;
+    load_in(min(rb - 2 + m, re), IN[m]);
+  });
   put_v(1, V[1], IN[1]);
   __syncthreads();  // (also publishes the table rows)
   stage1(rb - 1, 1, V[0], V[1], V[2], IN[1], TT[1], Z[1], DB[1], INV[1]);
-  V[0] = load_v(rb + 2);
   put_v(0, V[2], IN[2]);
   __syncthreads();
   stage1(rb, 0, V[1], V[2], V[3], IN[2], TT[2], Z[2], DB[2], INV[2]);
 
-  for (int r0 = rb; r0 < re; r0 += 4) {
-    unroll<0, 4>([&](auto kc) {
+  for (int r0 = rb; r0 < re; r0 += RS) {
+    unroll<0, RS>([&](auto kc) {
       constexpr int k = decltype(kc)::value;
       constexpr int p = (k + 1) & 1;
+      // slot of row r + d at iteration k
+      constexpr int s0 = (k + 2) % RS, s1 = (k + 3) % RS, s2 = (k + 4) % RS;
+      constexpr int sm1 = (k + 1) % RS;
+      constexpr int sv = (k + 4 + PF) % RS, si = (k + 3 + PF) % RS;
       const int r = r0 + k;
       const bool live = r < re;
-      V[(k + 1) & 3] = load_v(min(r + 3, re + 1));
-      load_in(min(r + 2, re), IN[k & 3]);
-      put_v(p, V[(k + 3) & 3], IN[(k + 3) & 3]);  // v row r+1
-      lz[p][tid + 1] = Z[(k + 2) & 3];            // z1 row r
+      V[sv] = load_v(min(r + 2 + PF, re + 1));
+      load_in(min(r + 1 + PF, re), IN[si]);
+      put_v(p, V[s1], IN[s1]);  // v row r+1
+      lz[p][tid + 1] = Z[s0];   // z1 row r
       __syncthreads();
-      stage1(min(r + 1, re), p, V[(k + 2) & 3], V[(k + 3) & 3], V[k & 3], IN[(k + 3) & 3],
-             TT[(k + 3) & 3], Z[(k + 3) & 3], DB[(k + 3) & 3], INV[(k + 3) & 3]);
-      const double2 w = stage2(min(r, re), p, Z[(k + 1) & 3], Z[(k + 2) & 3], Z[(k + 3) & 3],
-                               TT[(k + 2) & 3], DB[(k + 2) & 3], INV[(k + 2) & 3]);
+      stage1(min(r + 1, re), p, V[s0], V[s1], V[s2], IN[s1], TT[s1], Z[s1], DB[s1], INV[s1]);
+      const double2 w = stage2(min(r, re), p, Z[sm1], Z[s0], Z[s1], TT[s0], DB[s0], INV[s0]);
       if (outl && live) {
         double2* q = a.out0 + (size_t)r * n + c;
         __builtin_nontemporal_store(w.x, &q->x);
@@ -932,7 +938,7 @@ __device__ __forceinline__ void sl2_tile9(const StencilArgs& a, const int t) {
 // SHAPE (5-point): 0 = sl2_tile (two barriers per row), 1 = sl2_tile_1b (one barrier per row),
 // 2 = sl2_wave (wave strips, no barrier), 3 = sl2_tile_v2 (one barrier, LDS tables, mask-free
 // interior tiles).  The 9-point operator has sl2_tile9 only.
-template <bool CONSTC, bool NTU, int TPB, bool S9, int SHAPE = 0>
+template <bool CONSTC, bool NTU, int TPB, bool S9, int SHAPE = 0, int PF = 1>
 __global__ __launch_bounds__(TPB) void sl2_kernel(const StencilArgs a) {
   if (a.stop && *a.stop) return;  // queued GMRES cycle already stopped
   const int L = blockIdx.x;
@@ -954,22 +960,22 @@ __global__ __launch_bounds__(TPB) void sl2_kernel(const StencilArgs a) {
       const bool interior = i0 - 2 >= 0 && i0 + TPB - 1 < a.n && a.j0 + rb - 1 >= 0 &&
                             a.j0 + re < a.n;
       __shared__ Sl2Lds lds;
-      if (interior) sl2_tile_v2<CONSTC, NTU, false>(a, t, lds);
-      else sl2_tile_v2<CONSTC, NTU, true>(a, t, lds);
+      if (interior) sl2_tile_v2<CONSTC, NTU, false, PF>(a, t, lds);
+      else sl2_tile_v2<CONSTC, NTU, true, PF>(a, t, lds);
     }
     else sl2_tile<CONSTC, NTU, TPB>(a, t);
   }
 }
 
-template <int TPB, bool NTU, int SHAPE = 0>
+template <int TPB, bool NTU, int SHAPE = 0, int PF = 1>
 void launch_t(bool const_c, const StencilArgs& a, int blocks, hipStream_t s) {
   const bool s9 = a.tab_r2x != nullptr;  // 9-point operator (the tables themselves are unused)
   if (const_c) {
     if (s9) hipLaunchKernelGGL((sl2_kernel<true, NTU, TPB, true>), dim3(blocks), dim3(TPB), 0, s, a);
-    else hipLaunchKernelGGL((sl2_kernel<true, NTU, TPB, false, SHAPE>), dim3(blocks), dim3(TPB), 0, s, a);
+    else hipLaunchKernelGGL((sl2_kernel<true, NTU, TPB, false, SHAPE, PF>), dim3(blocks), dim3(TPB), 0, s, a);
   } else {
     if (s9) hipLaunchKernelGGL((sl2_kernel<false, NTU, TPB, true>), dim3(blocks), dim3(TPB), 0, s, a);
-    else hipLaunchKernelGGL((sl2_kernel<false, NTU, TPB, false, SHAPE>), dim3(blocks), dim3(TPB), 0, s, a);
+    else hipLaunchKernelGGL((sl2_kernel<false, NTU, TPB, false, SHAPE, PF>), dim3(blocks), dim3(TPB), 0, s, a);
   }
 }
 
@@ -985,12 +991,14 @@ void launch_sl2(bool const_c, const StencilArgs& a_in, hipStream_t stream, int v
   int tpb = 256;
   bool ntu = n <= 4608;
   int shape = 0;
+  bool pf2 = false;
   if (variant == 6 || variant == 18 || variant == 30 || variant == 42) {
     tpb = variant >= 24 ? 512 : 256;
     ntu = variant % 24 >= 12;
-  } else if (sl2_variant(variant)) {  // kSl2Variant + shape (1, 2) + 4 NT v loads
+  } else if (sl2_variant(variant)) {  // kSl2Variant + shape (0..3) + 4 NT v loads + 8 PF 2
     shape = (variant - kSl2Variant) & 3;
     ntu = ((variant - kSl2Variant) & 4) != 0;
+    pf2 = shape == 3 && ((variant - kSl2Variant) & 8) != 0;
   }
   if (a.tab_r2x) shape = 0;  // the 9-point operator has the LDS marching shape only
   const int rows = a.row_end - a.row_begin;
@@ -1015,8 +1023,13 @@ void launch_sl2(bool const_c, const StencilArgs& a_in, hipStream_t stream, int v
     if (ntu) launch_t<256, true, 1>(const_c, a, blocks, stream);
     else launch_t<256, false, 1>(const_c, a, blocks, stream);
   } else if (shape == 3) {
-    if (ntu) launch_t<256, true, 3>(const_c, a, blocks, stream);
-    else launch_t<256, false, 3>(const_c, a, blocks, stream);
+    if (pf2) {
+      if (ntu) launch_t<256, true, 3, 2>(const_c, a, blocks, stream);
+      else launch_t<256, false, 3, 2>(const_c, a, blocks, stream);
+    } else {
+      if (ntu) launch_t<256, true, 3>(const_c, a, blocks, stream);
+      else launch_t<256, false, 3>(const_c, a, blocks, stream);
+    }
   } else if (shape == 2) {
     if (ntu) launch_t<256, true, 2>(const_c, a, blocks, stream);
     else launch_t<256, false, 2>(const_c, a, blocks, stream);

@@ -182,7 +182,7 @@ def test_default_maxiter_and_restart_follow_the_global_size(op):
                                           callback_type="legacy")
     # this solve runs for hundreds of iterations, far past the horizon where scipy's own run is
     # reproducible to 1e-6: both must converge the same way, not bit for bit
-    assert info == infor == 0 and abs(len(c) - len(cr)) <= 2, (len(c), len(cr))
+    assert info == infor == 0 and abs(len(c) - len(cr)) <= 0.05 * len(cr), (len(c), len(cr))
     for u in (x, xr):
         assert np.linalg.norm(f - R @ u) <= 1e-3 * np.linalg.norm(f)
     assert np.linalg.norm(x - xr) <= 1e-3 * np.linalg.norm(xr)

@@ -228,7 +228,8 @@ def test_fused_shifted_laplace_on_slabs(slabs, stencil):
         np.testing.assert_array_equal(y, outs[0])
 
 
-SL2_SHAPES = [160, 161, 162, 163, 164, 165, 166, 167]  # kSl2Variant + shape (0-3) + 4 (NT v)
+SL2_SHAPES = [160, 161, 162, 163, 164, 165, 166, 167, 171, 175]  # kSl2Variant + shape (0-3)
+# + 4 (NT v) + 8 (prefetch 2, shape 3)
 
 
 @pytest.mark.parametrize("n,kind,rpb,slabs", [(97, "c2", 0, 1), (700, "c1", 13, 1),
@@ -257,7 +258,7 @@ def test_fused_shifted_laplace_shapes_bit_identical(n, kind, rpb, slabs):
         np.testing.assert_array_equal(A._apply_host(x, H._ffi.HH_APPLY_PREC_A), ref, err_msg=str(v))
     f = O.init_f1_mat(.5, .125, om, n).ravel()
     out = []
-    for v in (-1, 162, 163, 167):
+    for v in (-1, 162, 163, 167, 175):
         A.tune(v, rpb, 0)
         xs, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=12, M=M,
                                  callback=lambda r: None, callback_type="legacy",

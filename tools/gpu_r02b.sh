@@ -19,7 +19,7 @@ step() {  # step NAME SECONDS CMD...
 PYT="python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu"
 step t_shapes 300 $PYT tests/test_gpu_variants.py -k "shapes_bit_identical" -x
 step t_errors 200 $PYT tests/test_gpu_errors.py -k default_maxiter
-step t_fused 300 $PYT tests/test_gpu_variants.py -k fused -x
-step tune_sl2 300 python tools/tune_sl2.py --variants 165,163,167 --rpbs 16,32,48 --rounds 3
-step tune_sl2_gmres 300 python tools/tune_gmres_variant.py 4096 -1,163,167
+step t_fused 300 $PYT tests/test_gpu_variants.py -k "shapes_bit" -x
+step tune_sl2 300 python tools/tune_sl2.py --variants 165,163,167,171,175 --rpbs 16,32 --rounds 3
+step tune_sl2_gmres 300 python tools/tune_gmres_variant.py 4096 -1,167,175
 echo done
