@@ -514,8 +514,9 @@ __device__ __forceinline__ void sl2_tile_v2(const StencilArgs& a, const int t, S
     lz[0][TPB + 1] = z2;
     lz[1][TPB + 1] = z2;
   }
-  // rows rb-2 .. rb+1+PF of v and rb-1 .. rb+PF of 1/c^2 (slot = row - rb + 2)
-  unroll<0, 4 + PF>([&](auto kc) {
+  // rows rb-2 .. rb+1+PF of v and rb-1 .. rb+PF of 1/c^2 (slot = (row - rb + 2) % RS; with
+  // PF 1 row rb+2 reuses the slot of row rb-2, so it is loaded once that row is consumed)
+  unroll<0, 4>([&](auto kc) {
     constexpr int m = decltype(kc)::value;
     V[m] = load_v(min(rb - 2 + m, re + 1));
   });
@@ -526,6 +527,10 @@ __device__ __forceinline__ void sl2_tile_v2(const StencilArgs& a, const int t, S
   put_v(1, V[1], IN[1]);
   __syncthreads();  // (also publishes the table rows)
   stage1(rb - 1, 1, V[0], V[1], V[2], IN[1], TT[1], Z[1], DB[1], INV[1]);
+  unroll<4, 4 + PF>([&](auto kc) {
+    constexpr int m = decltype(kc)::value;
+    V[m % RS] = load_v(min(rb - 2 + m, re + 1));
+  });
   put_v(0, V[2], IN[2]);
   __syncthreads();
   stage1(rb, 0, V[1], V[2], V[3], IN[2], TT[2], Z[2], DB[2], INV[2]);
