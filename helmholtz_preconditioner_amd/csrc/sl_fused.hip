@@ -989,28 +989,42 @@ void launch_t(bool const_c, const StencilArgs& a, int blocks, hipStream_t s) {
 void launch_sl2(bool const_c, const StencilArgs& a_in, hipStream_t stream, int variant) {
   StencilArgs a = a_in;
   const int n = a.n;
-  // 256-wide strips (126 VGPRs: 4 blocks per CU instead of 2 at 512; 4096^2 inside GMRES(20):
-  // 768 vs 754 it/s, profiles/r01v_tune_sl2*.log), non-temporal v (just written by the previous
-  // kernel) on rows up to 4608 points; a stencil tuning variant (hh_op_tune) of the LDS family
-  // picks the strip width (>= 24: 512) and NT v loads (% 24 >= 12)
+  // Round-1 shape (0, two barriers per row; still the 9-point one): 256-wide strips (126 VGPRs:
+  // 4 blocks per CU instead of 2 at 512), non-temporal v on rows up to 4608 points; a stencil
+  // tuning variant of the LDS family (6/18/30/42) selects it with its strip width (>= 24: 512)
+  // and NT v loads (% 24 >= 12); kSl2Variant + ... selects any shape (hh_internal.hpp).
+  // Default: shape 3 (one barrier per row, LDS row tables, mask-free interior tiles) with
+  // prefetch distance 2 and v loaded through the cache.  Inside GMRES(20) at 4096^2 it averages
+  // 118.7 us against 133.2 us for the two-barrier shape (rocprofv3, profiles/r02f_*); cold
+  // standalone applies 141.8 vs 146.8 us (profiles/r02e_tune_sl2.log).
   int tpb = 256;
-  bool ntu = n <= 4608;
-  int shape = 0;
-  bool pf2 = false;
-  if (variant == 6 || variant == 18 || variant == 30 || variant == 42) {
+  bool ntu = false;
+  int shape = 3;
+  bool pf2 = true;
+  if (variant == 6 || variant == 18 || variant == 30 || variant == 42) {  // (lds_family)
     tpb = variant >= 24 ? 512 : 256;
     ntu = variant % 24 >= 12;
+    shape = 0;  // the round-1 two-barrier shape
+    pf2 = false;
   } else if (sl2_variant(variant)) {  // kSl2Variant + shape (0..3) + 4 NT v loads + 8 PF 2
     shape = (variant - kSl2Variant) & 3;
     ntu = ((variant - kSl2Variant) & 4) != 0;
     pf2 = shape == 3 && ((variant - kSl2Variant) & 8) != 0;
   }
-  if (a.tab_r2x) shape = 0;  // the 9-point operator has the LDS marching shape only
+  const bool lds_family = variant == 6 || variant == 18 || variant == 30 || variant == 42;
+  if (a.tab_r2x) {  // the 9-point operator has the two-barrier LDS shape only (round-1 default:
+    shape = 0;      // NT v on rows up to 4608 points)
+    pf2 = false;
+    if (!lds_family) ntu = n <= 4608;
+  }
   const int rows = a.row_end - a.row_begin;
   if (shape == 3 && a.rows_per_block > kSl2MaxBand) {  // LDS table capacity of the shape
-    if (a.row_step == a.rows_per_block) a.row_step = kSl2MaxBand;
-    if (a.row_step <= 0 || a.row_step > kSl2MaxBand) shape = 1;  // (spaced bands: keep)
-    else a.rows_per_block = kSl2MaxBand;
+    if (a.row_step <= 0 || a.row_step == a.rows_per_block) {
+      a.rows_per_block = kSl2MaxBand;
+      a.row_step = 0;
+    } else {
+      shape = 1;  // (spaced bands taller than the table: the one-barrier shape)
+    }
   }
   if (a.row_step <= 0) a.row_step = a.rows_per_block;  // (> 0: spaced boundary bands)
   // output columns per tile: TPB - 2 (strip shapes) or 4 wave strips of 62 (shape 2)

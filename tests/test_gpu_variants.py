@@ -232,7 +232,7 @@ SL2_SHAPES = [160, 161, 162, 163, 164, 165, 166, 167, 171, 175]  # kSl2Variant +
 # + 4 (NT v) + 8 (prefetch 2, shape 3)
 
 
-@pytest.mark.parametrize("n,kind,rpb,slabs", [(97, "c2", 0, 1), (700, "c1", 13, 1),
+@pytest.mark.parametrize("n,kind,rpb,slabs", [(97, "c2", 0, 1), (700, "c1", 13, 1), (700, "c1", 100, 1),
                                               (1100, "const", 0, 1), (2100, "c1", 0, 1),
                                               (301, "c1", 0, 3), (63, "c1", 0, 1),
                                               (125, "c2", 5, 2)])
