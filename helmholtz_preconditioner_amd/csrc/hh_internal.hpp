@@ -183,7 +183,9 @@ struct GivensState {
   double2* H;      // [restart][restart+1]   H[col*(restart+1) + k]
   double2* G;      // [restart][2] (c, s)
   double2* S;      // [restart+1]
-  double* vscale;  // [restart+1] real scales of the stored basis vectors
+  double* vscale;  // [restart+1] real scales of the stored basis vectors (1 / their norms)
+  double* sscale;  // [restart+1] scale of each SpMV input: = vscale (two-allreduce mode), or
+                   // its Pythagorean estimate (one-allreduce mode, gmres_lag_kernel)
   double2* ycoef;  // [restart] x-update coefficients y_k * vscale_k
   double* status;  // [8]: 0 presid, 1 breakdown, 2 h0, 3 h1, 4 rnorm, 5 mnorm
   double* status_it;  // [restart][4]: presid, breakdown, h0, h1 of every inner iteration
@@ -201,6 +203,11 @@ struct GivensState {
 void launch_gmres_column(const GivensState& g, int col, const double* red_dots,
                          const double* red_norm, const double* norm_partials, int norm_count,
                          double eps, double ptol, int stop_col, hipStream_t stream);
+// One-allreduce iteration j (lagged normalisation; krylov.hip gmres_lag_kernel): finishes column
+// j-1 with |u_j|^2 = *sig2, starts column j from the raw dots red_dots (2(j+1) doubles, |w|^2
+// after them) and estimates the next SpMV input scale.  final_step: only finish column j-1.
+void launch_gmres_lag(const GivensState& g, int j, const double* red_dots, const double* sig2,
+                      bool final_step, double eps, double ptol, int stop_col, hipStream_t stream);
 // Start of a cycle: S[0] = ||Mr||, vscale[0] = 1/||Mr|| from red[idx_m]; status[4] = ||r||.
 void launch_gmres_start(const GivensState& g, const double* red, int idx_r, int idx_m,
                         hipStream_t stream);

@@ -227,28 +227,20 @@ __device__ double wave_reduce_like_block(const double* partials, int count, int 
   return x;
 }
 
-__global__ void gmres_column_kernel(GivensState g, int col, const double* rd, const double* rn,
-                                    const double* npart, int ncount, double eps, double ptol,
-                                    int stop_col) {
-  if (g.ctrl[0]) return;
-  double rn0;
-  if (npart) {
-    rn0 = wave_reduce_like_block(npart, ncount, kMaxNorms);
-  }
-  if (threadIdx.x != 0) return;
-  if (!npart) rn0 = rn[0];
+// Second half of a Hessenberg column (lane 0): subdiagonal h1 against h0 (scipy's breakdown
+// test), the previous Givens rotations, a new one (zlartg), the residual estimate and the inner
+// exit test (iterative.py:767-795).  h[0 .. col] are already in place.
+__device__ void gmres_finish_column(const GivensState& g, int col, double h0, double h1,
+                                    double inv_sigma_next, double eps, double ptol, int stop_col) {
   const int R1 = g.restart + 1;
   double2* h = g.H + (size_t)col * R1;
-  for (int k = 0; k <= col; ++k) h[k] = cscale(make_double2(rd[2 * k], rd[2 * k + 1]), g.vscale[k]);
-  const double h0 = sqrt(rd[2 * (col + 1)]);
-  const double h1 = sqrt(rn0);
   h[col + 1] = make_double2(h1, 0.0);
   double brk = 0.0;
   if (h1 <= eps * h0) {
     h[col + 1] = make_double2(0.0, 0.0);
     brk = 1.0;
   } else {
-    g.vscale[col + 1] = 1.0 / h1;
+    g.vscale[col + 1] = inv_sigma_next;
   }
   for (int k = 0; k < col; ++k) {
     const double c = g.G[2 * k].x;
@@ -282,6 +274,69 @@ __global__ void gmres_column_kernel(GivensState g, int col, const double* rd, co
   if (presid <= ptol || brk != 0.0 || col >= stop_col) g.ctrl[0] = 1;
 }
 
+__global__ void gmres_column_kernel(GivensState g, int col, const double* rd, const double* rn,
+                                    const double* npart, int ncount, double eps, double ptol,
+                                    int stop_col) {
+  if (g.ctrl[0]) return;
+  double rn0;
+  if (npart) {
+    rn0 = wave_reduce_like_block(npart, ncount, kMaxNorms);
+  }
+  if (threadIdx.x != 0) return;
+  if (!npart) rn0 = rn[0];
+  const int R1 = g.restart + 1;
+  double2* h = g.H + (size_t)col * R1;
+  for (int k = 0; k <= col; ++k) h[k] = cscale(make_double2(rd[2 * k], rd[2 * k + 1]), g.vscale[k]);
+  const double h0 = sqrt(rd[2 * (col + 1)]);
+  const double h1 = sqrt(rn0);
+  gmres_finish_column(g, col, h0, h1, 1.0 / h1, eps, ptol, stop_col);
+}
+
+// One-allreduce iteration j (lagged normalisation, world > 1; see runtime.cpp hh_gmres).  The
+// basis is stored raw: u_k with exact norms sigma_k (vscale[k] = 1/sigma_k once known) and the
+// SpMV of iteration j ran on sscale[j] u_j, sscale[j] an estimate of 1/sigma_j.  With raw dots
+// d_k = <u_k, w> (rd[2k], rd[2k+1], k <= j), |w|^2 = rd[2j+2] and |u_j|^2 = rd[2j+3] (j >= 1), all
+// from the iteration's single allreduce:
+//   (a) vscale[j] = 1/sigma_j;
+//   (b) column j-1 is finished: h1 = sigma_j vscale[j-1] / sscale[j-1] (the Hessenberg
+//       subdiagonal the previous iteration could not know), rotations, presid, exit test;
+//   (c) column j is started: h_kj = d_k vscale[k] f, h0 = |w| f with f = vscale[j] / sscale[j]
+//       (the true <v_k, M A v_j> and |M A v_j| of scipy's normalised basis);
+//   (d) sscale[j+1] = 1 / sqrt(|w|^2 - sum_k |d_k|^2 vscale[k]^2) (Pythagoras, floored): only
+//       the scale of the next SpMV's input -- never part of H -- so cancellation in it cannot
+//       reach the solve.
+// The update (w -= sum_k d_k vscale[k]^2 u_k) follows with the exact vscale.  `final` (after the
+// cycle's last iteration): rd is unused and sig2 holds |u_j|^2 -- steps (a), (b) only.
+__global__ void gmres_lag_kernel(GivensState g, int j, const double* rd, const double* sig2,
+                                 int final_step, double eps, double ptol, int stop_col) {
+  if (g.ctrl[0] || threadIdx.x != 0) return;
+  const int R1 = g.restart + 1;
+  double vj = g.vscale[0];
+  if (j >= 1) {
+    const double sj = sqrt(*sig2);
+    vj = 1.0 / sj;
+    const int col = j - 1;
+    const double f = g.vscale[col] / g.sscale[col];
+    const double h0 = g.status_it[4 * col + 2];  // stored when the column was started
+    const double h1 = sj * f;
+    gmres_finish_column(g, col, h0, h1, vj, eps, ptol, stop_col);
+    if (g.ctrl[0] || final_step) return;
+  }
+  const double f = vj / g.sscale[j];
+  double2* h = g.H + (size_t)j * R1;
+  const double w2 = rd[2 * (j + 1)];
+  double rest = w2;
+  for (int k = 0; k <= j; ++k) {
+    const double vk = k == j ? vj : g.vscale[k];
+    const double2 d = make_double2(rd[2 * k], rd[2 * k + 1]);
+    h[k] = cscale(cscale(d, vk), f);
+    rest -= cabs2(d) * vk * vk;
+  }
+  g.status_it[4 * j + 2] = sqrt(w2) * f;
+  const double floor2 = fmax(w2 * 1e-28, 1e-300);
+  g.sscale[j + 1] = 1.0 / sqrt(fmax(rest, floor2));
+}
+
 __global__ void gmres_start_kernel(GivensState g, const double* red, int idx_r, int idx_m) {
   if (threadIdx.x != 0) return;
   g.ctrl[0] = 0;
@@ -291,6 +346,7 @@ __global__ void gmres_start_kernel(GivensState g, const double* red, int idx_r, 
   for (int k = 0; k <= g.restart; ++k) g.S[k] = make_double2(0.0, 0.0);
   g.S[0] = make_double2(mn, 0.0);
   g.vscale[0] = 1.0 / mn;
+  g.sscale[0] = 1.0 / mn;
   g.status[4] = rn;
   g.status[5] = mn;
 }
@@ -425,6 +481,12 @@ void launch_gmres_column(const GivensState& g, int col, const double* red_dots,
                          double eps, double ptol, int stop_col, hipStream_t stream) {
   hipLaunchKernelGGL(gmres_column_kernel, dim3(1), dim3(kWave), 0, stream, g, col, red_dots,
                      red_norm, norm_partials, norm_count, eps, ptol, stop_col);
+}
+
+void launch_gmres_lag(const GivensState& g, int j, const double* red_dots, const double* sig2,
+                      bool final_step, double eps, double ptol, int stop_col, hipStream_t stream) {
+  hipLaunchKernelGGL(gmres_lag_kernel, dim3(1), dim3(kWave), 0, stream, g, j, red_dots, sig2,
+                     final_step ? 1 : 0, eps, ptol, stop_col);
 }
 
 void launch_gmres_start(const GivensState& g, const double* red, int idx_r, int idx_m,

@@ -136,6 +136,10 @@ struct hh_op {
   double2* gbuf = nullptr;
   GivensState gs{};
   double* status_h = nullptr;
+  // in-solve reductions per inner iteration (hh_op_set_krylov_mode): 0 auto (two allreduces on
+  // one rank -- where they are free --, one across ranks), 1 two, 2 one (lagged normalisation)
+  int krylov_mode = 0;
+  double* npart = nullptr;  // update-kernel norm partials, kept one iteration (one-allreduce mode)
   // timing hooks
   hipEvent_t tk0 = nullptr, tk1 = nullptr;
   // device stop flag of the GMRES cycle being queued (nullptr outside hh_gmres)
@@ -611,7 +615,8 @@ void ensure_gmres(hh_op* op, int restart) {
   op->V_cols = restart + 1;
   const int R1 = restart + 1;
   const size_t nH = (size_t)restart * R1, nG = 2 * (size_t)restart, nS = R1, nY = restart;
-  const size_t total2 = nH + nG + nS + nY + (R1 + 8 + 1) / 2 + 8 + 2 * (size_t)restart + 8;
+  const size_t total2 = nH + nG + nS + nY + (R1 + 8 + 1) / 2 + 8 + 2 * (size_t)restart + 8 +
+                        (R1 + 1) / 2 + 1;
   op->gbuf = dalloc<double2>(total2);
   HIPC(hipMemsetAsync(op->gbuf, 0, total2 * sizeof(double2), op->ctx->stream));
   GivensState& g = op->gs;
@@ -622,6 +627,8 @@ void ensure_gmres(hh_op* op, int restart) {
   g.vscale = reinterpret_cast<double*>(g.ycoef + nY);
   g.status = g.vscale + R1 + 1;
   g.status_it = g.status + 8;
+  g.sscale = g.status_it + 4 * (size_t)restart;
+  if (!op->npart) op->npart = dalloc<double>((size_t)kMaxStreamBlocks * kMaxNorms);
   dfree(op->gctrl);
   op->gctrl = dalloc<int>(8);
   HIPC(hipMemsetAsync(op->gctrl, 0, 8 * sizeof(int), op->ctx->stream));
@@ -974,6 +981,7 @@ static void op_release(hh_op* op) {
   dfree(op->V);
   dfree(op->gbuf);
   dfree(op->gctrl);
+  dfree(op->npart);
   dfree(op->sw_P);
   dfree(op->sw_y);
   dfree(op->sw_uF);
@@ -1397,6 +1405,14 @@ HH_API int hh_op_set_stencil(hh_op* op, int points, double alpha, double c, doub
   GUARD_END
 }
 
+HH_API int hh_op_set_krylov_mode(hh_op* op, int mode) {
+  GUARD_BEGIN
+  REQUIRE(op, "null op");
+  REQUIRE(mode >= 0 && mode <= 2, "krylov mode must be 0 (auto), 1 (two reductions) or 2 (one)");
+  op->krylov_mode = mode;
+  GUARD_END
+}
+
 HH_API int hh_op_sl_fusion(hh_op* op, int enable) {
   GUARD_BEGIN
   REQUIRE(op, "null op");
@@ -1571,6 +1587,9 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
   double presid = 0.0, rnorm = 0.0;
   long inner = 0;
   bool legacy = legacy_maxiter != 0;
+  // collectives per inner iteration: one (lagged normalisation) by default across ranks, two on
+  // one rank (no collective there; the exact-norm path keeps round 1's bit-for-bit results)
+  const bool lagged = !reorth && (op->krylov_mode == 2 || (op->krylov_mode == 0 && c->world > 1));
 
   for (long iteration = 0; iteration < maxiter; ++iteration) {
     if (iteration == 0) {
@@ -1591,7 +1610,32 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     const long left = legacy ? maxiter - inner : (long)restart;
     const int stop_col = (int)std::min<long>(restart - 1, left - 1);
     op->stop_flag = g.ctrl;
-    for (int c2 = 0; c2 <= stop_col; ++c2) {
+    for (int c2 = 0; c2 <= stop_col && lagged; ++c2) {
+      // ONE allreduce per inner iteration (lagged normalisation, gmres_lag_kernel): the norm of
+      // the vector the previous update wrote (u_c2, its partials kept in npart) travels with
+      // this iteration's raw dots; the Hessenberg subdiagonal of column c2-1 is completed from
+      // it, one iteration late, and the SpMV meanwhile runs on a Pythagorean estimate of the
+      // scale.  Same Krylov space, same H to rounding, same exit decisions (one wasted SpMV +
+      // projection when a column stops the cycle).
+      double2* vcol = V + (size_t)c2 * ldv;
+      double2* w = V + (size_t)(c2 + 1) * ldv;
+      const int* stp = g.ctrl;
+      apply_MA(op, vcol, g.sscale + c2, w);  // w = M A (s_c2 u_c2)
+      const int K = c2 + 1;
+      launch_multidot(V, ldv, K, w, L, op->partials, blocks, s, stp);
+      launch_reduce(op->partials, blocks, 2 * K + 2, 2 * K + 1, op->red + 16, s, stp);
+      if (c2 > 0) launch_reduce(op->npart, blocks, kMaxNorms, 1, op->red + 16 + 2 * K + 1, s, stp);
+      allreduce_sum_dev(op, op->red + 16, 2 * K + (c2 > 0 ? 2 : 1));
+      launch_gmres_lag(g, c2, op->red + 16, op->red + 16 + 2 * K + 1, false, eps, ptol, stop_col, s);
+      launch_update(V, ldv, K, op->red + 16, g.vscale, w, w, L, op->npart, blocks, s, stp);
+      HIPC(hipGetLastError());
+      if (c2 == stop_col) {  // the cycle's last column needs the norm of the last update
+        launch_reduce(op->npart, blocks, kMaxNorms, 1, op->red + 8, s, stp);
+        allreduce_sum_dev(op, op->red + 8, 1);
+        launch_gmres_lag(g, c2 + 1, nullptr, op->red + 8, true, eps, ptol, stop_col, s);
+      }
+    }
+    for (int c2 = 0; c2 <= stop_col && !lagged; ++c2) {
       double2* vcol = V + (size_t)c2 * ldv;
       double2* w = V + (size_t)(c2 + 1) * ldv;
       const int* stp = g.ctrl;

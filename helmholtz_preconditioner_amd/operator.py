@@ -268,6 +268,17 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
         (identical results; for A/B timing)."""
         check(lib.hh_op_sl_fusion(self.handle, int(bool(enable))))
 
+    KRYLOV_MODES = {"auto": 0, "two": 1, "one": 2}
+
+    def krylov_mode(self, mode: str = "auto"):
+        """Global reductions per GMRES inner iteration: "two" (projections, then the updated
+        vector's norm -- exact normalisation), "one" (lagged normalisation: one allreduce per
+        iteration), "auto" (one across ranks, two on a single rank).  Results agree to
+        rounding."""
+        if mode not in self.KRYLOV_MODES:
+            raise ValueError(f"mode must be one of {sorted(self.KRYLOV_MODES)}")
+        check(lib.hh_op_set_krylov_mode(self.handle, self.KRYLOV_MODES[mode]))
+
     def stats(self):
         s = _ffi.HHStats()
         check(lib.hh_op_last_stats(self.handle, ctypes.byref(s)))

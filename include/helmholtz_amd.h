@@ -205,6 +205,15 @@ int hh_gmres(hh_op* op, const hh_vec* b, hh_vec* x, double rtol, double atol,
 typedef int (*hh_gmres_cycle_callback)(void* user, long cycle);
 int hh_op_set_cycle_callback(hh_op* op, hh_gmres_cycle_callback cb, void* user);
 
+/* Global reductions per GMRES inner iteration (no reference counterpart: scipy runs on one
+ * process).  mode 1: classical Gram-Schmidt with two -- the projections (+ |w|^2), then the norm
+ * of the updated vector (the round-1 path, bit-for-bit).  mode 2: ONE -- the norm of the vector
+ * the previous iteration's update wrote travels with the projections (lagged normalisation: the
+ * Hessenberg subdiagonal of column j is completed in iteration j+1, the SpMV input is scaled by a
+ * Pythagorean estimate meanwhile; H, the residual history and x agree to rounding, one extra
+ * collective per restart cycle).  mode 0 (default): 2 across ranks, 1 on a single rank.  CGS2
+ * (reorth) always uses mode 1. */
+int hh_op_set_krylov_mode(hh_op* op, int mode);
 /* Performance tuning of the stencil kernel used by HH_APPLY_A: variant in [0, 48) selects the
  * marching kernel's W/E exchange (LDS row / direct cached loads / wave shuffle), prefetch depth,
  * load/store cache policy and strip width, 96 + R (R = 2 .. 8 rows, + 16 / + 32 cache-policy

@@ -1,0 +1,133 @@
+"""GPU tier: the one-allreduce GMRES iteration (hh_op_set_krylov_mode 2, lagged normalisation;
+the default across ranks) forced on a single rank, against the reference's own histories
+(tests/golden, scipy gmres as code.py:516 calls it) and the oracle -- the same 1e-6 contract as
+the two-allreduce path -- and against the two-allreduce path itself.
+
+Covered: stagnating runs at restart boundaries (legacy maxiter inside a cycle), a converging
+run with adaptive ptol and several restart cycles, a nonzero x0, all three preconditioners,
+breakdown (zero right-hand side in a cycle), callback types.
+"""
+import numpy as np
+import pytest
+
+import helmholtz_preconditioner_amd as H
+from conftest import load_golden, medium, rand_complex
+from oracle import helmholtz_oracle as O
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = H.Context(device=0)
+    yield c
+
+
+def relerr(a, b):
+    return np.linalg.norm(a - b) / np.linalg.norm(b)
+
+
+@pytest.mark.parametrize("name", ["gmres_n128_none.npz", "gmres_n128_jacobi.npz",
+                                  "gmres_n64_c1_none.npz"])
+def test_one_allreduce_matches_reference_golden(ctx, name):
+    z = load_golden(name)
+    n = int(z["n"])
+    om = complex(z["omega"])
+    cm = medium(str(z["medium"]), n)
+    A = H.build_A_matrix(int(z["b"]), float(z["C"]), float(z["eta"]), om, float(z["h"]), n, cm,
+                         context=ctx)
+    A.krylov_mode("one")
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    M = "jacobi" if str(z["precond"]) == "jacobi" else None
+    hist = []
+    x, info = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=int(z["K"]), M=M,
+                      callback=hist.append, callback_type='legacy')
+    hist = np.array(hist)
+    assert info == int(z["info"]) and len(hist) == int(z["niter"])
+    assert np.max(np.abs(hist - z["history"]) / z["history"]) < TOL
+    assert relerr(x, z["x"]) < TOL
+
+
+@pytest.mark.parametrize("precond", ["none", "jacobi", "sl"])
+@pytest.mark.parametrize("restart,K", [(20, 45), (7, 30), (1, 6)])
+def test_one_allreduce_matches_two_allreduce(ctx, precond, restart, K):
+    """same histories and fields as the exact-normalisation path to rounding (1e-10), with
+    legacy maxiter ending inside a cycle and at a cycle edge; restart 1 (a single column per
+    cycle: only the final lagged step)"""
+    n, b, C, wn = 96, 12, 81.0, 6.0
+    om, h, eta = O.problem_params(n, b, wn, 2.0)
+    cm = medium("c1", n)
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    A = H.build_A_matrix(b, C, eta, om, h, n, cm, context=ctx)
+    M = {"none": None, "jacobi": "jacobi",
+         "sl": H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7)}[precond]
+    out = []
+    for mode in ("two", "one"):
+        A.krylov_mode(mode)
+        x, info, hist = H.gmres(A, f, rtol=1e-3, restart=restart, maxiter=K, M=M,
+                                callback=lambda r: None, callback_type="legacy",
+                                return_history=True)
+        out.append((x, info, hist))
+    A.krylov_mode("auto")
+    (x2, i2, h2), (x1, i1, h1) = out
+    assert i1 == i2 and len(h1) == len(h2) == K
+    assert np.max(np.abs(h1 - h2) / h2) < 1e-10
+    assert relerr(x1, x2) < 1e-10
+
+
+def test_one_allreduce_converging_cycles_and_x0(ctx):
+    """a converging run (info 0, several restart cycles, adaptive ptol, pr_norm counting) and a
+    nonzero x0, against scipy"""
+    import scipy.sparse.linalg
+    n, b, C, wn, al = 40, 6, 61.0, 1.0, 2.0
+    cm = medium("c2", n)
+    om, h, eta = O.problem_params(n, b, wn, al)
+    Aref = O.build_A_matrix(b, C, eta, om, h, n, cm)
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    A = H.build_A_matrix(b, C, eta, om, h, n, cm, context=ctx)
+    A.krylov_mode("one")
+    xr, infor, histr, _ = O.gmres_reference(Aref, f, M=O.jacobi_preconditioner(Aref), rtol=1e-4,
+                                            restart=10, maxiter=400)
+    x, info, hist = H.gmres(A, f, rtol=1e-4, restart=10, maxiter=400, M="jacobi",
+                            callback=lambda r: None, callback_type='legacy', return_history=True)
+    assert info == infor == 0 and len(hist) == len(histr)
+    assert np.max(np.abs(hist - histr) / histr) < TOL
+    assert relerr(x, xr) < TOL
+    ref = []
+    x3, info3 = scipy.sparse.linalg.gmres(Aref, f, rtol=1e-5, restart=10, maxiter=8,
+                                          M=O.jacobi_preconditioner(Aref),
+                                          callback=ref.append, callback_type="pr_norm")
+    got = []
+    x4, info4 = H.gmres(A, f, rtol=1e-5, restart=10, maxiter=8, M="jacobi", callback=got.append,
+                        callback_type="pr_norm")
+    assert info4 == info3 and len(got) == len(ref)
+    assert np.max(np.abs(np.array(got) - np.array(ref)) / np.array(ref)) < TOL
+    x0 = 1e-3 * rand_complex(n * n, 9)
+    xr0, infor0, histr0, _ = O.gmres_reference(Aref, f, rtol=1e-3, restart=20, maxiter=60,
+                                               x0=x0.copy())
+    x5, info5, hist5 = H.gmres(A, f, x0=x0, rtol=1e-3, restart=20, maxiter=60,
+                               callback=lambda r: None, callback_type='legacy',
+                               return_history=True)
+    assert info5 == infor0 and len(hist5) == len(histr0)
+    assert np.max(np.abs(hist5 - histr0) / histr0) < TOL
+    assert relerr(x5, xr0) < TOL
+
+
+def test_one_allreduce_exact_solution_breakdown(ctx):
+    """a right-hand side that is an eigenvector-like image (b = A e_p: the Krylov space closes
+    at once for M = None on a 1x1-dominant system) must end with scipy's breakdown semantics"""
+    import scipy.sparse.linalg
+    n = 24
+    om, h, eta = O.problem_params(n, 6, 2.0, 2.0)
+    cm = medium("const", n)
+    Aref = O.build_A_matrix(6, 61.0, eta, om, h, n, cm)
+    A = H.build_A_matrix(6, 61.0, eta, om, h, n, cm, context=ctx)
+    d = Aref.diagonal()
+    f = d.copy()  # Jacobi-preconditioned system: M f = ones, M A ones = ... (closes quickly)
+    A.krylov_mode("one")
+    x, info = H.gmres(A, f, rtol=1e-10, restart=20, maxiter=3, M="jacobi")
+    xr, infor = scipy.sparse.linalg.gmres(Aref, f, rtol=1e-10, restart=20, maxiter=3,
+                                          M=O.jacobi_preconditioner(Aref))
+    assert info == infor
+    assert relerr(x, xr) < 1e-8
