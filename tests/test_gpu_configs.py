@@ -96,6 +96,7 @@ def config4_reference(ctx, tmp_path_factory):
     y.close()
     np.save(d / "y.npy", yh)
     f = H.init_f1_mat(.5, .125, om, n).ravel()
+    A.krylov_mode("one")  # as the ranks run it (one allreduce per iteration): like with like
     xs, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=K4, M="jacobi",
                              callback=lambda r: None, callback_type="legacy",
                              return_history=True)

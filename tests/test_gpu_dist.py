@@ -64,6 +64,7 @@ def _single_domain(n, stencil=5, default_limits=False):
     om, h, eta = H.problem_params(n, 12, 6.0, 2.0)
     A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.init_c1_mat(.5, .5, n), context=ctx,
                          stencil=stencil)
+    A.krylov_mode("one")  # the ranks' default (one allreduce per iteration): like with like
     rng = np.random.default_rng(5)
     xg = rng.standard_normal(n * n) + 1j * rng.standard_normal(n * n)
     res = dict(y=A @ xg)
@@ -115,7 +116,9 @@ def _check_against_single_domain(parts, ref, world, n):
     if "x_default" in ref:
         x = np.concatenate([p["x_default"] for p in parts])
         assert all(int(p["info_default"]) == int(ref["info_default"]) for p in parts)
-        assert np.linalg.norm(x - ref["x_default"]) <= 1e-8 * np.linalg.norm(ref["x_default"])
+        # (a converging run of hundreds of iterations: past the 1e-8 reproducibility horizon of
+        # reordered reductions)
+        assert np.linalg.norm(x - ref["x_default"]) <= 1e-6 * np.linalg.norm(ref["x_default"])
 
 
 def test_uneven_slabs_default_limits(tmp_path):

@@ -17,6 +17,6 @@ step() {  # step NAME SECONDS CMD...
   return 0
 }
 PYT="python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu"
-step t_krylov 300 $PYT tests/test_gpu_krylov_modes.py
+step t_gmres 300 $PYT tests/test_gpu_gmres.py tests/test_gpu_driver.py
 step t_dist 600 $PYT tests/test_gpu_dist.py tests/test_gpu_configs.py -k "not config2 and not config3"
 echo done
