@@ -164,3 +164,115 @@ def gmres_dist(op, b, rtol, restart, maxiter):
         ptol_f = max(eps, 0.25 * ptol_f) if presid <= ptol else min(1.0, 1.5 * ptol_f)
         ptol = presid * min(ptol_f, atol / rn)
     return x, (0 if rn <= atol else maxiter), np.array(hist)
+
+
+_COUNT = {"allreduce": 0}
+
+
+def counted_allreduce(vals):
+    _COUNT["allreduce"] += 1
+    return allreduce(vals)
+
+
+def gmres_dist_lagged(op, b, rtol, restart, maxiter):
+    """The one-allreduce inner iteration of csrc/krylov.hip gmres_lag_kernel (the runtime's
+    default across ranks), restated: raw basis u_k with exact norms sigma_k learned one
+    iteration late (the norm of the vector an update wrote travels with the next iteration's
+    projections), SpMV inputs scaled by the Pythagorean estimate meanwhile.  Returns
+    (x, info, history, allreduces per inner iteration inside the cycles' loops -- the last
+    column's norm adds one per cycle)."""
+    lartg = get_lapack_funcs('lartg', dtype=np.complex128)
+    eps = np.finfo(float).eps
+    x = np.zeros_like(b)
+    bn = gnorm(b)
+    atol = rtol * bn
+    Mb = gnorm(op.psolve(b))
+    ptol_f = 1.0
+    ptol = Mb * min(ptol_f, atol / bn)
+    U = np.empty((restart + 1, b.size), complex)
+    vs = np.zeros(restart + 1)   # exact 1 / sigma_k
+    ss = np.zeros(restart + 1)   # SpMV input scales
+    H = np.zeros((restart, restart + 1), complex)
+    G = np.zeros((restart, 2), complex)
+    hist, inner, cycle_reduces = [], 0, 0
+    r = b.copy()
+    presid = 0.0
+    for _ in range(maxiter):
+        U[0] = op.psolve(r)
+        t = gnorm(U[0])
+        vs[0] = ss[0] = 1 / t
+        S = np.zeros(restart + 1, complex)
+        S[0] = t
+        brk = False
+        h0 = {}
+        stop_col = min(restart - 1, maxiter - inner - 1)
+
+        def finish(col, h1):
+            nonlocal brk, presid
+            H[col, col + 1] = h1
+            if h1 <= eps * h0[col]:
+                H[col, col + 1] = 0
+                brk = True
+            for k in range(col):
+                c, s = G[k]
+                n0, n1 = H[col, [k, k + 1]]
+                H[col, [k, k + 1]] = [c * n0 + s * n1, -s.conj() * n0 + c * n1]
+            c, s, mag = lartg(H[col, col], H[col, col + 1])
+            G[col] = [c, s]
+            H[col, [col, col + 1]] = mag, 0
+            tmp = -np.conj(s) * S[col]
+            S[[col, col + 1]] = [c * S[col], tmp]
+            presid = abs(tmp)
+            hist.append(presid / bn)
+            return presid <= ptol or brk or col >= stop_col
+
+        col, done = -1, False
+        for j in range(stop_col + 1):
+            w = ss[j] * op.psolve(op.apply(U[j]))
+            loc = [np.vdot(U[k], w) for k in range(j + 1)]
+            vals = sum(([c.real, c.imag] for c in loc), []) + [np.vdot(w, w).real]
+            if j > 0:
+                vals.append(np.vdot(U[j], U[j]).real)   # the previous update's vector
+            raw = counted_allreduce(vals)
+            cycle_reduces += 1
+            d = raw[0:2 * (j + 1):2] + 1j * raw[1:2 * (j + 1):2]
+            w2 = raw[2 * (j + 1)]
+            if j > 0:
+                sj = np.sqrt(raw[2 * (j + 1) + 1])
+                f = vs[j - 1] / ss[j - 1]
+                vs[j] = 1 / sj
+                col = j - 1
+                if finish(col, sj * f):
+                    done = True
+                    break
+            f = vs[j] / ss[j]
+            H[j, :j + 1] = d * vs[:j + 1] * f
+            h0[j] = np.sqrt(w2) * f
+            ss[j + 1] = 1 / np.sqrt(max(w2 - np.sum(np.abs(d) ** 2 * vs[:j + 1] ** 2),
+                                        max(w2 * 1e-28, 1e-300)))
+            U[j + 1] = w - (d * vs[:j + 1] ** 2) @ U[:j + 1]
+        if not done:  # the cycle's last column: one more (per-cycle) reduction
+            sl = np.sqrt(counted_allreduce([np.vdot(U[stop_col + 1], U[stop_col + 1]).real])[0])
+            col = stop_col
+            vs[stop_col + 1] = 1 / sl
+            finish(col, sl * vs[col] / ss[col])
+        inner += col + 1
+        if H[col, col] == 0:
+            S[col] = 0
+        y = S[:col + 1].copy()
+        for k in range(col, 0, -1):
+            if y[k] != 0:
+                y[k] /= H[k, k]
+                y[:k] -= y[k] * H[k, :k]
+        if y[0] != 0:
+            y[0] /= H[0, 0]
+        x += (y * vs[:col + 1]) @ U[:col + 1]
+        r = b - op.apply(x)
+        rn = gnorm(r)
+        if inner == maxiter:
+            return x, (0 if rn <= atol else maxiter), np.array(hist), cycle_reduces / inner
+        if rn <= atol or brk:
+            break
+        ptol_f = max(eps, 0.25 * ptol_f) if presid <= ptol else min(1.0, 1.5 * ptol_f)
+        ptol = presid * min(ptol_f, atol / rn)
+    return x, (0 if rn <= atol else maxiter), np.array(hist), cycle_reduces / inner

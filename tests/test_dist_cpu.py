@@ -51,7 +51,7 @@ def test_file_rendezvous_two_processes():
     assert all(v == bytes(range(128)) for v in got.values()) and len(got) == 3
 
 
-def _gloo_worker(rank, world, port, case, out):
+def _gloo_worker(rank, world, port, case, out, lagged=False):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -68,13 +68,23 @@ def _gloo_worker(rank, world, port, case, out):
                          medium(str(z["medium"]), n), j0, j1,
                          jacobi=str(z["precond"]) == "jacobi")
     f = O.init_f1_mat(.5, .125, om, n)[j0:j1].ravel()
-    x, info, hist = DM.gmres_dist(op, f, 1e-3, 20, int(z["K"]))
-    np.savez(out, x=x, info=info, hist=hist, j0=j0, j1=j1)
+    if lagged:
+        x, info, hist, per_it = DM.gmres_dist_lagged(op, f, 1e-3, 20, int(z["K"]))
+    else:
+        x, info, hist = DM.gmres_dist(op, f, 1e-3, 20, int(z["K"]))
+        per_it = 2.0
+    np.savez(out, x=x, info=info, hist=hist, j0=j0, j1=j1, per_it=per_it)
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case,world", [("gmres_n64_c1_none.npz", 2), ("gmres_n128_jacobi.npz", 3)])
-def test_distributed_gmres_mirror_matches_reference(case, world):
+@pytest.mark.parametrize("case,world,lagged", [("gmres_n64_c1_none.npz", 2, False),
+                                               ("gmres_n128_jacobi.npz", 3, False),
+                                               ("gmres_n64_c1_none.npz", 2, True),
+                                               ("gmres_n128_jacobi.npz", 3, True)])
+def test_distributed_gmres_mirror_matches_reference(case, world, lagged):
+    """lagged: the one-allreduce iteration (the runtime's default across ranks) -- the golden
+    histories to 1e-9, with ONE allreduce per inner iteration inside the restart cycles (plus
+    one per cycle for the last column's norm)."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -82,7 +92,7 @@ def test_distributed_gmres_mirror_matches_reference(case, world):
     ctx = mp.get_context("spawn")
     with tempfile.TemporaryDirectory() as td:
         outs = [os.path.join(td, f"r{r}.npz") for r in range(world)]
-        ps = [ctx.Process(target=_gloo_worker, args=(r, world, port, case, outs[r]))
+        ps = [ctx.Process(target=_gloo_worker, args=(r, world, port, case, outs[r], lagged))
               for r in range(world)]
         for p in ps:
             p.start()
@@ -93,8 +103,10 @@ def test_distributed_gmres_mirror_matches_reference(case, world):
         z = load_golden(case)
         x = np.concatenate([p["x"] for p in parts])
         for p in parts:
-            assert int(p["info"]) == int(z["info"])
+            assert int(p["info"]) == int(z["info"]) and len(p["hist"]) == len(z["history"])
             assert np.max(np.abs(p["hist"] - z["history"]) / z["history"]) < 1e-9
+            if lagged:  # one allreduce per inner iteration inside the cycles
+                assert float(p["per_it"]) == 1.0
         assert np.linalg.norm(x - z["x"]) / np.linalg.norm(z["x"]) < 1e-9
 
 
