@@ -81,6 +81,7 @@ SIGNATURES = [
     ("hh_op_set_cycle_callback", c_int, [c_void_p, GMRES_CYCLE_CALLBACK, c_void_p]),
     ("hh_op_sl_fusion", c_int, [c_void_p, c_int]),
     ("hh_op_set_krylov_mode", c_int, [c_void_p, c_int]),
+    ("hh_op_set_small_cycle", c_int, [c_void_p, c_int]),
     ("hh_op_tune", c_int, [c_void_p, c_int, c_int, c_int]),
     ("hh_op_sweep_mode", c_int, [c_void_p, c_int, c_ip]),
     ("hh_tune_krylov", c_int, [c_int, c_int]),

@@ -211,6 +211,28 @@ void launch_gmres_lag(const GivensState& g, int j, const double* red_dots, const
 // Start of a cycle: S[0] = ||Mr||, vscale[0] = 1/||Mr|| from red[idx_m]; status[4] = ||r||.
 void launch_gmres_start(const GivensState& g, const double* red, int idx_r, int idx_m,
                         hipStream_t stream);
+// A whole restart cycle in one launch for small single-rank grids (gmres_small.hip): workgroup g
+// owns row g with the basis on chip, one grid barrier per inner iteration (lagged
+// normalisation, as gmres_lag_kernel), then the triangular solve and x += V y.
+struct SmallCycleArgs {
+  int n, restart, stop_col;
+  const double2* tab_i;    // as StencilArgs (single slab: rows 0 .. n-1)
+  const double2* tab_j;
+  const double* invc2;     // or nullptr (constant medium)
+  double invc2_const;
+  const double2* v0;       // V[0] = M r, unnormalised (scale g.vscale[0])
+  double2* x;              // x += V y at the end of the cycle
+  GivensState g;           // vscale[0], S[0] in; status_it, ctrl[0..1] out
+  double eps, ptol;
+  double* zbuf;            // [2][n][2n]  z rows handed to the neighbours
+  double* part;            // [2][n][2 (kMaxProj + 1) + 2] partial sums
+  unsigned* bar;           // arrival counter (zeroed before every launch)
+  unsigned* timeout_word;  // set when a barrier wait gives up
+};
+bool small_cycle_eligible(int n, int restart);
+size_t small_cycle_lds_bytes(int n, int restart);
+size_t small_cycle_scratch_doubles(int n);
+void launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi, hipStream_t s);
 // End of a cycle: triangular solve for y, ycoef_k = y_k * vscale_k.
 void launch_gmres_solve(const GivensState& g, int col, hipStream_t stream);
 

@@ -140,6 +140,10 @@ struct hh_op {
   // one rank -- where they are free --, one across ranks), 1 two, 2 one (lagged normalisation)
   int krylov_mode = 0;
   double* npart = nullptr;  // update-kernel norm partials, kept one iteration (one-allreduce mode)
+  // whole-cycle kernel for small grids (gmres_small.hip): hand-off scratch and barrier words
+  int small_cycle = -1;     // -1 auto, 0 off, 1 on where eligible (hh_op_set_small_cycle)
+  double* small_scr = nullptr;
+  unsigned* small_bar = nullptr;  // [4]: arrival counter, timeout word (16 B, zeroed per launch)
   // timing hooks
   hipEvent_t tk0 = nullptr, tk1 = nullptr;
   // device stop flag of the GMRES cycle being queued (nullptr outside hh_gmres)
@@ -982,6 +986,8 @@ static void op_release(hh_op* op) {
   dfree(op->gbuf);
   dfree(op->gctrl);
   dfree(op->npart);
+  dfree(op->small_scr);
+  dfree(op->small_bar);
   dfree(op->sw_P);
   dfree(op->sw_y);
   dfree(op->sw_uF);
@@ -1413,6 +1419,14 @@ HH_API int hh_op_set_krylov_mode(hh_op* op, int mode) {
   GUARD_END
 }
 
+HH_API int hh_op_set_small_cycle(hh_op* op, int mode) {
+  GUARD_BEGIN
+  REQUIRE(op, "null op");
+  REQUIRE(mode >= -1 && mode <= 1, "small-cycle mode must be -1 (auto), 0 (off) or 1 (on)");
+  op->small_cycle = mode;
+  GUARD_END
+}
+
 HH_API int hh_op_sl_fusion(hh_op* op, int enable) {
   GUARD_BEGIN
   REQUIRE(op, "null op");
@@ -1590,6 +1604,17 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
   // collectives per inner iteration: one (lagged normalisation) by default across ranks, two on
   // one rank (no collective there; the exact-norm path keeps round 1's bit-for-bit results)
   const bool lagged = !reorth && (op->krylov_mode == 2 || (op->krylov_mode == 0 && c->world > 1));
+  // small single-rank grids: the whole cycle in one launch (gmres_small.hip) -- launch-bound
+  // otherwise (five kernel boundaries per inner iteration at ~0.5 MB each)
+  const bool small = !reorth && op->small_cycle != 0 && c->world == 1 && op->slabs.size() == 1 &&
+                     op->points == 5 &&
+                     (op->pkind == HH_PREC_NONE || op->pkind == HH_PREC_JACOBI) &&
+                     (op->krylov_mode != 1) && small_cycle_eligible(op->n, restart) &&
+                     (op->small_cycle == 1 || (size_t)op->n * op->n <= ((size_t)1 << 18));
+  if (small && !op->small_scr) {
+    op->small_scr = dalloc<double>(small_cycle_scratch_doubles(op->n));
+    op->small_bar = dalloc<unsigned>(4);
+  }
 
   for (long iteration = 0; iteration < maxiter; ++iteration) {
     if (iteration == 0) {
@@ -1610,7 +1635,30 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     const long left = legacy ? maxiter - inner : (long)restart;
     const int stop_col = (int)std::min<long>(restart - 1, left - 1);
     op->stop_flag = g.ctrl;
-    for (int c2 = 0; c2 <= stop_col && lagged; ++c2) {
+    if (small) {
+      const Slab& sl = op->slabs[0];
+      SmallCycleArgs sa{};
+      sa.n = op->n;
+      sa.restart = restart;
+      sa.stop_col = stop_col;
+      sa.tab_i = op->tab_i;
+      sa.tab_j = sl.tab_j;
+      sa.invc2 = op->const_c ? nullptr : sl.invc2;
+      sa.invc2_const = op->invc2_const;
+      sa.v0 = V;
+      sa.x = x;
+      sa.g = g;
+      sa.eps = eps;
+      sa.ptol = ptol;
+      sa.zbuf = op->small_scr;
+      sa.part = op->small_scr + 2 * (size_t)op->n * 2 * op->n;
+      sa.bar = op->small_bar;
+      sa.timeout_word = op->small_bar + 1;
+      HIPC(hipMemsetAsync(op->small_bar, 0, 4 * sizeof(unsigned), s));
+      launch_small_cycle(sa, op->const_c, op->pkind == HH_PREC_JACOBI, s);
+      HIPC(hipGetLastError());
+    }
+    for (int c2 = 0; c2 <= stop_col && lagged && !small; ++c2) {
       // ONE allreduce per inner iteration (lagged normalisation, gmres_lag_kernel): the norm of
       // the vector the previous update wrote (u_c2, its partials kept in npart) travels with
       // this iteration's raw dots; the Hessenberg subdiagonal of column c2-1 is completed from
@@ -1635,7 +1683,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         launch_gmres_lag(g, c2 + 1, nullptr, op->red + 8, true, eps, ptol, stop_col, s);
       }
     }
-    for (int c2 = 0; c2 <= stop_col && !lagged; ++c2) {
+    for (int c2 = 0; c2 <= stop_col && !lagged && !small; ++c2) {
       double2* vcol = V + (size_t)c2 * ldv;
       double2* w = V + (size_t)(c2 + 1) * ldv;
       const int* stp = g.ctrl;
@@ -1676,9 +1724,18 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
                         hipMemcpyDeviceToHost, s));
     HIPC(hipMemcpyAsync(op->status_h + 4 * restart, g.ctrl, 2 * sizeof(int),
                         hipMemcpyDeviceToHost, s));
+    if (small)
+      HIPC(hipMemcpyAsync(op->status_h + 4 * restart + 1, op->small_bar + 1, sizeof(unsigned),
+                          hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
     int ctl[2];
     std::memcpy(ctl, op->status_h + 4 * restart, 2 * sizeof(int));
+    if (small) {
+      unsigned tmo = 0;
+      std::memcpy(&tmo, op->status_h + 4 * restart + 1, sizeof(unsigned));
+      REQUIRE(tmo == 0, "small-grid GMRES cycle: a grid barrier timed out (workgroups not "
+                        "co-resident?); hh_op_set_small_cycle(op, 0) selects the regular cycle");
+    }
     col = ctl[1];
     REQUIRE(col >= 0 && col <= stop_col, "GMRES cycle state corrupt (last column %d)", col);
     for (int k = 0; k <= col; ++k) {
@@ -1693,8 +1750,10 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     presid = op->status_h[4 * col];
     breakdown = op->status_h[4 * col + 1] != 0.0;
     op->stats.restarts++;
-    launch_gmres_solve(g, col, s);
-    launch_xupdate(V, ldv, col + 1, g.ycoef, x, L, blocks, s);
+    if (!small) {  // (the whole-cycle kernel has solved and updated x itself)
+      launch_gmres_solve(g, col, s);
+      launch_xupdate(V, ldv, col + 1, g.ycoef, x, L, blocks, s);
+    }
     residual(op, b, x, V, 4);  // r = b - A x; V[0] = M r for the next cycle
     read_dev(op, op->red + 4, st, 1);
     rnorm = std::sqrt(st[0]);

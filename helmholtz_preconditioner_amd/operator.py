@@ -279,6 +279,14 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
             raise ValueError(f"mode must be one of {sorted(self.KRYLOV_MODES)}")
         check(lib.hh_op_set_krylov_mode(self.handle, self.KRYLOV_MODES[mode]))
 
+    def small_cycle(self, mode: str = "auto"):
+        """Whole-cycle GMRES kernel for small single-rank grids (csrc/gmres_small.hip): "auto"
+        (where it applies and n^2 <= 2^18), "on" (wherever it applies), "off"."""
+        modes = {"auto": -1, "off": 0, "on": 1}
+        if mode not in modes:
+            raise ValueError(f"mode must be one of {sorted(modes)}")
+        check(lib.hh_op_set_small_cycle(self.handle, modes[mode]))
+
     def stats(self):
         s = _ffi.HHStats()
         check(lib.hh_op_last_stats(self.handle, ctypes.byref(s)))

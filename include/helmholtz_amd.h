@@ -214,6 +214,14 @@ int hh_op_set_cycle_callback(hh_op* op, hh_gmres_cycle_callback cb, void* user);
  * collective per restart cycle).  mode 0 (default): 2 across ranks, 1 on a single rank.  CGS2
  * (reorth) always uses mode 1. */
 int hh_op_set_krylov_mode(hh_op* op, int mode);
+/* Whole-cycle GMRES kernel for small grids (no reference counterpart): a restart cycle of
+ * hh_gmres as ONE launch whose workgroups keep the Krylov basis on chip and meet once per inner
+ * iteration (lagged normalisation as krylov mode 2), instead of five launches per iteration.
+ * Applies on a single rank and slab, 5-point operator, M = none or Jacobi, without reorth, when
+ * n <= 256 and the basis fits the LDS (3 n (restart + 1) x 16 B <= ~150 KB).  mode -1 (default):
+ * used when it applies and n^2 <= 2^18; 1: whenever it applies; 0: never.  Results agree with the
+ * regular cycle to rounding. */
+int hh_op_set_small_cycle(hh_op* op, int mode);
 /* Performance tuning of the stencil kernel used by HH_APPLY_A: variant in [0, 48) selects the
  * marching kernel's W/E exchange (LDS row / direct cached loads / wave shuffle), prefetch depth,
  * load/store cache policy and strip width, 96 + R (R = 2 .. 8 rows, + 16 / + 32 cache-policy
