@@ -97,18 +97,22 @@ __device__ bool grid_barrier(unsigned* counter, unsigned target, unsigned* timeo
   return ctl[2] == 0;
 }
 
-// fixed-order block reduction of `cols` per-thread values value(c) into sh.sum[c]: a butterfly
-// in every wave, then the waves in index order.  Identical on every workgroup for identical
-// inputs.
-template <int MAXC, class F>
-__device__ void block_sum(F&& value, int cols, const Shared& sh) {
+// fixed-order block reduction of the per-thread registers v[0 .. cols) into sh.sum: a butterfly
+// in every wave -- all MAXC columns interleaved, so the shuffle latencies overlap -- then the
+// waves in index order.  Identical on every workgroup for identical inputs (lane 0's sum).
+template <int MAXC>
+__device__ __forceinline__ void block_sum(double (&v)[MAXC], int cols, const Shared& sh) {
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const int waves = (blockDim.x + kWave - 1) / kWave;
-  for (int c = 0; c < cols; ++c) {
-    double x = value(c);
 #pragma unroll
-    for (int off = kWave / 2; off > 0; off >>= 1) x += __shfl_xor(x, off);
-    if (lane == 0) sh.wred[wave * MAXC + c] = x;
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) v[c] += __shfl_xor(v[c], off);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+      if (c < cols) sh.wred[wave * MAXC + c] = v[c];
   }
   __syncthreads();
   if ((int)threadIdx.x < cols) {
@@ -190,11 +194,13 @@ __device__ bool finish_column(const Shared& sh, const SmallCycleArgs& a, int col
   return presid <= a.ptol || brk != 0.0 || col >= a.stop_col;
 }
 
-template <bool CONSTC, bool JAC>
+// MAXC: partial-sum columns held in registers, >= 2 (restart + 1) + 2 (instantiated per
+// restart range, launch_small_cycle)
+template <bool CONSTC, bool JAC, int MAXC>
 __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallCycleArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = a.n, R = a.restart, R1 = R + 1;
-  constexpr int MAXC = 2 * (kMaxProj + 1) + 2;  // partial-sum columns
+  constexpr int PSTRIDE = 2 * (kMaxProj + 1) + 2;  // row stride of the global partials
   const int g = blockIdx.x, t = threadIdx.x;
   const bool act = t < n;
   const int tc = min(t, n - 1);
@@ -215,8 +221,8 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
     sh.vs = (l1*)take(sizeof(double) * R1);
     sh.ss = (l1*)take(sizeof(double) * R1);
     sh.h0s = (l1*)take(sizeof(double) * R);
-    sh.wred = (l1*)take(sizeof(double) * MAXC * (kSmallThreads / kWave));
-    sh.sum = (l1*)take(sizeof(double) * MAXC);
+    sh.wred = (l1*)take(sizeof(double) * PSTRIDE * (kSmallThreads / kWave));
+    sh.sum = (l1*)take(sizeof(double) * PSTRIDE);
     sh.ctl = (li*)take(sizeof(int) * 4);
   }
   auto Urow = [&](int k, int r) -> l2* { return sh.U + ((size_t)k * 3 + r) * n; };
@@ -282,34 +288,40 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
     }
     const int cols = 2 * K + 2;
     // per column: conj(u_k) z (re, im) for k < K, |z|^2, |u_j|^2 of the own row (lagged norm)
-    block_sum<MAXC>([&](int c) -> double {
-      if (c < 2 * K) {
-        const double2 dk = cfma_conj(csel(act, Urow(c >> 1, 1)[tc], z2), z, z2);
-        return (c & 1) ? dk.y : dk.x;
-      }
-      if (c == 2 * K) return fma(z.x, z.x, z.y * z.y);
-      return j > 0 ? cabs2(uC) : 0.0;
-    }, cols, sh);
-    double* pout = a.part + ((size_t)par * G + g) * MAXC;
+#pragma unroll
+    for (int k = 0; k < MAXC / 2; ++k) {
+      double2 dk = z2;
+      if (k < K) dk = cfma_conj(csel(act, Urow(k, 1)[tc], z2), z, z2);
+      v[2 * k] = dk.x;
+      v[2 * k + 1] = dk.y;
+    }
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      if (c == 2 * K) v[c] = fma(z.x, z.x, z.y * z.y);
+      if (c == 2 * K + 1) v[c] = j > 0 ? cabs2(uC) : 0.0;
+    }
+    block_sum<MAXC>(v, cols, sh);
+    double* pout = a.part + ((size_t)par * G + g) * PSTRIDE;
     if ((int)t < cols) st_sc1(pout + t, sh.sum[t]);
     epoch++;
     if (!grid_barrier(a.bar, epoch * G, a.timeout_word, sh.ctl)) return;
     // every workgroup sums all partials in the same order: thread q holds workgroup q's row
-    // (G <= blockDim), every load in flight at once (unconditional, clamped columns)
+    // (G <= blockDim), every load in flight at once (unconditional, clamped columns), and the
+    // neighbours' z rows (for the ghost update below) loaded alongside
+    const int glo = min(max(g - 1, 0), n - 1), ghi = min(g + 1, n - 1);
+    const double* zlo = a.zbuf + ((size_t)par * n + glo) * 2 * n + 2 * tc;
+    const double* zhi = a.zbuf + ((size_t)par * n + ghi) * 2 * n + 2 * tc;
+    const double2 zl = make_double2(ld_sc1(zlo), ld_sc1(zlo + 1));
+    const double2 zh = make_double2(ld_sc1(zhi), ld_sc1(zhi + 1));
     {
-      const double* pin = a.part + ((size_t)par * G + min((unsigned)t, G - 1)) * MAXC;
+      const double* pin = a.part + ((size_t)par * G + min((unsigned)t, G - 1)) * PSTRIDE;
       const bool own = t < G;
 #pragma unroll
       for (int c = 0; c < MAXC; ++c) v[c] = ld_sc1(pin + min(c, cols - 1));
 #pragma unroll
       for (int c = 0; c < MAXC; ++c) v[c] = own ? v[c] : 0.0;
     }
-    block_sum<MAXC>([&](int c) -> double {
-      double x = 0.0;
-#pragma unroll
-      for (int q = 0; q < MAXC; ++q) x = q == c ? v[q] : x;  // (static register indexing)
-      return x;
-    }, cols, sh);
+    block_sum<MAXC>(v, cols, sh);
     if (t == 0) {  // the lagged-normalisation step (krylov.hip gmres_lag_kernel), on lane 0
       double vj = sh.vs[0];
       bool stop = false;
@@ -344,20 +356,12 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
     // u_{j+1} = z - sum_k c_k u_k on the own row and both ghost rows (neighbours' z from the
     // barrier's hand-off; beyond the grid the ghost stays zero)
     if (act) {
+#pragma unroll
       for (int r = 0; r < 3; ++r) {
         const int gr = g - 1 + r;
-        double2 w;
-        if (r == 1) {
-          w = z;
-        } else if (gr >= 0 && gr < n) {
-          const double* zin = a.zbuf + ((size_t)par * n + gr) * 2 * n;
-          w = make_double2(ld_sc1(zin + 2 * t), ld_sc1(zin + 2 * t + 1));
-        } else {
-          Urow(j + 1, r)[t] = z2;
-          continue;
-        }
+        double2 w = r == 0 ? zl : (r == 1 ? z : zh);
         for (int k = 0; k < K; ++k) w = csub(w, cmul(sh.coef[k], Urow(k, r)[t]));
-        Urow(j + 1, r)[t] = w;
+        Urow(j + 1, r)[t] = csel(gr >= 0 && gr < n, w, z2);
       }
     }
     __syncthreads();
@@ -365,14 +369,18 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
   if (!stopped) {
     // the cycle's last column needs |u_{stop_col+1}|: one more reduction round
     const int last = a.stop_col + 1;
-    const double un = act ? cabs2(Urow(last, 1)[tc]) : 0.0;
-    block_sum<MAXC>([&](int) { return un; }, 1, sh);
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) v[c] = 0.0;
+    v[0] = act ? cabs2(Urow(last, 1)[tc]) : 0.0;
+    block_sum<MAXC>(v, 1, sh);
     const int par = epoch & 1;
-    if (t == 0) st_sc1(a.part + ((size_t)par * G + g) * MAXC, sh.sum[0]);
+    if (t == 0) st_sc1(a.part + ((size_t)par * G + g) * PSTRIDE, sh.sum[0]);
     epoch++;
     if (!grid_barrier(a.bar, epoch * G, a.timeout_word, sh.ctl)) return;
-    const double pq = t < G ? ld_sc1(a.part + ((size_t)par * G + t) * MAXC) : 0.0;
-    block_sum<MAXC>([&](int) { return pq; }, 1, sh);
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) v[c] = 0.0;
+    v[0] = t < G ? ld_sc1(a.part + ((size_t)par * G + t) * PSTRIDE) : 0.0;
+    block_sum<MAXC>(v, 1, sh);
     if (t == 0) {
       const double sg = sqrt(sh.sum[0]);
       const int col = a.stop_col;
@@ -415,15 +423,15 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
 size_t small_cycle_lds_bytes(int n, int restart) {
   const size_t R1 = restart + 1;
   auto al = [](size_t b) { return (b + 15) / 16 * 16; };
-  constexpr int MAXC = 2 * (kMaxProj + 1) + 2;
+  constexpr int PSTRIDE = 2 * (kMaxProj + 1) + 2;
   return al(16 * R1 * 3 * n) + al(16 * (size_t)restart * R1) + al(32 * (size_t)restart) +
          2 * al(16 * R1) + 2 * al(8 * R1) + al(8 * (size_t)restart) +
-         al(8 * (size_t)MAXC * (kSmallThreads / kWave)) + al(8 * MAXC) + al(16);
+         al(8 * (size_t)PSTRIDE * (kSmallThreads / kWave)) + al(8 * PSTRIDE) + al(16);
 }
 
 size_t small_cycle_scratch_doubles(int n) {
-  constexpr int MAXC = 2 * (kMaxProj + 1) + 2;
-  return 2 * (size_t)n * 2 * n + 2 * (size_t)n * MAXC;
+  constexpr int PSTRIDE = 2 * (kMaxProj + 1) + 2;
+  return 2 * (size_t)n * 2 * n + 2 * (size_t)n * PSTRIDE;
 }
 
 bool small_cycle_eligible(int n, int restart) {
@@ -431,14 +439,22 @@ bool small_cycle_eligible(int n, int restart) {
          small_cycle_lds_bytes(n, restart) <= (size_t)150 * 1024;
 }
 
-template <bool C, bool J>
-void launch_one(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s) {
+template <bool C, bool J, int MAXC>
+void launch_mc(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s) {
   // dynamic LDS above 64 KB (gfx950 has 160 KB per CU) must be allowed per kernel, once
   static const hipError_t attr = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(&gmres_small_cycle_kernel<C, J>),
+      reinterpret_cast<const void*>(&gmres_small_cycle_kernel<C, J, MAXC>),
       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)attr;
-  hipLaunchKernelGGL((gmres_small_cycle_kernel<C, J>), grid, block, lds, s, a);
+  hipLaunchKernelGGL((gmres_small_cycle_kernel<C, J, MAXC>), grid, block, lds, s, a);
+}
+template <bool C, bool J>
+void launch_one(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s) {
+  const int cols = 2 * (a.restart + 1) + 2;  // registers per thread for the partial sums
+  if (cols <= 12) launch_mc<C, J, 12>(a, grid, block, lds, s);
+  else if (cols <= 24) launch_mc<C, J, 24>(a, grid, block, lds, s);
+  else if (cols <= 44) launch_mc<C, J, 44>(a, grid, block, lds, s);
+  else launch_mc<C, J, 2 * (kMaxProj + 1) + 2>(a, grid, block, lds, s);
 }
 
 void launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi, hipStream_t s) {

@@ -49,9 +49,9 @@ def test_small_cycle_matches_reference_golden(ctx, name):
     assert info == int(z["info"]) and len(hist) == int(z["niter"])
     assert np.max(np.abs(hist - z["history"]) / z["history"]) < TOL
     assert relerr(x, z["x"]) < TOL
-    xo, _, ho = out["off"]
-    assert np.max(np.abs(hist - ho) / ho) < 1e-10
-    assert relerr(x, xo) < 1e-10
+    xo, _, ho = out["off"]  # (other summation order, lagged normalisation: rounding only)
+    assert np.max(np.abs(hist - ho) / ho) < 1e-9
+    assert relerr(x, xo) < 1e-9
 
 
 @pytest.mark.parametrize("n,kind,precond,restart,K", [
