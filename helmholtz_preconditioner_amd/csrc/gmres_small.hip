@@ -258,6 +258,18 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
 
   unsigned epoch = 0;
   const unsigned G = gridDim.x;
+  // optional phase timing (workgroup 0, thread 0; s_memrealtime ticks): 0 stencil + partial
+  // sums, 1 barrier, 2 partial reduction, 3 lagged Givens step, 4 basis update
+  const bool prof = a.phase_ticks != nullptr && g == 0 && t == 0;
+  unsigned long long tk[5] = {0, 0, 0, 0, 0};
+  unsigned long long tprev = prof ? wall_clock64() : 0;
+  auto tick = [&](int ph) {
+    if (prof) {
+      const unsigned long long now = wall_clock64();
+      tk[ph] += now - tprev;
+      tprev = now;
+    }
+  };
   double v[MAXC];
   bool stopped = false;
   int j = 0;
@@ -303,8 +315,10 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
     block_sum<MAXC>(v, cols, sh);
     double* pout = a.part + ((size_t)par * G + g) * PSTRIDE;
     if ((int)t < cols) st_sc1(pout + t, sh.sum[t]);
+    tick(0);
     epoch++;
     if (!grid_barrier(a.bar, epoch * G, a.timeout_word, sh.ctl)) return;
+    tick(1);
     // every workgroup sums all partials in the same order: thread q holds workgroup q's row
     // (G <= blockDim), every load in flight at once (unconditional, clamped columns), and the
     // neighbours' z rows (for the ghost update below) loaded alongside
@@ -322,6 +336,7 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
       for (int c = 0; c < MAXC; ++c) v[c] = own ? v[c] : 0.0;
     }
     block_sum<MAXC>(v, cols, sh);
+    tick(2);
     if (t == 0) {  // the lagged-normalisation step (krylov.hip gmres_lag_kernel), on lane 0
       double vj = sh.vs[0];
       bool stop = false;
@@ -349,6 +364,7 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
       sh.ctl[0] = stop ? 1 : 0;
     }
     __syncthreads();
+    tick(3);
     if (sh.ctl[0]) {
       stopped = true;
       break;
@@ -365,7 +381,10 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
       }
     }
     __syncthreads();
+    tick(4);
   }
+  if (prof)
+    for (int q = 0; q < 5; ++q) a.phase_ticks[q] += tk[q];
   if (!stopped) {
     // the cycle's last column needs |u_{stop_col+1}|: one more reduction round
     const int last = a.stop_col + 1;

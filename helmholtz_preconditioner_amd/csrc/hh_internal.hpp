@@ -228,6 +228,7 @@ struct SmallCycleArgs {
   double* part;            // [2][n][2 (kMaxProj + 1) + 2] partial sums
   unsigned* bar;           // arrival counter (zeroed before every launch)
   unsigned* timeout_word;  // set when a barrier wait gives up
+  unsigned long long* phase_ticks;  // optional [8]: workgroup 0's wall-clock ticks per phase
 };
 bool small_cycle_eligible(int n, int restart);
 size_t small_cycle_lds_bytes(int n, int restart);

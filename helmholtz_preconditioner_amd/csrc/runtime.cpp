@@ -144,6 +144,7 @@ struct hh_op {
   int small_cycle = -1;     // -1 auto, 0 off, 1 on where eligible (hh_op_set_small_cycle)
   double* small_scr = nullptr;
   unsigned* small_bar = nullptr;  // [4]: arrival counter, timeout word (16 B, zeroed per launch)
+  unsigned long long* small_ticks = nullptr;  // phase timing of the small cycle (diagnostic)
   // timing hooks
   hipEvent_t tk0 = nullptr, tk1 = nullptr;
   // device stop flag of the GMRES cycle being queued (nullptr outside hh_gmres)
@@ -988,6 +989,7 @@ static void op_release(hh_op* op) {
   dfree(op->npart);
   dfree(op->small_scr);
   dfree(op->small_bar);
+  dfree(op->small_ticks);
   dfree(op->sw_P);
   dfree(op->sw_y);
   dfree(op->sw_uF);
@@ -1427,6 +1429,27 @@ HH_API int hh_op_set_small_cycle(hh_op* op, int mode) {
   GUARD_END
 }
 
+HH_API int hh_op_small_cycle_profile(hh_op* op, int enable, double* phase_us) {
+  GUARD_BEGIN
+  REQUIRE(op, "null op");
+  HIPC(hipSetDevice(op->ctx->device));
+  if (phase_us && op->small_ticks) {
+    unsigned long long t[8];
+    HIPC(hipMemcpy(t, op->small_ticks, sizeof(t), hipMemcpyDeviceToHost));
+    int mhz = 100;  // s_memrealtime: a constant 100 MHz clock on gfx9
+    (void)hipDeviceGetAttribute(&mhz, hipDeviceAttributeWallClockRate, op->ctx->device);
+    const double khz = mhz > 0 ? (double)mhz : 100000.0;  // (the attribute is in kHz)
+    for (int q = 0; q < 8; ++q) phase_us[q] = t[q] * 1e3 / khz;
+  }
+  if (enable && !op->small_ticks) op->small_ticks = dalloc<unsigned long long>(8);
+  if (op->small_ticks) HIPC(hipMemset(op->small_ticks, 0, 8 * sizeof(unsigned long long)));
+  if (!enable) {
+    dfree(op->small_ticks);
+    op->small_ticks = nullptr;
+  }
+  GUARD_END
+}
+
 HH_API int hh_op_sl_fusion(hh_op* op, int enable) {
   GUARD_BEGIN
   REQUIRE(op, "null op");
@@ -1654,6 +1677,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       sa.part = op->small_scr + 2 * (size_t)op->n * 2 * op->n;
       sa.bar = op->small_bar;
       sa.timeout_word = op->small_bar + 1;
+      sa.phase_ticks = op->small_ticks;
       HIPC(hipMemsetAsync(op->small_bar, 0, 4 * sizeof(unsigned), s));
       launch_small_cycle(sa, op->const_c, op->pkind == HH_PREC_JACOBI, s);
       HIPC(hipGetLastError());

@@ -222,6 +222,11 @@ int hh_op_set_krylov_mode(hh_op* op, int mode);
  * used when it applies and n^2 <= 2^18; 1: whenever it applies; 0: never.  Results agree with the
  * regular cycle to rounding. */
 int hh_op_set_small_cycle(hh_op* op, int mode);
+/* Diagnostic: phase timing of the small-grid cycle kernel (workgroup 0's wall clock summed over
+ * the following solves): phase_us (optional, 8 doubles) receives the totals so far in us
+ * (0 stencil + partial sums, 1 grid barrier, 2 partial reduction, 3 lagged Givens step, 4 basis
+ * update), then the counters restart (enable = 1) or stop (enable = 0). */
+int hh_op_small_cycle_profile(hh_op* op, int enable, double* phase_us);
 /* Performance tuning of the stencil kernel used by HH_APPLY_A: variant in [0, 48) selects the
  * marching kernel's W/E exchange (LDS row / direct cached loads / wave shuffle), prefetch depth,
  * load/store cache policy and strip width, 96 + R (R = 2 .. 8 rows, + 16 / + 32 cache-policy

@@ -1,0 +1,43 @@
+"""Where the time of the small-grid whole-cycle GMRES kernel goes (BASELINE config 1 by default):
+per-phase wall-clock totals of workgroup 0 (hh_op_small_cycle_profile) per inner iteration, and
+the solve's iterations per second with the kernel on and off.
+usage: python tools/prof_small_cycle.py [--n 128] [--iters 200] [--precond none|jacobi]"""
+import argparse
+import ctypes
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import helmholtz_preconditioner_amd as H  # noqa: E402
+from helmholtz_preconditioner_amd import _ffi  # noqa: E402
+
+p = argparse.ArgumentParser()
+p.add_argument("--n", type=int, default=128)
+p.add_argument("--iters", type=int, default=200)
+p.add_argument("--wave-num", type=float, default=8.0)
+p.add_argument("--precond", default="none")
+a = p.parse_args()
+n = a.n
+om, h, eta = H.problem_params(n, 12, a.wave_num, 2.0)
+A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.constant_c_mat(n))
+f = A.vector(H.init_f1_mat(.5, .125, om, n).ravel())
+M = None if a.precond == "none" else "jacobi"
+for mode in ("on", "off", "on"):
+    A.small_cycle(mode)
+    H.gmres(A, f, rtol=1e-14, restart=20, maxiter=20, M=M, callback=lambda r: None,
+            callback_type="legacy")
+    ph = (ctypes.c_double * 8)()
+    _ffi.check(_ffi.lib.hh_op_small_cycle_profile(A.handle, 1, ph))
+    t0 = time.perf_counter()
+    H.gmres(A, f, rtol=1e-14, restart=20, maxiter=a.iters, M=M, callback=lambda r: None,
+            callback_type="legacy")
+    dt = time.perf_counter() - t0
+    _ffi.check(_ffi.lib.hh_op_small_cycle_profile(A.handle, 0, ph))
+    per = [ph[q] / a.iters for q in range(5)]
+    print(f"n={n} small_cycle={mode}: {a.iters / dt:9.1f} it/s ({dt / a.iters * 1e6:6.2f} us/it)"
+          + ("" if mode == "off" else
+             "  phases us/it: stencil+dots %.2f barrier %.2f reduce %.2f givens %.2f update %.2f"
+             % tuple(per)), flush=True)
