@@ -63,6 +63,7 @@ using l1 = HH_LDS double;
 using li = HH_LDS int;
 struct Shared {  // LDS layout (carved from dynamic shared memory; see small_cycle_lds_bytes)
   l2* U;     // [R1][3][n]: rows 0 = g-1 (ghost), 1 = g (own), 2 = g+1 (ghost)
+  l2* zrow;  // [n] this iteration's z on the own row
   l2* H;     // [R][R1]
   l2* Gr;    // [R][2] Givens (c, s)
   l2* S;     // [R1]
@@ -70,21 +71,35 @@ struct Shared {  // LDS layout (carved from dynamic shared memory; see small_cyc
   l1* vs;    // [R1] exact 1 / |u_k|
   l1* ss;    // [R1] scale of each SpMV input
   l1* h0s;   // [R]
-  l1* wred;  // [waves][W] per-wave partial sums
-  l1* sum;   // [W] reduced sums
+  l1* red;   // [kSmallThreads] chunk sums of the partial reduction
+  l1* sum;   // [PSTRIDE] reduced sums
   li* ctl;   // [4]: 0 stop, 1 last column, 2 abort
 };
 
-// agent-scope arrival counter (zeroed before the launch): every storing wave has drained its
-// sc1 stores, one lane adds, lane 0 of wave 0 polls with relaxed sc1 loads until all `blocks`
-// workgroups have arrived `epoch` times.  Returns false on timeout (every workgroup then exits).
-__device__ bool grid_barrier(unsigned* counter, unsigned target, unsigned* timeout_word, li* ctl) {
+// Two-level arrival barrier (zeroed before the launch): workgroups are grouped by blockIdx % 8
+// (the dispatcher's XCD round-robin: a performance grouping only, correctness never depends on
+// it); each adds to its group's counter with an agent-scope atomic, the group's last arriver (told
+// by the value its add returns) adds to the top counter, and thread 0 of every workgroup polls
+// the top counter with relaxed sc1 loads.  Every storing wave drains vmcnt first (the hand-off
+// form of MI355X_MICROARCH.md: sc1 stores, one lane's counter add per workgroup, sc1 loads of
+// the handed-off bytes after the poll and a workgroup barrier).  Bounded spin: false on timeout.
+__device__ bool grid_barrier(unsigned* words, unsigned epoch, unsigned G, unsigned* timeout_word,
+                             li* ctl) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned grp = blockIdx.x & 7;
+    const unsigned ngroups = G < 8 ? G : 8;
+    const unsigned gsize = (G - grp + 7) / 8;  // workgroups with this blockIdx % 8
+    unsigned* top = words;                     // words[0]: top counter; [4 + 16 grp]: groups
+    unsigned* mine = words + 4 + 16 * grp;     // (a 64-B line per counter)
+    const unsigned old =
+        __hip_atomic_fetch_add((gu32*)mine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == epoch * gsize)
+      __hip_atomic_fetch_add((gu32*)top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned spins = 0;
-    while (__hip_atomic_load((gu32*)counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    while (__hip_atomic_load((gu32*)top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+           epoch * ngroups) {
       __builtin_amdgcn_s_sleep(1);
       if (++spins > kSpinLimit) {
         __hip_atomic_store((gu32*)timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -95,32 +110,6 @@ __device__ bool grid_barrier(unsigned* counter, unsigned target, unsigned* timeo
   }
   __syncthreads();
   return ctl[2] == 0;
-}
-
-// fixed-order block reduction of the per-thread registers v[0 .. cols) into sh.sum: a butterfly
-// in every wave -- all MAXC columns interleaved, so the shuffle latencies overlap -- then the
-// waves in index order.  Identical on every workgroup for identical inputs (lane 0's sum).
-template <int MAXC>
-__device__ __forceinline__ void block_sum(double (&v)[MAXC], int cols, const Shared& sh) {
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  const int waves = (blockDim.x + kWave - 1) / kWave;
-#pragma unroll
-  for (int off = kWave / 2; off > 0; off >>= 1) {
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) v[c] += __shfl_xor(v[c], off);
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c)
-      if (c < cols) sh.wred[wave * MAXC + c] = v[c];
-  }
-  __syncthreads();
-  if ((int)threadIdx.x < cols) {
-    double s = 0.0;
-    for (int w = 0; w < waves; ++w) s += sh.wred[w * MAXC + threadIdx.x];
-    sh.sum[threadIdx.x] = s;
-  }
-  __syncthreads();
 }
 
 // LAPACK zlartg main branch (krylov.hip)
@@ -194,16 +183,17 @@ __device__ bool finish_column(const Shared& sh, const SmallCycleArgs& a, int col
   return presid <= a.ptol || brk != 0.0 || col >= a.stop_col;
 }
 
-// MAXC: partial-sum columns held in registers, >= 2 (restart + 1) + 2 (instantiated per
-// restart range, launch_small_cycle)
-template <bool CONSTC, bool JAC, int MAXC>
+constexpr int kPStride = 2 * (kMaxProj + 1) + 2;  // partial-sum columns (global layout)
+constexpr int kChunk = 64;                         // partial sums one thread loads in flight
+
+template <bool CONSTC, bool JAC>
 __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallCycleArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = a.n, R = a.restart, R1 = R + 1;
-  constexpr int PSTRIDE = 2 * (kMaxProj + 1) + 2;  // row stride of the global partials
-  const int g = blockIdx.x, t = threadIdx.x;
+  const int g = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
   const bool act = t < n;
   const int tc = min(t, n - 1);
+  const unsigned G = gridDim.x;
   Shared sh;
   {
     using lc = HH_LDS char;
@@ -214,6 +204,7 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
       return q;
     };
     sh.U = (l2*)take(sizeof(double2) * (size_t)R1 * 3 * n);
+    sh.zrow = (l2*)take(sizeof(double2) * n);
     sh.H = (l2*)take(sizeof(double2) * (size_t)R * R1);
     sh.Gr = (l2*)take(sizeof(double2) * 2 * (size_t)R);
     sh.S = (l2*)take(sizeof(double2) * R1);
@@ -221,12 +212,14 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
     sh.vs = (l1*)take(sizeof(double) * R1);
     sh.ss = (l1*)take(sizeof(double) * R1);
     sh.h0s = (l1*)take(sizeof(double) * R);
-    sh.wred = (l1*)take(sizeof(double) * PSTRIDE * (kSmallThreads / kWave));
-    sh.sum = (l1*)take(sizeof(double) * PSTRIDE);
+    sh.red = (l1*)take(sizeof(double) * kSmallThreads);
+    sh.sum = (l1*)take(sizeof(double) * kPStride);
     sh.ctl = (li*)take(sizeof(int) * 4);
   }
   auto Urow = [&](int k, int r) -> l2* { return sh.U + ((size_t)k * 3 + r) * n; };
   const double2 z2 = make_double2(0.0, 0.0);
+  // global partial sums, column-major: part[parity][column][workgroup]
+  auto pcol = [&](int par, int c) { return a.part + ((size_t)par * kPStride + c) * G; };
 
   // operator coefficients of this thread's point (stencil.hip's formulas; row g, column t)
   const double2 AW = a.tab_i[tc], AE = a.tab_i[n + tc], R1c = a.tab_i[2 * n + tc];
@@ -256,8 +249,37 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
   }
   __syncthreads();
 
+  // the fixed-order sum over all workgroups of `cols` partial columns into sh.sum: thread t
+  // takes column t / hq and the t % hq-th chunk of the workgroups (loads in flight together),
+  // then the chunk sums of a column add up in chunk order.  Identical on every workgroup.
+  auto reduce_partials = [&](int par, int cols) {
+    const int hq = max(1, min(nt / cols, (int)G));
+    const int chunk = ((int)G + hq - 1) / hq;
+    const int c = t / hq, h = t % hq;
+    double s = 0.0;
+    if (c < cols) {
+      const double* col = pcol(par, c);
+      const int q0 = h * chunk, q1 = min((int)G, q0 + chunk);
+      for (int b = q0; b < q1; b += kChunk) {
+        double v[kChunk];
+#pragma unroll
+        for (int i = 0; i < kChunk; ++i) v[i] = ld_sc1(col + min(b + i, q1 - 1));
+#pragma unroll
+        for (int i = 0; i < kChunk; ++i)
+          if (b + i < q1) s += v[i];
+      }
+      sh.red[t] = s;
+    }
+    __syncthreads();
+    if (t < cols) {
+      double r = 0.0;
+      for (int q = 0; q < hq; ++q) r += sh.red[t * hq + q];
+      sh.sum[t] = r;
+    }
+    __syncthreads();
+  };
+
   unsigned epoch = 0;
-  const unsigned G = gridDim.x;
   // optional phase timing (workgroup 0, thread 0; s_memrealtime ticks): 0 stencil + partial
   // sums, 1 barrier, 2 partial reduction, 3 lagged Givens step, 4 basis update
   const bool prof = a.phase_ticks != nullptr && g == 0 && t == 0;
@@ -270,10 +292,8 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
       tprev = now;
     }
   };
-  double v[MAXC];
   bool stopped = false;
-  int j = 0;
-  for (; j <= a.stop_col; ++j) {
+  for (int j = 0; j <= a.stop_col; ++j) {
     const int K = j + 1;
     // z = M A (s_j u_j) on the own row (zero Dirichlet rows beyond the grid are zero ghosts)
     // (by-value selects of loads from clamped columns: a select of lvalues would become a
@@ -289,86 +309,102 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
     Au = cfma(E, uE, Au);
     Au = cfma(N, uN, Au);
     const double sj = sh.ss[j];
-    double2 z = JAC ? cscale(cdiv(Au, D), sj) : cscale(Au, sj);
-    if (!act) z = z2;
-    // hand the z row to the neighbours (sc1 stores), partial sums of the own row
+    const double2 z = csel(act, JAC ? cscale(cdiv(Au, D), sj) : cscale(Au, sj), z2);
+    // hand the z row to the neighbours (sc1 stores); keep it in LDS for the partial sums
     const int par = epoch & 1;
     double* zout = a.zbuf + ((size_t)par * n + g) * 2 * n;
     if (act) {
       st_sc1(zout + 2 * t, z.x);
       st_sc1(zout + 2 * t + 1, z.y);
+      sh.zrow[t] = z;
     }
-    const int cols = 2 * K + 2;
-    // per column: conj(u_k) z (re, im) for k < K, |z|^2, |u_j|^2 of the own row (lagged norm)
-#pragma unroll
-    for (int k = 0; k < MAXC / 2; ++k) {
-      double2 dk = z2;
-      if (k < K) dk = cfma_conj(csel(act, Urow(k, 1)[tc], z2), z, z2);
-      v[2 * k] = dk.x;
-      v[2 * k + 1] = dk.y;
+    __syncthreads();
+    // partial sums of the own row, one thread per column, points in a fixed order (two
+    // interleaved accumulators): conj(u_k) z for k < K, |z|^2 (thread K), |u_j|^2 (K + 1)
+    if (t <= K + 1) {
+      double2 a0 = z2, a1 = z2;
+      const l2* uk = Urow(min(t, j), 1);
+      int p = 0;
+      for (; p + 1 < n; p += 2) {
+        const double2 z0 = sh.zrow[p], zq = sh.zrow[p + 1];
+        const double2 u0 = uk[p], uq = uk[p + 1];
+        if (t < K) {
+          a0 = cfma_conj(u0, z0, a0);
+          a1 = cfma_conj(uq, zq, a1);
+        } else if (t == K) {
+          a0.x = fma(z0.x, z0.x, fma(z0.y, z0.y, a0.x));
+          a1.x = fma(zq.x, zq.x, fma(zq.y, zq.y, a1.x));
+        } else {
+          a0.x = fma(u0.x, u0.x, fma(u0.y, u0.y, a0.x));
+          a1.x = fma(uq.x, uq.x, fma(uq.y, uq.y, a1.x));
+        }
+      }
+      if (p < n) {
+        const double2 z0 = sh.zrow[p], u0 = uk[p];
+        if (t < K) a0 = cfma_conj(u0, z0, a0);
+        else if (t == K) a0.x = fma(z0.x, z0.x, fma(z0.y, z0.y, a0.x));
+        else a0.x = fma(u0.x, u0.x, fma(u0.y, u0.y, a0.x));
+      }
+      const double2 d = cadd(a0, a1);
+      if (t < K) {
+        st_sc1(pcol(par, 2 * t) + g, d.x);
+        st_sc1(pcol(par, 2 * t + 1) + g, d.y);
+      } else if (t == K) {
+        st_sc1(pcol(par, 2 * K) + g, d.x);
+      } else {
+        st_sc1(pcol(par, 2 * K + 1) + g, j > 0 ? d.x : 0.0);
+      }
     }
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      if (c == 2 * K) v[c] = fma(z.x, z.x, z.y * z.y);
-      if (c == 2 * K + 1) v[c] = j > 0 ? cabs2(uC) : 0.0;
-    }
-    block_sum<MAXC>(v, cols, sh);
-    double* pout = a.part + ((size_t)par * G + g) * PSTRIDE;
-    if ((int)t < cols) st_sc1(pout + t, sh.sum[t]);
     tick(0);
     epoch++;
-    if (!grid_barrier(a.bar, epoch * G, a.timeout_word, sh.ctl)) return;
+    if (!grid_barrier(a.bar, epoch, G, a.timeout_word, sh.ctl)) return;
     tick(1);
-    // every workgroup sums all partials in the same order: thread q holds workgroup q's row
-    // (G <= blockDim), every load in flight at once (unconditional, clamped columns), and the
-    // neighbours' z rows (for the ghost update below) loaded alongside
+    // the neighbours' z rows (for the ghost update below) in flight with the partial sums
     const int glo = min(max(g - 1, 0), n - 1), ghi = min(g + 1, n - 1);
     const double* zlo = a.zbuf + ((size_t)par * n + glo) * 2 * n + 2 * tc;
     const double* zhi = a.zbuf + ((size_t)par * n + ghi) * 2 * n + 2 * tc;
     const double2 zl = make_double2(ld_sc1(zlo), ld_sc1(zlo + 1));
     const double2 zh = make_double2(ld_sc1(zhi), ld_sc1(zhi + 1));
-    {
-      const double* pin = a.part + ((size_t)par * G + min((unsigned)t, G - 1)) * PSTRIDE;
-      const bool own = t < G;
-#pragma unroll
-      for (int c = 0; c < MAXC; ++c) v[c] = ld_sc1(pin + min(c, cols - 1));
-#pragma unroll
-      for (int c = 0; c < MAXC; ++c) v[c] = own ? v[c] : 0.0;
-    }
-    block_sum<MAXC>(v, cols, sh);
+    reduce_partials(par, 2 * K + 2);
     tick(2);
-    if (t == 0) {  // the lagged-normalisation step (krylov.hip gmres_lag_kernel), on lane 0
-      double vj = sh.vs[0];
+    // the lagged-normalisation step (krylov.hip gmres_lag_kernel): column j-1 finished on
+    // lane 0 (sequential rotations), column j started by one thread per entry
+    if (t == 0) {
       bool stop = false;
       if (j >= 1) {
         const double sg = sqrt(sh.sum[2 * K + 1]);
-        vj = 1.0 / sg;
         const int col = j - 1;
-        stop = finish_column(sh, a, col, sg * sh.vs[col] / sh.ss[col], vj);
-      }
-      if (!stop) {
-        const double f = vj / sh.ss[j];
-        l2* h = sh.H + (size_t)j * R1;
-        const double w2 = sh.sum[2 * K];
-        double rest = w2;
-        for (int k = 0; k <= j; ++k) {
-          const double vk = k == j ? vj : sh.vs[k];
-          const double2 d = make_double2(sh.sum[2 * k], sh.sum[2 * k + 1]);
-          h[k] = cscale(cscale(d, vk), f);
-          rest -= cabs2(d) * vk * vk;
-          sh.coef[k] = cscale(cscale(d, vk), vk);  // krylov.hip update_kernel's coefficient
-        }
-        sh.h0s[j] = sqrt(w2) * f;
-        sh.ss[j + 1] = 1.0 / sqrt(fmax(rest, fmax(w2 * 1e-28, 1e-300)));
+        stop = finish_column(sh, a, col, sg * sh.vs[col] / sh.ss[col], 1.0 / sg);
+        sh.vs[j] = 1.0 / sg;  // (also on breakdown: unused then)
       }
       sh.ctl[0] = stop ? 1 : 0;
     }
     __syncthreads();
-    tick(3);
     if (sh.ctl[0]) {
+      tick(3);
       stopped = true;
       break;
     }
+    const double vj = sh.vs[j];
+    const double f = vj / sh.ss[j];
+    if (t <= j) {
+      const double vk = sh.vs[t];
+      const double2 d = make_double2(sh.sum[2 * t], sh.sum[2 * t + 1]);
+      sh.H[(size_t)j * R1 + t] = cscale(cscale(d, vk), f);
+      sh.coef[t] = cscale(cscale(d, vk), vk);  // krylov.hip update_kernel's coefficient
+    }
+    if (t == 0) {
+      const double w2 = sh.sum[2 * K];
+      double rest = w2;
+      for (int k = 0; k <= j; ++k) {
+        const double vk = sh.vs[k];
+        rest -= cabs2(make_double2(sh.sum[2 * k], sh.sum[2 * k + 1])) * vk * vk;
+      }
+      sh.h0s[j] = sqrt(w2) * f;
+      sh.ss[j + 1] = 1.0 / sqrt(fmax(rest, fmax(w2 * 1e-28, 1e-300)));
+    }
+    __syncthreads();
+    tick(3);
     // u_{j+1} = z - sum_k c_k u_k on the own row and both ghost rows (neighbours' z from the
     // barrier's hand-off; beyond the grid the ghost stays zero)
     if (act) {
@@ -388,18 +424,16 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
   if (!stopped) {
     // the cycle's last column needs |u_{stop_col+1}|: one more reduction round
     const int last = a.stop_col + 1;
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) v[c] = 0.0;
-    v[0] = act ? cabs2(Urow(last, 1)[tc]) : 0.0;
-    block_sum<MAXC>(v, 1, sh);
     const int par = epoch & 1;
-    if (t == 0) st_sc1(a.part + ((size_t)par * G + g) * PSTRIDE, sh.sum[0]);
+    if (t == 0) {
+      const l2* ul = Urow(last, 1);
+      double s = 0.0;
+      for (int p = 0; p < n; ++p) s = fma(ul[p].x, ul[p].x, fma(ul[p].y, ul[p].y, s));
+      st_sc1(pcol(par, 0) + g, s);
+    }
     epoch++;
-    if (!grid_barrier(a.bar, epoch * G, a.timeout_word, sh.ctl)) return;
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) v[c] = 0.0;
-    v[0] = t < G ? ld_sc1(a.part + ((size_t)par * G + t) * PSTRIDE) : 0.0;
-    block_sum<MAXC>(v, 1, sh);
+    if (!grid_barrier(a.bar, epoch, G, a.timeout_word, sh.ctl)) return;
+    reduce_partials(par, 1);
     if (t == 0) {
       const double sg = sqrt(sh.sum[0]);
       const int col = a.stop_col;
@@ -442,15 +476,13 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
 size_t small_cycle_lds_bytes(int n, int restart) {
   const size_t R1 = restart + 1;
   auto al = [](size_t b) { return (b + 15) / 16 * 16; };
-  constexpr int PSTRIDE = 2 * (kMaxProj + 1) + 2;
-  return al(16 * R1 * 3 * n) + al(16 * (size_t)restart * R1) + al(32 * (size_t)restart) +
-         2 * al(16 * R1) + 2 * al(8 * R1) + al(8 * (size_t)restart) +
-         al(8 * (size_t)PSTRIDE * (kSmallThreads / kWave)) + al(8 * PSTRIDE) + al(16);
+  return al(16 * R1 * 3 * n) + al(16 * (size_t)n) + al(16 * (size_t)restart * R1) +
+         al(32 * (size_t)restart) + 2 * al(16 * R1) + 2 * al(8 * R1) + al(8 * (size_t)restart) +
+         al(8 * (size_t)kSmallThreads) + al(8 * kPStride) + al(16);
 }
 
 size_t small_cycle_scratch_doubles(int n) {
-  constexpr int PSTRIDE = 2 * (kMaxProj + 1) + 2;
-  return 2 * (size_t)n * 2 * n + 2 * (size_t)n * PSTRIDE;
+  return 2 * (size_t)n * 2 * n + 2 * (size_t)kPStride * n;
 }
 
 bool small_cycle_eligible(int n, int restart) {
@@ -458,22 +490,14 @@ bool small_cycle_eligible(int n, int restart) {
          small_cycle_lds_bytes(n, restart) <= (size_t)150 * 1024;
 }
 
-template <bool C, bool J, int MAXC>
-void launch_mc(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s) {
-  // dynamic LDS above 64 KB (gfx950 has 160 KB per CU) must be allowed per kernel, once
-  static const hipError_t attr = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(&gmres_small_cycle_kernel<C, J, MAXC>),
-      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)attr;
-  hipLaunchKernelGGL((gmres_small_cycle_kernel<C, J, MAXC>), grid, block, lds, s, a);
-}
 template <bool C, bool J>
 void launch_one(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s) {
-  const int cols = 2 * (a.restart + 1) + 2;  // registers per thread for the partial sums
-  if (cols <= 12) launch_mc<C, J, 12>(a, grid, block, lds, s);
-  else if (cols <= 24) launch_mc<C, J, 24>(a, grid, block, lds, s);
-  else if (cols <= 44) launch_mc<C, J, 44>(a, grid, block, lds, s);
-  else launch_mc<C, J, 2 * (kMaxProj + 1) + 2>(a, grid, block, lds, s);
+  // dynamic LDS above 64 KB (gfx950 has 160 KB per CU) must be allowed per kernel, once
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&gmres_small_cycle_kernel<C, J>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)attr;
+  hipLaunchKernelGGL((gmres_small_cycle_kernel<C, J>), grid, block, lds, s, a);
 }
 
 void launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi, hipStream_t s) {

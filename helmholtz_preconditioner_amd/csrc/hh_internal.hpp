@@ -226,10 +226,13 @@ struct SmallCycleArgs {
   double eps, ptol;
   double* zbuf;            // [2][n][2n]  z rows handed to the neighbours
   double* part;            // [2][n][2 (kMaxProj + 1) + 2] partial sums
-  unsigned* bar;           // arrival counter (zeroed before every launch)
+  unsigned* bar;           // barrier words (kSmallBarWords, zeroed before every launch)
   unsigned* timeout_word;  // set when a barrier wait gives up
   unsigned long long* phase_ticks;  // optional [8]: workgroup 0's wall-clock ticks per phase
 };
+// barrier words of the small cycle: [0] top counter, [1] timeout word, [4 + 16 k] the counter
+// of workgroup group k (k < 8; one 64-B line each); zeroed before every launch
+constexpr int kSmallBarWords = 4 + 16 * 8;
 bool small_cycle_eligible(int n, int restart);
 size_t small_cycle_lds_bytes(int n, int restart);
 size_t small_cycle_scratch_doubles(int n);

@@ -1636,7 +1636,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
                      (op->small_cycle == 1 || (size_t)op->n * op->n <= ((size_t)1 << 18));
   if (small && !op->small_scr) {
     op->small_scr = dalloc<double>(small_cycle_scratch_doubles(op->n));
-    op->small_bar = dalloc<unsigned>(4);
+    op->small_bar = dalloc<unsigned>(kSmallBarWords);
   }
 
   for (long iteration = 0; iteration < maxiter; ++iteration) {
@@ -1676,9 +1676,9 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       sa.zbuf = op->small_scr;
       sa.part = op->small_scr + 2 * (size_t)op->n * 2 * op->n;
       sa.bar = op->small_bar;
-      sa.timeout_word = op->small_bar + 1;
+      sa.timeout_word = op->small_bar + 1;  // (words[4 ..]: the eight group counters)
       sa.phase_ticks = op->small_ticks;
-      HIPC(hipMemsetAsync(op->small_bar, 0, 4 * sizeof(unsigned), s));
+      HIPC(hipMemsetAsync(op->small_bar, 0, kSmallBarWords * sizeof(unsigned), s));
       launch_small_cycle(sa, op->const_c, op->pkind == HH_PREC_JACOBI, s);
       HIPC(hipGetLastError());
     }
