@@ -48,7 +48,8 @@ __device__ __forceinline__ double2 csel(bool c, double2 a, double2 b) {
   return make_double2(c ? a.x : b.x, c ? a.y : b.y);
 }
 
-constexpr int kSmallThreads = 256;    // block size cap (n <= 256)
+constexpr int kSmallThreads = 256;    // block size cap for the grid's rows (n <= 256)
+constexpr int kPStride = 2 * (kMaxProj + 1) + 2;  // partial-sum columns (global layout)
 constexpr unsigned kSpinLimit = 1u << 22;  // ~1 s of polling: a barrier wait is microseconds
 
 // LDS pointers carry address space 3 on the device (ds_ instructions, not flat ones); the host
@@ -76,40 +77,90 @@ struct Shared {  // LDS layout (carved from dynamic shared memory; see small_cyc
   li* ctl;   // [4]: 0 stop, 1 last column, 2 abort
 };
 
-// Two-level arrival barrier (zeroed before the launch): workgroups are grouped by blockIdx % 8
-// (the dispatcher's XCD round-robin: a performance grouping only, correctness never depends on
-// it); each adds to its group's counter with an agent-scope atomic, the group's last arriver (told
-// by the value its add returns) adds to the top counter, and thread 0 of every workgroup polls
-// the top counter with relaxed sc1 loads.  Every storing wave drains vmcnt first (the hand-off
-// form of MI355X_MICROARCH.md: sc1 stores, one lane's counter add per workgroup, sc1 loads of
-// the handed-off bytes after the poll and a workgroup barrier).  Bounded spin: false on timeout.
-__device__ bool grid_barrier(unsigned* words, unsigned epoch, unsigned G, unsigned* timeout_word,
-                             li* ctl) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// Grouped all-reduce of `cols` doubles per workgroup (the barrier words are zeroed before the
+// launch; rows/sums are double-buffered by `par`, so a round never overwrites what a slower
+// workgroup may still read from the round before):
+//  1. every workgroup publishes its row part[par][g][0 .. cols) (sc1 stores by threads < cols,
+//     every storing wave drains vmcnt, workgroup barrier) and thread 0 adds to its group's
+//     counter (groups: blockIdx % 8, the dispatcher's XCD round-robin -- a performance grouping
+//     only);
+//  2. the group's LAST arriver (told by the value its add returns) sums the group's rows in
+//     member order into gsum[par][grp] and adds to the top counter;
+//  3. the top counter's last arriver sums the group sums in group order into fsum[par], then
+//     raises the round's flag;
+//  4. everyone polls the flag (thread 0, relaxed sc1 loads, bounded) and reads fsum into LDS.
+// The arithmetic order is fixed whichever workgroup happens to be last: identical sums on every
+// workgroup and every run.  Hand-offs in MI355X_MICROARCH.md's valid form (sc1 stores drained
+// before one lane's agent-scope add or flag store; sc1 loads after the poll + a workgroup
+// barrier).  Returns false on timeout (every workgroup then leaves the kernel).
+struct ArArgs {
+  double* part;   // [2][G][kPStride]
+  double* gsum;   // [2][8][kPStride]
+  double* fsum;   // [2][kPStride]
+  unsigned* words;  // [0] top counter, [1] timeout, [2] flag, [4 + 16 grp] group counters
+};
+__device__ bool allreduce_rows(const ArArgs& ar, int par, unsigned epoch, int cols, l1* out,
+                               li* ctl) {
+  const unsigned G = gridDim.x, g = blockIdx.x, t = threadIdx.x;
+  const unsigned grp = g & 7;
+  const unsigned ngroups = G < 8 ? G : 8;
+  const unsigned gsize = (G - grp + 7) / 8;
+  unsigned* top = ar.words;
+  unsigned* tmo = ar.words + 1;
+  unsigned* flag = ar.words + 2;
+  unsigned* mine = ar.words + 4 + 16 * grp;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's row stores drained
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned grp = blockIdx.x & 7;
-    const unsigned ngroups = G < 8 ? G : 8;
-    const unsigned gsize = (G - grp + 7) / 8;  // workgroups with this blockIdx % 8
-    unsigned* top = words;                     // words[0]: top counter; [4 + 16 grp]: groups
-    unsigned* mine = words + 4 + 16 * grp;     // (a 64-B line per counter)
+  if (t == 0) {
     const unsigned old =
         __hip_atomic_fetch_add((gu32*)mine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1 == epoch * gsize)
-      __hip_atomic_fetch_add((gu32*)top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ctl[3] = old + 1 == epoch * gsize ? 1 : 0;
+  }
+  __syncthreads();
+  if (ctl[3]) {  // last of the group: the group sum, members in index order
+    if ((int)t < cols) {
+      double s = 0.0;
+      for (unsigned q = grp; q < G; q += 8)
+        s += ld_sc1(ar.part + ((size_t)par * G + q) * kPStride + t);
+      st_sc1(ar.gsum + ((size_t)par * 8 + grp) * kPStride + t, s);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      const unsigned old =
+          __hip_atomic_fetch_add((gu32*)top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ctl[3] = old + 1 == epoch * ngroups ? 2 : 0;
+    }
+    __syncthreads();
+    if (ctl[3] == 2) {  // last group: the final sums, groups in index order, then the flag
+      if ((int)t < cols) {
+        double s = 0.0;
+        for (unsigned k = 0; k < ngroups; ++k)
+          s += ld_sc1(ar.gsum + ((size_t)par * 8 + k) * kPStride + t);
+        st_sc1(ar.fsum + (size_t)par * kPStride + t, s);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0)
+        __hip_atomic_store((gu32*)flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (t == 0) {
     unsigned spins = 0;
-    while (__hip_atomic_load((gu32*)top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-           epoch * ngroups) {
+    while (__hip_atomic_load((gu32*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch) {
       __builtin_amdgcn_s_sleep(1);
       if (++spins > kSpinLimit) {
-        __hip_atomic_store((gu32*)timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ctl[2] = 1;
         break;
       }
     }
   }
   __syncthreads();
-  return ctl[2] == 0;
+  if (ctl[2]) return false;
+  if ((int)t < cols) out[t] = ld_sc1(ar.fsum + (size_t)par * kPStride + t);
+  __syncthreads();
+  return true;
 }
 
 // LAPACK zlartg main branch (krylov.hip)
@@ -183,14 +234,15 @@ __device__ bool finish_column(const Shared& sh, const SmallCycleArgs& a, int col
   return presid <= a.ptol || brk != 0.0 || col >= a.stop_col;
 }
 
-constexpr int kPStride = 2 * (kMaxProj + 1) + 2;  // partial-sum columns (global layout)
-constexpr int kChunk = 64;                         // partial sums one thread loads in flight
 
 template <bool CONSTC, bool JAC>
-__global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallCycleArgs a) {
+__global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kernel(SmallCycleArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = a.n, R = a.restart, R1 = R + 1;
   const int g = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+  // threads 0 .. nrow-1 own the row's columns; the last wave (lane `book`) keeps the books:
+  // it completes the previous Hessenberg column while the others update the basis
+  const int nrow = nt - kWave, book = nt - kWave;
   const bool act = t < n;
   const int tc = min(t, n - 1);
   const unsigned G = gridDim.x;
@@ -212,14 +264,17 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
     sh.vs = (l1*)take(sizeof(double) * R1);
     sh.ss = (l1*)take(sizeof(double) * R1);
     sh.h0s = (l1*)take(sizeof(double) * R);
-    sh.red = (l1*)take(sizeof(double) * kSmallThreads);
+    sh.red = (l1*)take(2 * sizeof(double) * (kSmallThreads + kWave));
     sh.sum = (l1*)take(sizeof(double) * kPStride);
     sh.ctl = (li*)take(sizeof(int) * 4);
   }
   auto Urow = [&](int k, int r) -> l2* { return sh.U + ((size_t)k * 3 + r) * n; };
   const double2 z2 = make_double2(0.0, 0.0);
-  // global partial sums, column-major: part[parity][column][workgroup]
-  auto pcol = [&](int par, int c) { return a.part + ((size_t)par * kPStride + c) * G; };
+  ArArgs ar;
+  ar.part = a.part;
+  ar.gsum = a.part + 2 * (size_t)G * kPStride;
+  ar.fsum = ar.gsum + 2 * 8 * (size_t)kPStride;
+  ar.words = a.bar;
 
   // operator coefficients of this thread's point (stencil.hip's formulas; row g, column t)
   const double2 AW = a.tab_i[tc], AE = a.tab_i[n + tc], R1c = a.tab_i[2 * n + tc];
@@ -245,43 +300,13 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
     sh.ss[0] = a.g.vscale[0];
     const double2 s0 = a.g.S[0];
     for (int k = 0; k < R1; ++k) sh.S[k] = csel(k == 0, s0, z2);
-    sh.ctl[0] = sh.ctl[1] = sh.ctl[2] = 0;
+    sh.ctl[0] = sh.ctl[1] = sh.ctl[2] = sh.ctl[3] = 0;
   }
   __syncthreads();
 
-  // the fixed-order sum over all workgroups of `cols` partial columns into sh.sum: thread t
-  // takes column t / hq and the t % hq-th chunk of the workgroups (loads in flight together),
-  // then the chunk sums of a column add up in chunk order.  Identical on every workgroup.
-  auto reduce_partials = [&](int par, int cols) {
-    const int hq = max(1, min(nt / cols, (int)G));
-    const int chunk = ((int)G + hq - 1) / hq;
-    const int c = t / hq, h = t % hq;
-    double s = 0.0;
-    if (c < cols) {
-      const double* col = pcol(par, c);
-      const int q0 = h * chunk, q1 = min((int)G, q0 + chunk);
-      for (int b = q0; b < q1; b += kChunk) {
-        double v[kChunk];
-#pragma unroll
-        for (int i = 0; i < kChunk; ++i) v[i] = ld_sc1(col + min(b + i, q1 - 1));
-#pragma unroll
-        for (int i = 0; i < kChunk; ++i)
-          if (b + i < q1) s += v[i];
-      }
-      sh.red[t] = s;
-    }
-    __syncthreads();
-    if (t < cols) {
-      double r = 0.0;
-      for (int q = 0; q < hq; ++q) r += sh.red[t * hq + q];
-      sh.sum[t] = r;
-    }
-    __syncthreads();
-  };
-
   unsigned epoch = 0;
   // optional phase timing (workgroup 0, thread 0; s_memrealtime ticks): 0 stencil + partial
-  // sums, 1 barrier, 2 partial reduction, 3 lagged Givens step, 4 basis update
+  // sums, 1 all-reduce, 2 (unused), 3 coefficients, 4 basis update + Givens
   const bool prof = a.phase_ticks != nullptr && g == 0 && t == 0;
   unsigned long long tk[5] = {0, 0, 0, 0, 0};
   unsigned long long tprev = prof ? wall_clock64() : 0;
@@ -295,6 +320,7 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
   bool stopped = false;
   for (int j = 0; j <= a.stop_col; ++j) {
     const int K = j + 1;
+    const int cols = 2 * K + 2;
     // z = M A (s_j u_j) on the own row (zero Dirichlet rows beyond the grid are zero ghosts)
     // (by-value selects of loads from clamped columns: a select of lvalues would become a
     // select of addresses, i.e. flat loads)
@@ -319,105 +345,106 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
       sh.zrow[t] = z;
     }
     __syncthreads();
-    // partial sums of the own row, one thread per column, points in a fixed order (two
-    // interleaved accumulators): conj(u_k) z for k < K, |z|^2 (thread K), |u_j|^2 (K + 1)
-    if (t <= K + 1) {
-      double2 a0 = z2, a1 = z2;
-      const l2* uk = Urow(min(t, j), 1);
-      int p = 0;
-      for (; p + 1 < n; p += 2) {
-        const double2 z0 = sh.zrow[p], zq = sh.zrow[p + 1];
-        const double2 u0 = uk[p], uq = uk[p + 1];
-        if (t < K) {
-          a0 = cfma_conj(u0, z0, a0);
-          a1 = cfma_conj(uq, zq, a1);
-        } else if (t == K) {
-          a0.x = fma(z0.x, z0.x, fma(z0.y, z0.y, a0.x));
-          a1.x = fma(zq.x, zq.x, fma(zq.y, zq.y, a1.x));
-        } else {
-          a0.x = fma(u0.x, u0.x, fma(u0.y, u0.y, a0.x));
-          a1.x = fma(uq.x, uq.x, fma(uq.y, uq.y, a1.x));
+    // partial sums of the own row: K + 2 quantities (conj(u_k) z, k < K; |z|^2; |u_j|^2), each
+    // split over `seg` threads taking contiguous point ranges, added in segment order
+    {
+      const int nq = K + 2;
+      const int seg = max(1, min(nt / nq, 16));
+      const int q = t / seg, sgi = t % seg;
+      const int len = (n + seg - 1) / seg;
+      const int p0 = sgi * len, p1 = min(n, p0 + len);
+      double2 acc = z2;
+      if (q < nq) {
+        const l2* uk = Urow(min(q, j), 1);
+        for (int p = p0; p < p1; ++p) {
+          const double2 zp = sh.zrow[p];
+          const double2 up = uk[p];
+          if (q < K) acc = cfma_conj(up, zp, acc);
+          else if (q == K) acc.x = fma(zp.x, zp.x, fma(zp.y, zp.y, acc.x));
+          else acc.x = fma(up.x, up.x, fma(up.y, up.y, acc.x));
         }
+        sh.red[2 * t] = acc.x;
+        sh.red[2 * t + 1] = acc.y;
       }
-      if (p < n) {
-        const double2 z0 = sh.zrow[p], u0 = uk[p];
-        if (t < K) a0 = cfma_conj(u0, z0, a0);
-        else if (t == K) a0.x = fma(z0.x, z0.x, fma(z0.y, z0.y, a0.x));
-        else a0.x = fma(u0.x, u0.x, fma(u0.y, u0.y, a0.x));
-      }
-      const double2 d = cadd(a0, a1);
-      if (t < K) {
-        st_sc1(pcol(par, 2 * t) + g, d.x);
-        st_sc1(pcol(par, 2 * t + 1) + g, d.y);
-      } else if (t == K) {
-        st_sc1(pcol(par, 2 * K) + g, d.x);
-      } else {
-        st_sc1(pcol(par, 2 * K + 1) + g, j > 0 ? d.x : 0.0);
+      __syncthreads();
+      if (t < nq) {
+        double2 d = z2;
+        for (int i = 0; i < seg; ++i)
+          d = cadd(d, make_double2(sh.red[2 * (t * seg + i)], sh.red[2 * (t * seg + i) + 1]));
+        double* pr = ar.part + ((size_t)par * G + g) * kPStride;
+        if (t < K) {
+          st_sc1(pr + 2 * t, d.x);
+          st_sc1(pr + 2 * t + 1, d.y);
+        } else if (t == K) {
+          st_sc1(pr + 2 * K, d.x);
+        } else {
+          st_sc1(pr + 2 * K + 1, j > 0 ? d.x : 0.0);
+        }
       }
     }
     tick(0);
     epoch++;
-    if (!grid_barrier(a.bar, epoch, G, a.timeout_word, sh.ctl)) return;
+    // the neighbours' z rows are loaded after the all-reduce (whose flag orders them)
+    if (!allreduce_rows(ar, par, epoch, cols, sh.sum, sh.ctl)) return;
     tick(1);
-    // the neighbours' z rows (for the ghost update below) in flight with the partial sums
     const int glo = min(max(g - 1, 0), n - 1), ghi = min(g + 1, n - 1);
     const double* zlo = a.zbuf + ((size_t)par * n + glo) * 2 * n + 2 * tc;
     const double* zhi = a.zbuf + ((size_t)par * n + ghi) * 2 * n + 2 * tc;
     const double2 zl = make_double2(ld_sc1(zlo), ld_sc1(zlo + 1));
     const double2 zh = make_double2(ld_sc1(zhi), ld_sc1(zhi + 1));
-    reduce_partials(par, 2 * K + 2);
-    tick(2);
-    // the lagged-normalisation step (krylov.hip gmres_lag_kernel): column j-1 finished on
-    // lane 0 (sequential rotations), column j started by one thread per entry
-    if (t == 0) {
+    // the lagged-normalisation step (krylov.hip gmres_lag_kernel), split: 1/|u_j| and the
+    // update coefficients first (one thread per basis vector) ...
+    const double vj = j >= 1 ? 1.0 / sqrt(sh.sum[2 * K + 1]) : sh.vs[0];
+    if (t <= j) {
+      const double vk = t == j ? vj : sh.vs[t];
+      const double2 d = make_double2(sh.sum[2 * t], sh.sum[2 * t + 1]);
+      sh.coef[t] = cscale(cscale(d, vk), vk);  // krylov.hip update_kernel's coefficient
+    }
+    __syncthreads();
+    tick(3);
+    if (t < nrow) {
+      // ... then u_{j+1} = z - sum_k c_k u_k on the own row and both ghost rows (neighbours'
+      // z from the all-reduce's round; beyond the grid the ghost stays zero)
+      if (act) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const int gr = g - 1 + r;
+          double2 w = r == 0 ? zl : (r == 1 ? z : zh);
+          for (int k = 0; k < K; ++k) w = csub(w, cmul(sh.coef[k], Urow(k, r)[t]));
+          Urow(j + 1, r)[t] = csel(gr >= 0 && gr < n, w, z2);
+        }
+      }
+    } else if (t == book) {
+      // ... while the bookkeeping lane completes column j-1 (its subdiagonal from |u_j|,
+      // rotations, presid, exit test) and starts column j
       bool stop = false;
       if (j >= 1) {
-        const double sg = sqrt(sh.sum[2 * K + 1]);
         const int col = j - 1;
-        stop = finish_column(sh, a, col, sg * sh.vs[col] / sh.ss[col], 1.0 / sg);
-        sh.vs[j] = 1.0 / sg;  // (also on breakdown: unused then)
+        stop = finish_column(sh, a, col, (1.0 / vj) * sh.vs[col] / sh.ss[col], vj);
+      }
+      if (!stop) {
+        sh.vs[j] = vj;
+        const double f = vj / sh.ss[j];
+        l2* h = sh.H + (size_t)j * R1;
+        const double w2 = sh.sum[2 * K];
+        double rest = w2;
+        for (int k = 0; k <= j; ++k) {
+          const double vk = k == j ? vj : sh.vs[k];
+          const double2 d = make_double2(sh.sum[2 * k], sh.sum[2 * k + 1]);
+          h[k] = cscale(cscale(d, vk), f);
+          rest -= cabs2(d) * vk * vk;
+        }
+        sh.h0s[j] = sqrt(w2) * f;
+        sh.ss[j + 1] = 1.0 / sqrt(fmax(rest, fmax(w2 * 1e-28, 1e-300)));
       }
       sh.ctl[0] = stop ? 1 : 0;
     }
     __syncthreads();
+    tick(4);
     if (sh.ctl[0]) {
-      tick(3);
       stopped = true;
       break;
     }
-    const double vj = sh.vs[j];
-    const double f = vj / sh.ss[j];
-    if (t <= j) {
-      const double vk = sh.vs[t];
-      const double2 d = make_double2(sh.sum[2 * t], sh.sum[2 * t + 1]);
-      sh.H[(size_t)j * R1 + t] = cscale(cscale(d, vk), f);
-      sh.coef[t] = cscale(cscale(d, vk), vk);  // krylov.hip update_kernel's coefficient
-    }
-    if (t == 0) {
-      const double w2 = sh.sum[2 * K];
-      double rest = w2;
-      for (int k = 0; k <= j; ++k) {
-        const double vk = sh.vs[k];
-        rest -= cabs2(make_double2(sh.sum[2 * k], sh.sum[2 * k + 1])) * vk * vk;
-      }
-      sh.h0s[j] = sqrt(w2) * f;
-      sh.ss[j + 1] = 1.0 / sqrt(fmax(rest, fmax(w2 * 1e-28, 1e-300)));
-    }
-    __syncthreads();
-    tick(3);
-    // u_{j+1} = z - sum_k c_k u_k on the own row and both ghost rows (neighbours' z from the
-    // barrier's hand-off; beyond the grid the ghost stays zero)
-    if (act) {
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        const int gr = g - 1 + r;
-        double2 w = r == 0 ? zl : (r == 1 ? z : zh);
-        for (int k = 0; k < K; ++k) w = csub(w, cmul(sh.coef[k], Urow(k, r)[t]));
-        Urow(j + 1, r)[t] = csel(gr >= 0 && gr < n, w, z2);
-      }
-    }
-    __syncthreads();
-    tick(4);
   }
   if (prof)
     for (int q = 0; q < 5; ++q) a.phase_ticks[q] += tk[q];
@@ -429,11 +456,10 @@ __global__ __launch_bounds__(kSmallThreads) void gmres_small_cycle_kernel(SmallC
       const l2* ul = Urow(last, 1);
       double s = 0.0;
       for (int p = 0; p < n; ++p) s = fma(ul[p].x, ul[p].x, fma(ul[p].y, ul[p].y, s));
-      st_sc1(pcol(par, 0) + g, s);
+      st_sc1(ar.part + ((size_t)par * G + g) * kPStride, s);
     }
     epoch++;
-    if (!grid_barrier(a.bar, epoch, G, a.timeout_word, sh.ctl)) return;
-    reduce_partials(par, 1);
+    if (!allreduce_rows(ar, par, epoch, 1, sh.sum, sh.ctl)) return;
     if (t == 0) {
       const double sg = sqrt(sh.sum[0]);
       const int col = a.stop_col;
@@ -478,11 +504,13 @@ size_t small_cycle_lds_bytes(int n, int restart) {
   auto al = [](size_t b) { return (b + 15) / 16 * 16; };
   return al(16 * R1 * 3 * n) + al(16 * (size_t)n) + al(16 * (size_t)restart * R1) +
          al(32 * (size_t)restart) + 2 * al(16 * R1) + 2 * al(8 * R1) + al(8 * (size_t)restart) +
-         al(8 * (size_t)kSmallThreads) + al(8 * kPStride) + al(16);
+         al(16 * (size_t)(kSmallThreads + kWave)) + al(8 * kPStride) + al(16);
 }
 
 size_t small_cycle_scratch_doubles(int n) {
-  return 2 * (size_t)n * 2 * n + 2 * (size_t)kPStride * n;
+  // z rows [2][n][2n], then the all-reduce rows [2][n][kPStride], group sums [2][8][kPStride],
+  // final sums [2][kPStride]
+  return 2 * (size_t)n * 2 * n + 2 * (size_t)kPStride * (n + 8 + 1);
 }
 
 bool small_cycle_eligible(int n, int restart) {
@@ -501,7 +529,7 @@ void launch_one(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds, hipS
 }
 
 void launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi, hipStream_t s) {
-  const int threads = (a.n + kWave - 1) / kWave * kWave;
+  const int threads = (a.n + kWave - 1) / kWave * kWave + kWave;  // + the bookkeeping wave
   const size_t lds = small_cycle_lds_bytes(a.n, a.restart);
   const dim3 grid(a.n), block(threads);
   if (const_c) {

@@ -39,5 +39,5 @@ for mode in ("on", "off", "on"):
     per = [ph[q] / a.iters for q in range(5)]
     print(f"n={n} small_cycle={mode}: {a.iters / dt:9.1f} it/s ({dt / a.iters * 1e6:6.2f} us/it)"
           + ("" if mode == "off" else
-             "  phases us/it: stencil+dots %.2f barrier %.2f reduce %.2f givens %.2f update %.2f"
+             "  phases us/it: stencil+dots %.2f allreduce %.2f - %.2f coef %.2f update+givens %.2f"
              % tuple(per)), flush=True)
