@@ -77,73 +77,69 @@ struct Shared {  // LDS layout (carved from dynamic shared memory; see small_cyc
   li* ctl;   // [4]: 0 stop, 1 last column, 2 abort
 };
 
-// Grouped all-reduce of `cols` doubles per workgroup (the barrier words are zeroed before the
-// launch; rows/sums are double-buffered by `par`, so a round never overwrites what a slower
+// All-reduce of `cols` doubles per workgroup, one level (the words are zeroed before the
+// launch; rows and sums are double-buffered by `par`, so a round never overwrites what a slower
 // workgroup may still read from the round before):
-//  1. every workgroup publishes its row part[par][g][0 .. cols) (sc1 stores by threads < cols,
-//     every storing wave drains vmcnt, workgroup barrier) and thread 0 adds to its group's
-//     counter (groups: blockIdx % 8, the dispatcher's XCD round-robin -- a performance grouping
-//     only);
-//  2. the group's LAST arriver (told by the value its add returns) sums the group's rows in
-//     member order into gsum[par][grp] and adds to the top counter;
-//  3. the top counter's last arriver sums the group sums in group order into fsum[par], then
-//     raises the round's flag;
-//  4. everyone polls the flag (thread 0, relaxed sc1 loads, bounded) and reads fsum into LDS.
-// The arithmetic order is fixed whichever workgroup happens to be last: identical sums on every
-// workgroup and every run.  Hand-offs in MI355X_MICROARCH.md's valid form (sc1 stores drained
-// before one lane's agent-scope add or flag store; sc1 loads after the poll + a workgroup
-// barrier).  Returns false on timeout (every workgroup then leaves the kernel).
+//  1. every workgroup has published its row part[par][g][0 .. cols) (sc1 stores, drained by
+//     every storing wave, then a workgroup barrier); thread 0 adds to the arrival counter;
+//  2. the LAST arriver (told by the value its add returns) sums every column over all rows in
+//     row order -- each thread a column x a contiguous chunk of rows, its loads in flight
+//     together, the chunk sums added in chunk order -- into fsum[par], then raises the round's
+//     flag;
+//  3. everyone polls the flag (thread 0, relaxed sc1 loads, bounded) and reads fsum into LDS.
+// The arithmetic order is fixed whichever workgroup is last: identical sums on every workgroup
+// and every run.  Hand-offs in MI355X_MICROARCH.md's valid form (sc1 stores drained before one
+// lane's agent-scope add or flag store; sc1 loads after the poll + a workgroup barrier).
+// Returns false on timeout (every workgroup then leaves the kernel).
+constexpr int kChunk = 32;  // rows one reducing thread loads in flight per batch
 struct ArArgs {
-  double* part;   // [2][G][kPStride]
-  double* gsum;   // [2][8][kPStride]
-  double* fsum;   // [2][kPStride]
-  unsigned* words;  // [0] top counter, [1] timeout, [2] flag, [4 + 16 grp] group counters
+  double* part;     // [2][G][kPStride]
+  double* fsum;     // [2][kPStride]
+  unsigned* words;  // [0] arrival counter, [1] timeout, [2] flag
 };
 __device__ bool allreduce_rows(const ArArgs& ar, int par, unsigned epoch, int cols, l1* out,
-                               li* ctl) {
-  const unsigned G = gridDim.x, g = blockIdx.x, t = threadIdx.x;
-  const unsigned grp = g & 7;
-  const unsigned ngroups = G < 8 ? G : 8;
-  const unsigned gsize = (G - grp + 7) / 8;
-  unsigned* top = ar.words;
+                               l1* red, li* ctl) {
+  const unsigned G = gridDim.x;
+  const int t = threadIdx.x, nt = blockDim.x;
+  unsigned* cnt = ar.words;
   unsigned* tmo = ar.words + 1;
   unsigned* flag = ar.words + 2;
-  unsigned* mine = ar.words + 4 + 16 * grp;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's row stores drained
   __syncthreads();
   if (t == 0) {
     const unsigned old =
-        __hip_atomic_fetch_add((gu32*)mine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ctl[3] = old + 1 == epoch * gsize ? 1 : 0;
+        __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ctl[3] = old + 1 == epoch * G ? 1 : 0;
   }
   __syncthreads();
-  if (ctl[3]) {  // last of the group: the group sum, members in index order
-    if ((int)t < cols) {
+  if (ctl[3]) {  // the last arriver reduces
+    const int hq = max(1, min(nt / cols, (int)G));
+    const int chunk = ((int)G + hq - 1) / hq;
+    const int c = t / hq, h = t % hq;
+    if (c < cols) {
+      const int q0 = h * chunk, q1 = min((int)G, q0 + chunk);
       double s = 0.0;
-      for (unsigned q = grp; q < G; q += 8)
-        s += ld_sc1(ar.part + ((size_t)par * G + q) * kPStride + t);
-      st_sc1(ar.gsum + ((size_t)par * 8 + grp) * kPStride + t, s);
+      for (int b = q0; b < q1; b += kChunk) {
+        double v[kChunk];
+#pragma unroll
+        for (int i = 0; i < kChunk; ++i)
+          v[i] = ld_sc1(ar.part + ((size_t)par * G + min(b + i, q1 - 1)) * kPStride + c);
+#pragma unroll
+        for (int i = 0; i < kChunk; ++i)
+          if (b + i < q1) s += v[i];
+      }
+      red[t] = s;
+    }
+    __syncthreads();
+    if (t < cols) {
+      double r = 0.0;
+      for (int q = 0; q < hq; ++q) r += red[t * hq + q];
+      st_sc1(ar.fsum + (size_t)par * kPStride + t, r);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (t == 0) {
-      const unsigned old =
-          __hip_atomic_fetch_add((gu32*)top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      ctl[3] = old + 1 == epoch * ngroups ? 2 : 0;
-    }
-    __syncthreads();
-    if (ctl[3] == 2) {  // last group: the final sums, groups in index order, then the flag
-      if ((int)t < cols) {
-        double s = 0.0;
-        for (unsigned k = 0; k < ngroups; ++k)
-          s += ld_sc1(ar.gsum + ((size_t)par * 8 + k) * kPStride + t);
-        st_sc1(ar.fsum + (size_t)par * kPStride + t, s);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (t == 0)
-        __hip_atomic_store((gu32*)flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (t == 0)
+      __hip_atomic_store((gu32*)flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (t == 0) {
     unsigned spins = 0;
@@ -158,7 +154,7 @@ __device__ bool allreduce_rows(const ArArgs& ar, int par, unsigned epoch, int co
   }
   __syncthreads();
   if (ctl[2]) return false;
-  if ((int)t < cols) out[t] = ld_sc1(ar.fsum + (size_t)par * kPStride + t);
+  if (t < cols) out[t] = ld_sc1(ar.fsum + (size_t)par * kPStride + t);
   __syncthreads();
   return true;
 }
@@ -272,8 +268,7 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
   const double2 z2 = make_double2(0.0, 0.0);
   ArArgs ar;
   ar.part = a.part;
-  ar.gsum = a.part + 2 * (size_t)G * kPStride;
-  ar.fsum = ar.gsum + 2 * 8 * (size_t)kPStride;
+  ar.fsum = a.part + 2 * (size_t)G * kPStride;
   ar.words = a.bar;
 
   // operator coefficients of this thread's point (stencil.hip's formulas; row g, column t)
@@ -385,7 +380,7 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     tick(0);
     epoch++;
     // the neighbours' z rows are loaded after the all-reduce (whose flag orders them)
-    if (!allreduce_rows(ar, par, epoch, cols, sh.sum, sh.ctl)) return;
+    if (!allreduce_rows(ar, par, epoch, cols, sh.sum, sh.red, sh.ctl)) return;
     tick(1);
     const int glo = min(max(g - 1, 0), n - 1), ghi = min(g + 1, n - 1);
     const double* zlo = a.zbuf + ((size_t)par * n + glo) * 2 * n + 2 * tc;
@@ -459,7 +454,7 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
       st_sc1(ar.part + ((size_t)par * G + g) * kPStride, s);
     }
     epoch++;
-    if (!allreduce_rows(ar, par, epoch, 1, sh.sum, sh.ctl)) return;
+    if (!allreduce_rows(ar, par, epoch, 1, sh.sum, sh.red, sh.ctl)) return;
     if (t == 0) {
       const double sg = sqrt(sh.sum[0]);
       const int col = a.stop_col;
@@ -508,9 +503,8 @@ size_t small_cycle_lds_bytes(int n, int restart) {
 }
 
 size_t small_cycle_scratch_doubles(int n) {
-  // z rows [2][n][2n], then the all-reduce rows [2][n][kPStride], group sums [2][8][kPStride],
-  // final sums [2][kPStride]
-  return 2 * (size_t)n * 2 * n + 2 * (size_t)kPStride * (n + 8 + 1);
+  // z rows [2][n][2n], then the all-reduce rows [2][n][kPStride] and sums [2][kPStride]
+  return 2 * (size_t)n * 2 * n + 2 * (size_t)kPStride * (n + 1);
 }
 
 bool small_cycle_eligible(int n, int restart) {

@@ -230,9 +230,9 @@ struct SmallCycleArgs {
   unsigned* timeout_word;  // set when a barrier wait gives up
   unsigned long long* phase_ticks;  // optional [8]: workgroup 0's wall-clock ticks per phase
 };
-// barrier words of the small cycle: [0] top counter, [1] timeout word, [4 + 16 k] the counter
-// of workgroup group k (k < 8; one 64-B line each); zeroed before every launch
-constexpr int kSmallBarWords = 4 + 16 * 8;
+// all-reduce words of the small cycle: [0] arrival counter, [1] timeout word, [2] round flag;
+// zeroed before every launch (16 B)
+constexpr int kSmallBarWords = 4;
 bool small_cycle_eligible(int n, int restart);
 size_t small_cycle_lds_bytes(int n, int restart);
 size_t small_cycle_scratch_doubles(int n);
