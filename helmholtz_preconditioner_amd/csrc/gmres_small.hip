@@ -200,12 +200,23 @@ __device__ bool finish_column(const Shared& sh, const SmallCycleArgs& a, int col
   } else {
     sh.vs[col + 1] = inv_sigma_next;
   }
-  for (int k = 0; k < col; ++k) {
-    const double c = sh.Gr[2 * k].x;
-    const double2 s = sh.Gr[2 * k + 1];
-    const double2 n0 = h[k], n1 = h[k + 1];
-    h[k] = cadd(cscale(n0, c), cmul(s, n1));
-    h[k + 1] = cadd(cmul(make_double2(-s.x, s.y), n0), cscale(n1, c));
+  // the previous rotations, in order; the running entry is carried in registers and the next
+  // step's operands are loaded one step ahead (the chain never waits on an LDS round trip)
+  if (col > 0) {
+    double2 n0 = h[0];
+    double c = sh.Gr[0].x;
+    double2 s = sh.Gr[1], n1 = h[1];
+    for (int k = 0; k < col; ++k) {
+      const int kn = min(k + 1, col - 1);
+      const double cn = sh.Gr[2 * kn].x;
+      const double2 sn = sh.Gr[2 * kn + 1], n1n = h[kn + 1];
+      h[k] = cadd(cscale(n0, c), cmul(s, n1));
+      n0 = cadd(cmul(make_double2(-s.x, s.y), n0), cscale(n1, c));
+      c = cn;
+      s = sn;
+      n1 = n1n;
+    }
+    h[col] = n0;
   }
   double c;
   double2 s, r;
@@ -394,6 +405,9 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
       const double vk = t == j ? vj : sh.vs[t];
       const double2 d = make_double2(sh.sum[2 * t], sh.sum[2 * t + 1]);
       sh.coef[t] = cscale(cscale(d, vk), vk);  // krylov.hip update_kernel's coefficient
+      // column j of H (gmres_lag_kernel step (c)); the entries are untouched by the finishing
+      // of column j-1 below
+      sh.H[(size_t)j * R1 + t] = cscale(cscale(d, vk), vj / sh.ss[j]);
     }
     __syncthreads();
     tick(3);
@@ -420,14 +434,11 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
       if (!stop) {
         sh.vs[j] = vj;
         const double f = vj / sh.ss[j];
-        l2* h = sh.H + (size_t)j * R1;
         const double w2 = sh.sum[2 * K];
         double rest = w2;
         for (int k = 0; k <= j; ++k) {
           const double vk = k == j ? vj : sh.vs[k];
-          const double2 d = make_double2(sh.sum[2 * k], sh.sum[2 * k + 1]);
-          h[k] = cscale(cscale(d, vk), f);
-          rest -= cabs2(d) * vk * vk;
+          rest -= cabs2(make_double2(sh.sum[2 * k], sh.sum[2 * k + 1])) * vk * vk;
         }
         sh.h0s[j] = sqrt(w2) * f;
         sh.ss[j + 1] = 1.0 / sqrt(fmax(rest, fmax(w2 * 1e-28, 1e-300)));

@@ -1743,14 +1743,19 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       HIPC(hipGetLastError());
     }
     op->stop_flag = nullptr;  // (the SolveScope also clears it if anything above throws)
-    // one sync: per-iteration statuses + the last column executed
+    // one sync: per-iteration statuses + the last column executed (the whole-cycle kernel has
+    // already updated x: its true residual is queued behind it and read in the same sync)
+    if (small) residual(op, b, x, V, 4);  // r = b - A x; V[0] = M r for the next cycle
     HIPC(hipMemcpyAsync(op->status_h, g.status_it, 4 * (size_t)restart * sizeof(double),
                         hipMemcpyDeviceToHost, s));
     HIPC(hipMemcpyAsync(op->status_h + 4 * restart, g.ctrl, 2 * sizeof(int),
                         hipMemcpyDeviceToHost, s));
-    if (small)
+    if (small) {
       HIPC(hipMemcpyAsync(op->status_h + 4 * restart + 1, op->small_bar + 1, sizeof(unsigned),
                           hipMemcpyDeviceToHost, s));
+      HIPC(hipMemcpyAsync(op->status_h + 4 * restart + 2, op->red + 4, sizeof(double),
+                          hipMemcpyDeviceToHost, s));
+    }
     HIPC(hipStreamSynchronize(s));
     int ctl[2];
     std::memcpy(ctl, op->status_h + 4 * restart, 2 * sizeof(int));
@@ -1777,9 +1782,11 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     if (!small) {  // (the whole-cycle kernel has solved and updated x itself)
       launch_gmres_solve(g, col, s);
       launch_xupdate(V, ldv, col + 1, g.ycoef, x, L, blocks, s);
+      residual(op, b, x, V, 4);  // r = b - A x; V[0] = M r for the next cycle
+      read_dev(op, op->red + 4, st, 1);
+    } else {
+      st[0] = op->status_h[4 * restart + 2];
     }
-    residual(op, b, x, V, 4);  // r = b - A x; V[0] = M r for the next cycle
-    read_dev(op, op->red + 4, st, 1);
     rnorm = std::sqrt(st[0]);
     if (legacy && inner == maxiter) {
       finish(inner, rnorm <= atol ? 0 : (int)std::min<long>(maxiter, 0x7fffffff), rnorm);
