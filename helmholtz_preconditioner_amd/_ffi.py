@@ -34,6 +34,8 @@ HH_TRANSPORT_RCCL, HH_TRANSPORT_SHM = 0, 1
 # callbacks return 0 to continue, non-zero to stop the solve (hh_gmres -> HH_ERR_ABORTED)
 GMRES_CALLBACK = ctypes.CFUNCTYPE(c_int, c_void_p, c_long, c_double)
 GMRES_CYCLE_CALLBACK = ctypes.CFUNCTYPE(c_int, c_void_p, c_long)
+GMRES_HISTORY_CALLBACK = ctypes.CFUNCTYPE(c_int, c_void_p, c_long, c_int,
+                                          ctypes.POINTER(ctypes.c_double))
 HH_ERR_ABORTED = -6
 ABI_VERSION = 2
 
@@ -79,6 +81,7 @@ SIGNATURES = [
                          c_int, c_dp, c_long, GMRES_CALLBACK, c_void_p, c_lp, c_ip, c_dp, c_dp]),
     ("hh_op_set_stencil", c_int, [c_void_p, c_int, c_double, c_double, c_double]),
     ("hh_op_set_cycle_callback", c_int, [c_void_p, GMRES_CYCLE_CALLBACK, c_void_p]),
+    ("hh_op_set_history_callback", c_int, [c_void_p, GMRES_HISTORY_CALLBACK, c_void_p]),
     ("hh_op_sl_fusion", c_int, [c_void_p, c_int]),
     ("hh_op_set_krylov_mode", c_int, [c_void_p, c_int]),
     ("hh_op_set_small_cycle", c_int, [c_void_p, c_int]),

@@ -28,6 +28,7 @@
 // from the regular cycle (histories agree to rounding; tests/test_gpu_small_cycle.py).
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
+#include "hh_error.hpp"
 
 namespace hh {
 namespace {
@@ -49,7 +50,7 @@ __device__ __forceinline__ double2 csel(bool c, double2 a, double2 b) {
 }
 
 constexpr int kSmallThreads = 256;    // block size cap for the grid's rows (n <= 256)
-constexpr int kPStride = 2 * (kMaxProj + 1) + 2;  // partial-sum columns (global layout)
+constexpr int kPStride = kSmallCols;  // partial-sum columns (global layout)
 constexpr unsigned kSpinLimit = 1u << 22;  // ~1 s of polling: a barrier wait is microseconds
 
 // LDS pointers carry address space 3 on the device (ds_ instructions, not flat ones); the host
@@ -72,117 +73,159 @@ struct Shared {  // LDS layout (carved from dynamic shared memory; see small_cyc
   l1* vs;    // [R1] exact 1 / |u_k|
   l1* ss;    // [R1] scale of each SpMV input
   l1* h0s;   // [R]
-  l1* red;   // [kSmallThreads] chunk sums of the partial reduction
+  l1* red;   // [kRedRuns + kRuns] segment sums of the partial sums, run sums of the reducer
   l1* sum;   // [PSTRIDE] reduced sums
   li* ctl;   // [4]: 0 stop, 1 last column, 2 abort
 };
 
-// All-reduce of `cols` doubles per workgroup, one level (the words are zeroed before the
-// launch; rows and sums are double-buffered by `par`, so a round never overwrites what a slower
-// workgroup may still read from the round before):
-//  1. every workgroup has published its row part[par][g][0 .. cols) (sc1 stores, drained by
-//     every storing wave, then a workgroup barrier); thread 0 adds to the arrival counter;
-//  2. the LAST arriver (told by the value its add returns) sums every column over all rows in
-//     row order -- each thread a column x a contiguous chunk of rows, its loads in flight
-//     together, the chunk sums added in chunk order -- into fsum[par], then raises the round's
-//     flag;
-//  3. everyone polls the flag (thread 0, relaxed sc1 loads, bounded) and reads fsum into LDS.
-// The arithmetic order is fixed whichever workgroup is last: identical sums on every workgroup
-// and every run.  Hand-offs in MI355X_MICROARCH.md's valid form (sc1 stores drained before one
-// lane's agent-scope add or flag store; sc1 loads after the poll + a workgroup barrier).
-// Returns false on timeout (every workgroup then leaves the kernel).
-constexpr int kChunk = 32;  // rows one reducing thread loads in flight per batch
+// All-reduce of `cols` doubles per workgroup with NO counter and NO flag: every value travels
+// as two 8-byte granules {tag, 32-bit half} (MI355X_MICROARCH.md's "the data is the flag" form
+// for small payloads -- a granule is written by one 8-byte store, so a reader that sees the tag
+// sees the half that came with it; nothing needs ordering or draining).  The tag is the launch's
+// sequence number and the round (epoch), so granules of an earlier round or launch never match.
+//  1. every workgroup has stored its row of partial sums as granules, part[par][g][.];
+//  2. column c is reduced by workgroup c mod G: thread q polls row q's two granules of the
+//     column until both carry the round's tag, then the rows are summed in row order (32 runs
+//     of consecutive rows, the run sums in run order) and the sum is stored as two granules;
+//  3. every workgroup polls the `cols` sums' granules until tagged.
+// Two hops (partials -> reducer -> everyone) and no serialised atomics.  The arithmetic order is
+// fixed: identical sums on every workgroup and every run.  Rows and sums are double-buffered by
+// `par`: a round's granules are only overwritten two rounds later, which no workgroup can reach
+// before every workgroup has read them.  Returns false on timeout (every workgroup then leaves).
+constexpr int kRuns = 32;
+constexpr int kBatch = 8;  // LDS loads a thread keeps in flight in its reduction loops
+constexpr int kRunMax = (kSmallThreads + kRuns - 1) / kRuns;  // rows per run, at most
+// sh.red: [0, kRedRuns) the partial-sum segments of the caller, [kRedRuns, + kRuns) run sums
+constexpr int kRedRuns = 2 * (kSmallThreads + kWave);
 struct ArArgs {
-  double* part;     // [2][G][kPStride]
-  double* fsum;     // [2][kPStride]
-  unsigned* words;  // [0] arrival counter, [1] timeout, [2] flag
+  unsigned long long* part;  // [2][G][2 kPStride]
+  unsigned long long* sums;  // [2][2 kPStride]
+  unsigned* timeout;
+  unsigned seq;
 };
+__device__ __forceinline__ unsigned gran_tag(unsigned seq, unsigned epoch) {
+  return (seq << 8) | (epoch & 0xffu);
+}
+__device__ __forceinline__ void st_gran(unsigned long long* p, unsigned tag, double v) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned long long tg = (unsigned long long)tag << 32;
+  __hip_atomic_store((gu64*)p, tg | (u >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((gu64*)(p + 1), tg | (u & 0xffffffffull), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+// polls the two granules of one double until both carry `tag`; false on timeout
+__device__ __forceinline__ bool ld_gran(const unsigned long long* p, unsigned tag, double* v) {
+  unsigned spins = 0;
+  for (;;) {
+    const unsigned long long hi =
+        __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long lo =
+        __hip_atomic_load((gu64*)(p + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((unsigned)(hi >> 32) == tag && (unsigned)(lo >> 32) == tag) {
+      *v = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
+      return true;
+    }
+    if (++spins > kSpinLimit) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
 __device__ bool allreduce_rows(const ArArgs& ar, int par, unsigned epoch, int cols, l1* out,
-                               l1* red, li* ctl) {
-  const unsigned G = gridDim.x;
-  const int t = threadIdx.x, nt = blockDim.x;
-  unsigned* cnt = ar.words;
-  unsigned* tmo = ar.words + 1;
-  unsigned* flag = ar.words + 2;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's row stores drained
-  __syncthreads();
-  if (t == 0) {
-    const unsigned old =
-        __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ctl[3] = old + 1 == epoch * G ? 1 : 0;
-  }
-  __syncthreads();
-  if (ctl[3]) {  // the last arriver reduces
-    const int hq = max(1, min(nt / cols, (int)G));
-    const int chunk = ((int)G + hq - 1) / hq;
-    const int c = t / hq, h = t % hq;
-    if (c < cols) {
-      const int q0 = h * chunk, q1 = min((int)G, q0 + chunk);
+                               l1* red) {
+  const int G = gridDim.x, g = blockIdx.x;
+  const int t = threadIdx.x;
+  const unsigned tag = gran_tag(ar.seq, epoch);
+  const int run = (G + kRuns - 1) / kRuns;  // rows per summing thread (<= 16)
+  bool ok = true;
+  for (int c = g; c < cols; c += G) {
+    if (t < kRuns) {
+      // this thread's run of rows, all granules in flight together, polled until tagged;
+      // then summed in row order
+      const int q0 = t * run, q1 = min(G, q0 + run);
       double s = 0.0;
-      for (int b = q0; b < q1; b += kChunk) {
-        double v[kChunk];
+      unsigned spins = 0;
+      for (;;) {
+        unsigned long long v[2 * kRunMax];
 #pragma unroll
-        for (int i = 0; i < kChunk; ++i)
-          v[i] = ld_sc1(ar.part + ((size_t)par * G + min(b + i, q1 - 1)) * kPStride + c);
+        for (int i = 0; i < kRunMax; ++i) {
+          const unsigned long long* p =
+              ar.part + ((size_t)par * G + min(q0 + i, q1 - 1)) * 2 * kPStride + 2 * c;
+          v[2 * i] = i < q1 - q0 ? __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+          v[2 * i + 1] = i < q1 - q0 ? __hip_atomic_load((gu64*)(p + 1), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        }
+        bool all = true;
 #pragma unroll
-        for (int i = 0; i < kChunk; ++i)
-          if (b + i < q1) s += v[i];
+        for (int i = 0; i < kRunMax; ++i)
+          if (i < q1 - q0)
+            all = all && (unsigned)(v[2 * i] >> 32) == tag &&
+                  (unsigned)(v[2 * i + 1] >> 32) == tag;
+        if (all) {
+#pragma unroll
+          for (int i = 0; i < kRunMax; ++i)
+            if (i < q1 - q0)
+              s += __longlong_as_double(
+                  (long long)((v[2 * i] << 32) | (v[2 * i + 1] & 0xffffffffull)));
+          break;
+        }
+        if (++spins > kSpinLimit) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
       }
-      red[t] = s;
+      red[kRedRuns + t] = s;
     }
     __syncthreads();
-    if (t < cols) {
-      double r = 0.0;
-      for (int q = 0; q < hq; ++q) r += red[t * hq + q];
-      st_sc1(ar.fsum + (size_t)par * kPStride + t, r);
+    if (t == 0) {
+      double s = 0.0;
+      for (int q = 0; q < kRuns; ++q) s += red[kRedRuns + q];
+      st_gran(ar.sums + (size_t)par * 2 * kPStride + 2 * c, tag, s);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  }
+  if (t < cols) {
+    double v = 0.0;
+    ok = ld_gran(ar.sums + (size_t)par * 2 * kPStride + 2 * t, tag, &v) && ok;
+    out[t] = v;
+  }
+  if (__syncthreads_or(!ok)) {
     if (t == 0)
-      __hip_atomic_store((gu32*)flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((gu32*)ar.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
   }
-  if (t == 0) {
-    unsigned spins = 0;
-    while (__hip_atomic_load((gu32*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > kSpinLimit) {
-        __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ctl[2] = 1;
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  if (ctl[2]) return false;
-  if (t < cols) out[t] = ld_sc1(ar.fsum + (size_t)par * kPStride + t);
-  __syncthreads();
   return true;
 }
 
-// LAPACK zlartg main branch (krylov.hip)
-__device__ void zlartg_s(double2 f, double2 g, double* c, double2* s, double2* r) {
-  if (g.x == 0.0 && g.y == 0.0) {
-    *c = 1.0;
-    *s = make_double2(0.0, 0.0);
-    *r = f;
-    return;
-  }
-  if (f.x == 0.0 && f.y == 0.0) {
+// LAPACK zlartg main branch (krylov.hip), by value: each branch yields all three results (no
+// output pointers -- a branch-selected store target would become a scratch slot)
+struct Rot {
+  double c;
+  double2 s, r;
+};
+__device__ __forceinline__ Rot zlartg_s(double2 f, double2 g) {
+  const bool gz = g.x == 0.0 && g.y == 0.0;
+  const bool fz = f.x == 0.0 && f.y == 0.0;
+  Rot o;
+  if (gz) {
+    o.c = 1.0;
+    o.s = make_double2(0.0, 0.0);
+    o.r = f;
+  } else if (fz) {
     const double d = hypot(g.x, g.y);
-    *c = 0.0;
-    *s = make_double2(g.x / d, -g.y / d);
-    *r = make_double2(d, 0.0);
-    return;
+    o.c = 0.0;
+    o.s = make_double2(g.x / d, -g.y / d);
+    o.r = make_double2(d, 0.0);
+  } else {
+    const double f2 = cabs2(f);
+    const double g2 = cabs2(g);
+    const double h2 = f2 + g2;
+    const double cc = sqrt(f2 / h2);
+    o.c = cc;
+    o.r = make_double2(f.x / cc, f.y / cc);
+    const double d = sqrt(f2 * h2);
+    o.s = cmul(cconj(g), make_double2(f.x / d, f.y / d));
   }
-  const double f2 = cabs2(f);
-  const double g2 = cabs2(g);
-  const double h2 = f2 + g2;
-  const double cc = sqrt(f2 / h2);
-  *c = cc;
-  *r = make_double2(f.x / cc, f.y / cc);
-  const double d = sqrt(f2 * h2);
-  const double2 fd = make_double2(f.x / d, f.y / d);
-  *s = cmul(cconj(g), fd);
+  return o;
 }
 
 // lane 0: complete column `col` with its subdiagonal h1 (krylov.hip gmres_finish_column); the
@@ -218,12 +261,12 @@ __device__ bool finish_column(const Shared& sh, const SmallCycleArgs& a, int col
     }
     h[col] = n0;
   }
-  double c;
-  double2 s, r;
-  zlartg_s(h[col], h[col + 1], &c, &s, &r);
+  const Rot rot = zlartg_s(h[col], h[col + 1]);
+  const double c = rot.c;
+  const double2 s = rot.s;
   sh.Gr[2 * col] = make_double2(c, 0.0);
   sh.Gr[2 * col + 1] = s;
-  h[col] = r;
+  h[col] = rot.r;
   h[col + 1] = make_double2(0.0, 0.0);
   const double2 Sc = sh.S[col];
   const double2 tmp = cmul(make_double2(-s.x, s.y), Sc);
@@ -271,7 +314,7 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     sh.vs = (l1*)take(sizeof(double) * R1);
     sh.ss = (l1*)take(sizeof(double) * R1);
     sh.h0s = (l1*)take(sizeof(double) * R);
-    sh.red = (l1*)take(2 * sizeof(double) * (kSmallThreads + kWave));
+    sh.red = (l1*)take(sizeof(double) * (kRedRuns + kRuns));
     sh.sum = (l1*)take(sizeof(double) * kPStride);
     sh.ctl = (li*)take(sizeof(int) * 4);
   }
@@ -279,8 +322,9 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
   const double2 z2 = make_double2(0.0, 0.0);
   ArArgs ar;
   ar.part = a.part;
-  ar.fsum = a.part + 2 * (size_t)G * kPStride;
-  ar.words = a.bar;
+  ar.sums = a.sums;
+  ar.timeout = a.timeout_word;
+  ar.seq = a.seq;
 
   // operator coefficients of this thread's point (stencil.hip's formulas; row g, column t)
   const double2 AW = a.tab_i[tc], AE = a.tab_i[n + tc], R1c = a.tab_i[2 * n + tc];
@@ -302,20 +346,23 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     if (act) Urow(0, r)[t] = csel(gr >= 0 && gr < n, u0, z2);
   }
   if (t == 0) {
-    sh.vs[0] = a.g.vscale[0];
-    sh.ss[0] = a.g.vscale[0];
-    const double2 s0 = a.g.S[0];
-    for (int k = 0; k < R1; ++k) sh.S[k] = csel(k == 0, s0, z2);
+    // gmres_start_kernel's scaling of V[0], on every workgroup
+    const double mn = sqrt(*a.mnorm2);
+    sh.vs[0] = 1.0 / mn;
+    sh.ss[0] = 1.0 / mn;
+    for (int k = 0; k < R1; ++k) sh.S[k] = make_double2(k == 0 ? mn : 0.0, 0.0);
     sh.ctl[0] = sh.ctl[1] = sh.ctl[2] = sh.ctl[3] = 0;
   }
   __syncthreads();
 
   unsigned epoch = 0;
-  // optional phase timing (workgroup 0, thread 0; s_memrealtime ticks): 0 stencil + partial
-  // sums, 1 all-reduce, 2 (unused), 3 coefficients, 4 basis update + Givens
+  // optional phase timing (workgroup 0, thread 0; s_memrealtime ticks): 0 stencil + z hand-off,
+  // 5 partial sums, 6 their publication, 1 all-reduce, 3 coefficients (+ the neighbours' z),
+  // 2 basis update, 4 the wait for the bookkeeping lane (Givens)
   const bool prof = a.phase_ticks != nullptr && g == 0 && t == 0;
-  unsigned long long tk[5] = {0, 0, 0, 0, 0};
+  unsigned long long tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long tprev = prof ? wall_clock64() : 0;
+  const unsigned long long cyc0 = prof ? __builtin_amdgcn_s_memtime() : 0;
   auto tick = [&](int ph) {
     if (prof) {
       const unsigned long long now = wall_clock64();
@@ -344,60 +391,118 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     const double2 z = csel(act, JAC ? cscale(cdiv(Au, D), sj) : cscale(Au, sj), z2);
     // hand the z row to the neighbours (sc1 stores); keep it in LDS for the partial sums
     const int par = epoch & 1;
-    double* zout = a.zbuf + ((size_t)par * n + g) * 2 * n;
+    // (tagged granules like the partial sums: no drain, the neighbours poll them)
+    const unsigned rtag = gran_tag(a.seq, epoch + 1);
+    unsigned long long* zout = a.zbuf + ((size_t)par * n + g) * 4 * n;
     if (act) {
-      st_sc1(zout + 2 * t, z.x);
-      st_sc1(zout + 2 * t + 1, z.y);
+      st_gran(zout + 4 * t, rtag, z.x);
+      st_gran(zout + 4 * t + 2, rtag, z.y);
       sh.zrow[t] = z;
     }
     __syncthreads();
+    tick(0);
     // partial sums of the own row: K + 2 quantities (conj(u_k) z, k < K; |z|^2; |u_j|^2), each
-    // split over `seg` threads taking contiguous point ranges, added in segment order
+    // split over `seg` threads taking every seg-th point (neighbouring lanes read neighbouring
+    // points: no LDS bank conflicts), the segments added in segment order.  Branch-free: for
+    // |z|^2 and |u_j|^2 both factors are the same vector (cfma_conj(v, v) = |v|^2 + 0 i).
     {
       const int nq = K + 2;
       const int seg = max(1, min(nt / nq, 16));
       const int q = t / seg, sgi = t % seg;
-      const int len = (n + seg - 1) / seg;
-      const int p0 = sgi * len, p1 = min(n, p0 + len);
+      const int len = (n - sgi + seg - 1) / seg;
       double2 acc = z2;
       if (q < nq) {
         const l2* uk = Urow(min(q, j), 1);
-        for (int p = p0; p < p1; ++p) {
-          const double2 zp = sh.zrow[p];
-          const double2 up = uk[p];
-          if (q < K) acc = cfma_conj(up, zp, acc);
-          else if (q == K) acc.x = fma(zp.x, zp.x, fma(zp.y, zp.y, acc.x));
-          else acc.x = fma(up.x, up.x, fma(up.y, up.y, acc.x));
+        const bool zz = q == K, uu = q == K + 1;
+        for (int i0 = 0; i0 < len; i0 += kBatch) {
+          double2 zp[kBatch], up[kBatch];
+#pragma unroll
+          for (int i = 0; i < kBatch; ++i) {  // loads in flight together
+            const int pi = min(sgi + seg * (i0 + i), n - 1);
+            zp[i] = sh.zrow[pi];
+            up[i] = uk[pi];
+          }
+#pragma unroll
+          for (int i = 0; i < kBatch; ++i) {
+            const bool in = i0 + i < len;
+            const double2 zv = csel(in, uu ? up[i] : zp[i], z2);
+            const double2 uv = csel(in, zz ? zp[i] : up[i], z2);
+            acc = cfma_conj(uv, zv, acc);
+          }
         }
-        sh.red[2 * t] = acc.x;
-        sh.red[2 * t + 1] = acc.y;
+        sh.red[2 * (sgi * nq + q)] = acc.x;  // [segment][quantity]
+        sh.red[2 * (sgi * nq + q) + 1] = acc.y;
       }
       __syncthreads();
+      tick(5);
+      // granules of the row's partial sums
+      const unsigned tag = rtag;
       if (t < nq) {
         double2 d = z2;
-        for (int i = 0; i < seg; ++i)
-          d = cadd(d, make_double2(sh.red[2 * (t * seg + i)], sh.red[2 * (t * seg + i) + 1]));
-        double* pr = ar.part + ((size_t)par * G + g) * kPStride;
+        for (int i0 = 0; i0 < seg; i0 += kBatch) {
+          double2 v[kBatch];
+#pragma unroll
+          for (int i = 0; i < kBatch; ++i) {
+            const int ii = min(i0 + i, seg - 1) * nq + t;
+            v[i] = make_double2(sh.red[2 * ii], sh.red[2 * ii + 1]);
+          }
+#pragma unroll
+          for (int i = 0; i < kBatch; ++i)
+            if (i0 + i < seg) d = cadd(d, v[i]);
+        }
+        unsigned long long* pr = ar.part + ((size_t)par * G + g) * 2 * kPStride;
         if (t < K) {
-          st_sc1(pr + 2 * t, d.x);
-          st_sc1(pr + 2 * t + 1, d.y);
+          st_gran(pr + 4 * t, tag, d.x);
+          st_gran(pr + 4 * t + 2, tag, d.y);
         } else if (t == K) {
-          st_sc1(pr + 2 * K, d.x);
+          st_gran(pr + 4 * K, tag, d.x);
         } else {
-          st_sc1(pr + 2 * K + 1, j > 0 ? d.x : 0.0);
+          st_gran(pr + 4 * K + 2, tag, j > 0 ? d.x : 0.0);
         }
       }
     }
-    tick(0);
+    tick(6);
     epoch++;
-    // the neighbours' z rows are loaded after the all-reduce (whose flag orders them)
-    if (!allreduce_rows(ar, par, epoch, cols, sh.sum, sh.red, sh.ctl)) return;
-    tick(1);
+    // the neighbours' z rows of this round: the eight granules are requested now, before the
+    // all-reduce (their latency hides behind it), and checked after it -- as a rule they have
+    // arrived (the all-reduce needed the neighbours' partial sums, stored after them); any that
+    // have not are polled until they carry the round's tag
     const int glo = min(max(g - 1, 0), n - 1), ghi = min(g + 1, n - 1);
-    const double* zlo = a.zbuf + ((size_t)par * n + glo) * 2 * n + 2 * tc;
-    const double* zhi = a.zbuf + ((size_t)par * n + ghi) * 2 * n + 2 * tc;
-    const double2 zl = make_double2(ld_sc1(zlo), ld_sc1(zlo + 1));
-    const double2 zh = make_double2(ld_sc1(zhi), ld_sc1(zhi + 1));
+    const unsigned long long* zlo = a.zbuf + ((size_t)par * n + glo) * 4 * n + 4 * tc;
+    const unsigned long long* zhi = a.zbuf + ((size_t)par * n + ghi) * 4 * n + 4 * tc;
+    unsigned long long zg[8];
+    auto load_ghosts = [&] {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        zg[i] = __hip_atomic_load((gu64*)(zlo + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        zg[4 + i] = __hip_atomic_load((gu64*)(zhi + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    };
+    if (act) load_ghosts();
+    if (!allreduce_rows(ar, par, epoch, cols, sh.sum, sh.red)) return;
+    tick(1);
+    double2 zl = z2, zh = z2;
+    bool zok = true;
+    if (act) {
+      unsigned spins = 0;
+      for (;;) {
+        bool all = true;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) all = all && (unsigned)(zg[i] >> 32) == rtag;
+        if (all) break;
+        if (++spins > kSpinLimit) {
+          zok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        load_ghosts();
+      }
+      auto dbl = [](unsigned long long hi, unsigned long long lo) {
+        return __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
+      };
+      zl = make_double2(dbl(zg[0], zg[1]), dbl(zg[2], zg[3]));
+      zh = make_double2(dbl(zg[4], zg[5]), dbl(zg[6], zg[7]));
+    }
     // the lagged-normalisation step (krylov.hip gmres_lag_kernel), split: 1/|u_j| and the
     // update coefficients first (one thread per basis vector) ...
     const double vj = j >= 1 ? 1.0 / sqrt(sh.sum[2 * K + 1]) : sh.vs[0];
@@ -405,24 +510,48 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
       const double vk = t == j ? vj : sh.vs[t];
       const double2 d = make_double2(sh.sum[2 * t], sh.sum[2 * t + 1]);
       sh.coef[t] = cscale(cscale(d, vk), vk);  // krylov.hip update_kernel's coefficient
+      sh.red[t] = cabs2(d) * vk * vk;  // the Pythagorean terms of the next input's scale
       // column j of H (gmres_lag_kernel step (c)); the entries are untouched by the finishing
       // of column j-1 below
       sh.H[(size_t)j * R1 + t] = cscale(cscale(d, vk), vj / sh.ss[j]);
     }
-    __syncthreads();
+    if (__syncthreads_or(!zok)) {
+      if (t == 0)
+        __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
     tick(3);
     if (t < nrow) {
       // ... then u_{j+1} = z - sum_k c_k u_k on the own row and both ghost rows (neighbours'
       // z from the all-reduce's round; beyond the grid the ghost stays zero)
       if (act) {
+        // the three rows' chains interleaved (independent: 3x the FMA-latency overlap), the
+        // loads of kStep basis vectors in flight together; terms in k order per row
+        constexpr int kStep = 4;
+        double2 w[3] = {zl, z, zh};
+        for (int k0 = 0; k0 < K; k0 += kStep) {
+          double2 cv[kStep], uv[3][kStep];
+#pragma unroll
+          for (int i = 0; i < kStep; ++i) {
+            const int k = min(k0 + i, K - 1);
+            cv[i] = sh.coef[k];
+#pragma unroll
+            for (int r = 0; r < 3; ++r) uv[r][i] = Urow(k, r)[t];
+          }
+#pragma unroll
+          for (int i = 0; i < kStep; ++i)
+            if (k0 + i < K) {
+#pragma unroll
+              for (int r = 0; r < 3; ++r) w[r] = csub(w[r], cmul(cv[i], uv[r][i]));
+            }
+        }
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
           const int gr = g - 1 + r;
-          double2 w = r == 0 ? zl : (r == 1 ? z : zh);
-          for (int k = 0; k < K; ++k) w = csub(w, cmul(sh.coef[k], Urow(k, r)[t]));
-          Urow(j + 1, r)[t] = csel(gr >= 0 && gr < n, w, z2);
+          Urow(j + 1, r)[t] = csel(gr >= 0 && gr < n, w[r], z2);
         }
       }
+      tick(2);
     } else if (t == book) {
       // ... while the bookkeeping lane completes column j-1 (its subdiagonal from |u_j|,
       // rotations, presid, exit test) and starts column j
@@ -436,9 +565,13 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
         const double f = vj / sh.ss[j];
         const double w2 = sh.sum[2 * K];
         double rest = w2;
-        for (int k = 0; k <= j; ++k) {
-          const double vk = k == j ? vj : sh.vs[k];
-          rest -= cabs2(make_double2(sh.sum[2 * k], sh.sum[2 * k + 1])) * vk * vk;
+        for (int k0 = 0; k0 <= j; k0 += kBatch) {
+          double v[kBatch];
+#pragma unroll
+          for (int i = 0; i < kBatch; ++i) v[i] = sh.red[min(k0 + i, j)];
+#pragma unroll
+          for (int i = 0; i < kBatch; ++i)
+            if (k0 + i <= j) rest -= v[i];
         }
         sh.h0s[j] = sqrt(w2) * f;
         sh.ss[j + 1] = 1.0 / sqrt(fmax(rest, fmax(w2 * 1e-28, 1e-300)));
@@ -453,7 +586,9 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     }
   }
   if (prof)
-    for (int q = 0; q < 5; ++q) a.phase_ticks[q] += tk[q];
+    for (int q = 0; q < 7; ++q) a.phase_ticks[q] += tk[q];
+  if (prof)  // shader-clock cycles over the loop (the effective clock: slot 7 / sum of slots)
+    a.phase_ticks[7] += __builtin_amdgcn_s_memtime() - cyc0;
   if (!stopped) {
     // the cycle's last column needs |u_{stop_col+1}|: one more reduction round
     const int last = a.stop_col + 1;
@@ -462,10 +597,10 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
       const l2* ul = Urow(last, 1);
       double s = 0.0;
       for (int p = 0; p < n; ++p) s = fma(ul[p].x, ul[p].x, fma(ul[p].y, ul[p].y, s));
-      st_sc1(ar.part + ((size_t)par * G + g) * kPStride, s);
+      st_gran(ar.part + ((size_t)par * G + g) * 2 * kPStride, gran_tag(a.seq, epoch + 1), s);
     }
     epoch++;
-    if (!allreduce_rows(ar, par, epoch, 1, sh.sum, sh.red, sh.ctl)) return;
+    if (!allreduce_rows(ar, par, epoch, 1, sh.sum, sh.red)) return;
     if (t == 0) {
       const double sg = sqrt(sh.sum[0]);
       const int col = a.stop_col;
@@ -478,7 +613,7 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
   if (t == 0) {
     auto Hc = [&](int c, int k) -> l2& { return sh.H[(size_t)c * R1 + k]; };
     if (Hc(col, col).x == 0.0 && Hc(col, col).y == 0.0) sh.S[col] = z2;
-    double2 y[kMaxProj];
+    l2* y = sh.coef;  // (in LDS: a dynamically indexed register array would go to scratch)
     for (int k = 0; k <= col; ++k) y[k] = sh.S[k];
     for (int k = col; k > 0; --k) {
       if (y[k].x != 0.0 || y[k].y != 0.0) {
@@ -488,18 +623,87 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
       }
     }
     if (y[0].x != 0.0 || y[0].y != 0.0) y[0] = cdiv_smith(y[0], Hc(0, 0));
-    for (int k = 0; k <= col; ++k) sh.coef[k] = cscale(y[k], sh.vs[k]);
-    if (g == 0) {
-      a.g.ctrl[1] = col;
-      a.g.ctrl[0] = 1;
-    }
+    for (int k = 0; k <= col; ++k) y[k] = cscale(y[k], sh.vs[k]);
   }
   __syncthreads();
+  double2 xn = z2;
   if (act) {
     double2 acc = z2;
     for (int k = 0; k <= col; ++k) acc = cfma(sh.coef[k], Urow(k, 1)[t], acc);
     double2* xp = a.x + (size_t)g * n + t;
-    *xp = cadd(*xp, acc);
+    xn = cadd(*xp, acc);
+    *xp = xn;
+  }
+  // The next cycle's start (runtime.cpp residual): r = b - A x, V[0] = M r, |r|^2 and |M r|^2,
+  // in two more rounds -- the x rows to the neighbours (tagged granules), then a two-column
+  // all-reduce -- instead of two launches and a copy after this one.
+  const unsigned xtag = gran_tag(a.seq, epoch + 1);
+  if (act) {
+    unsigned long long* xo = a.xbuf + (size_t)g * 4 * n + 4 * t;
+    st_gran(xo, xtag, xn.x);
+    st_gran(xo + 2, xtag, xn.y);
+  }
+  double2 xl = z2, xh = z2;
+  bool xok = true;
+  if (act) {
+    const unsigned long long* xlo = a.xbuf + (size_t)min(max(g - 1, 0), n - 1) * 4 * n + 4 * tc;
+    const unsigned long long* xhi = a.xbuf + (size_t)min(g + 1, n - 1) * 4 * n + 4 * tc;
+    double v[4];
+    xok = ld_gran(xlo, xtag, &v[0]) && ld_gran(xlo + 2, xtag, &v[1]) &&
+          ld_gran(xhi, xtag, &v[2]) && ld_gran(xhi + 2, xtag, &v[3]);
+    xl = make_double2(v[0], v[1]);
+    xh = make_double2(v[2], v[3]);
+    sh.zrow[t] = xn;
+  }
+  if (__syncthreads_or(!xok)) {
+    if (t == 0)
+      __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  double r2 = 0.0, m2 = 0.0;
+  if (act) {
+    const double2 xC = sh.zrow[tc];
+    const double2 xW = csel(t > 0, sh.zrow[max(tc - 1, 0)], z2);
+    const double2 xE = csel(t < n - 1, sh.zrow[min(tc + 1, n - 1)], z2);
+    const double2 xS = csel(g > 0, xl, z2);
+    const double2 xN = csel(g < n - 1, xh, z2);
+    double2 Ax = cmul(S, xS);
+    Ax = cfma(W, xW, Ax);
+    Ax = cfma(D, xC, Ax);
+    Ax = cfma(E, xE, Ax);
+    Ax = cfma(N, xN, Ax);
+    const double2 rr = csub(a.b[(size_t)g * n + t], Ax);
+    const double2 mr = JAC ? cdiv(rr, D) : rr;
+    a.v0[(size_t)g * n + t] = mr;
+    r2 = cabs2(rr);
+    m2 = cabs2(mr);
+  }
+  // row sums in point order (two threads, the loads in flight in batches)
+  sh.red[2 * t] = r2;
+  sh.red[2 * t + 1] = m2;
+  __syncthreads();
+  const int par = epoch & 1;
+  epoch++;
+  if (t < 2) {
+    double sacc = 0.0;
+    for (int p0 = 0; p0 < n; p0 += kBatch) {
+      double v[kBatch];
+#pragma unroll
+      for (int i = 0; i < kBatch; ++i) v[i] = sh.red[2 * min(p0 + i, n - 1) + t];
+#pragma unroll
+      for (int i = 0; i < kBatch; ++i)
+        if (p0 + i < n) sacc += v[i];
+    }
+    st_gran(ar.part + ((size_t)par * G + g) * 2 * kPStride + 2 * t, xtag, sacc);
+  }
+  if (!allreduce_rows(ar, par, epoch, 2, sh.sum, sh.red)) return;
+  if (g == 0 && t == 0) {
+    a.red[4] = sh.sum[0];  // (device: the next cycle's |r|^2, |M r|^2)
+    a.red[5] = sh.sum[1];
+    a.report[4] = sh.sum[0];  // (host: this cycle's report)
+    a.report[5] = sh.sum[1];
+    a.g.ctrl[1] = col;
+    a.g.ctrl[0] = 1;
   }
 }
 
@@ -510,12 +714,13 @@ size_t small_cycle_lds_bytes(int n, int restart) {
   auto al = [](size_t b) { return (b + 15) / 16 * 16; };
   return al(16 * R1 * 3 * n) + al(16 * (size_t)n) + al(16 * (size_t)restart * R1) +
          al(32 * (size_t)restart) + 2 * al(16 * R1) + 2 * al(8 * R1) + al(8 * (size_t)restart) +
-         al(16 * (size_t)(kSmallThreads + kWave)) + al(8 * kPStride) + al(16);
+         al(8 * (size_t)(kRedRuns + kRuns)) + al(8 * kPStride) + al(16);
 }
 
 size_t small_cycle_scratch_doubles(int n) {
-  // z rows [2][n][2n], then the all-reduce rows [2][n][kPStride] and sums [2][kPStride]
-  return 2 * (size_t)n * 2 * n + 2 * (size_t)kPStride * (n + 1);
+  // 8-byte granules: z rows [2][n][4n], x rows [n][4n], the all-reduce rows [2][n][2 kPStride]
+  // and sums [2][2 kPStride]
+  return 12 * (size_t)n * n + 4 * (size_t)kPStride * (n + 1);
 }
 
 bool small_cycle_eligible(int n, int restart) {
@@ -525,11 +730,21 @@ bool small_cycle_eligible(int n, int restart) {
 
 template <bool C, bool J>
 void launch_one(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s) {
-  // dynamic LDS above 64 KB (gfx950 has 160 KB per CU) must be allowed per kernel, once
-  static const hipError_t attr = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(&gmres_small_cycle_kernel<C, J>),
-      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)attr;
+  // dynamic LDS above 64 KB (gfx950 has 160 KB per CU, the kernel's static LDS included) must
+  // be allowed per kernel, once
+  static const hipError_t attr = [] {
+    const void* fn = reinterpret_cast<const void*>(&gmres_small_cycle_kernel<C, J>);
+    hipFuncAttributes fa{};
+    hipError_t e = hipFuncGetAttributes(&fa, fn);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024 - (int)fa.sharedSizeBytes);
+  }();
+  if (attr != hipSuccess) {
+    (void)hipGetLastError();  // (reported here, not by the next unrelated check)
+    fail(HH_ERR_HIP, "small-grid GMRES cycle: cannot enable %zu B of dynamic LDS (%s)", lds,
+         hipGetErrorString(attr));
+  }
   hipLaunchKernelGGL((gmres_small_cycle_kernel<C, J>), grid, block, lds, s, a);
 }
 

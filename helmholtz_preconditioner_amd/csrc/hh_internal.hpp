@@ -220,19 +220,24 @@ struct SmallCycleArgs {
   const double2* tab_j;
   const double* invc2;     // or nullptr (constant medium)
   double invc2_const;
-  const double2* v0;       // V[0] = M r, unnormalised (scale g.vscale[0])
+  double2* v0;             // V[0] = M r, unnormalised: in, and out for the next cycle
+  const double* mnorm2;    // |M r|^2 (the residual's reduction; gmres_start_kernel's input)
+  const double2* b;        // right-hand side (the next cycle's residual)
   double2* x;              // x += V y at the end of the cycle
-  GivensState g;           // vscale[0], S[0] in; status_it, ctrl[0..1] out
+  double* red;             // device: red[4] = |r|^2, red[5] = |M r|^2 of the new x
+  double* report;          // host-mapped: report[4..5] the same, for the host's outer loop
+  GivensState g;           // status_it, ctrl[0..1] out (host-mapped: no copy after the cycle)
   double eps, ptol;
-  double* zbuf;            // [2][n][2n]  z rows handed to the neighbours
-  double* part;            // [2][n][2 (kMaxProj + 1) + 2] partial sums
-  unsigned* bar;           // barrier words (kSmallBarWords, zeroed before every launch)
-  unsigned* timeout_word;  // set when a barrier wait gives up
+  unsigned long long* zbuf;  // [2][n][4n] tagged granules of the z rows handed to the neighbours
+  unsigned long long* xbuf;  // [n][4n] tagged granules of the new x rows (the residual)
+  unsigned long long* part;  // [2][n][2 kSmallCols] tagged granules of the partial sums
+  unsigned long long* sums;  // [2][2 kSmallCols] tagged granules of the reduced sums
+  unsigned seq;            // launch sequence number: the tags of this launch's granules
+  unsigned* timeout_word;  // set when a wait gives up (zeroed at the start of a solve)
   unsigned long long* phase_ticks;  // optional [8]: workgroup 0's wall-clock ticks per phase
 };
-// all-reduce words of the small cycle: [0] arrival counter, [1] timeout word, [2] round flag;
-// zeroed before every launch (16 B)
-constexpr int kSmallBarWords = 4;
+// columns of the small cycle's all-reduce rows: 2 K dot halves, |z|^2, |u_j|^2 (K <= kMaxProj)
+constexpr int kSmallCols = 2 * (kMaxProj + 1) + 2;
 bool small_cycle_eligible(int n, int restart);
 size_t small_cycle_lds_bytes(int n, int restart);
 size_t small_cycle_scratch_doubles(int n);

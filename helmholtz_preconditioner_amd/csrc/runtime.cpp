@@ -13,6 +13,7 @@
 #include <complex>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <limits>
 #include <memory>
 #include <string>
@@ -74,9 +75,22 @@ struct hh_ctx {
   hipStream_t stream = nullptr;   // compute
   hipStream_t cstream = nullptr;  // halo exchange + boundary rows (highest priority)
   hipEvent_t ev_in = nullptr, ev_halo = nullptr;
+  hipEvent_t ev_sync = nullptr;   // end of a GMRES cycle's queue (spin_sync)
   double* dscratch = nullptr;     // device scratch for host collectives
   double* hpinned = nullptr;      // pinned host staging
 };
+
+namespace {
+// layout of the per-operator reduction buffer `red` (device) and its host mirror status_h:
+// [0, 256) reductions (norms at 0..15, dots from 16), [256, 384) the cycle's per-iteration
+// statuses (4 x restart), [384, 388) the cycle's control words (ints), [388] the small cycle's
+// timeout word; the end of a cycle copies [0, kRedReport) once
+constexpr int kRedDoubles = 512;
+constexpr int kRedStatus = 256;
+constexpr int kRedCtrl = 384;
+constexpr int kRedTimeout = 388;
+constexpr int kRedReport = 389;
+}  // namespace
 
 namespace {
 struct Slab {
@@ -143,13 +157,12 @@ struct hh_op {
   // whole-cycle kernel for small grids (gmres_small.hip): hand-off scratch and barrier words
   int small_cycle = -1;     // -1 auto, 0 off, 1 on where eligible (hh_op_set_small_cycle)
   double* small_scr = nullptr;
-  unsigned* small_bar = nullptr;  // [4]: arrival counter, timeout word (16 B, zeroed per launch)
+  unsigned small_seq = 0;          // launch sequence number (the tags of its hand-off granules)
   unsigned long long* small_ticks = nullptr;  // phase timing of the small cycle (diagnostic)
   // timing hooks
   hipEvent_t tk0 = nullptr, tk1 = nullptr;
   // device stop flag of the GMRES cycle being queued (nullptr outside hh_gmres)
   const int* stop_flag = nullptr;
-  int* gctrl = nullptr;
   // sweeping preconditioner (HH_PREC_SWEEP / HH_PREC_SWEEP_REF)
   SweepArgs sweep{};
   double2* sw_P = nullptr;
@@ -173,6 +186,9 @@ struct hh_op {
   // hh_op_set_cycle_callback: scipy's callback_type='x' hook, once per restart cycle
   hh_gmres_cycle_callback cycle_cb = nullptr;
   void* cycle_user = nullptr;
+  // hh_op_set_history_callback: the per-iteration statuses of a cycle in one call
+  hh_gmres_history_callback hist_cb = nullptr;
+  void* hist_user = nullptr;
   int grid_override = 0;
   hh_stats stats{};
 };
@@ -571,9 +587,7 @@ void residual(hh_op* op, const double2* b, const double2* x, double2* v0, int ds
   switch (op->pkind) {
     case HH_PREC_NONE: {
       const int np = run_stencil(op, EPI_RES, x, nullptr, b, v0, nullptr, false);
-      reduce_norms(op, np, dst, 1);
-      HIPC(hipMemcpyAsync(op->red + dst + 1, op->red + dst, sizeof(double),
-                          hipMemcpyDeviceToDevice, op->ctx->stream));
+      reduce_norms(op, np, dst, 1);  // (|M r| = |r|: readers take red[dst], see mnorm_slot)
       break;
     }
     case HH_PREC_JACOBI: {
@@ -603,6 +617,29 @@ void residual(hh_op* op, const double2* b, const double2* x, double2* v0, int ds
     }
   }
 }
+
+// Waits for everything queued on `s` by polling an event (a busy host thread): the end of a
+// GMRES cycle is on the critical path of the next one, and a blocking stream synchronisation
+// adds the wake-up latency of the sleeping host thread to every cycle.
+void spin_sync(hh_ctx* c, hipStream_t s) {
+  static const int mode = [] {
+    const char* v = std::getenv("HH_SYNC_MODE");  // diagnostic: 0 block, 1 spin, 2 spin+yield
+    return v ? std::atoi(v) : 2;
+  }();
+  if (mode == 0) {
+    HIPC(hipStreamSynchronize(s));
+    return;
+  }
+  HIPC(hipEventRecord(c->ev_sync, s));
+  hipError_t e;
+  while ((e = hipEventQuery(c->ev_sync)) == hipErrorNotReady) {
+    if (mode == 2) std::this_thread::yield();
+  }
+  HIPC(e);
+}
+
+// where residual(op, .., dst) left |M r|^2: red[dst + 1], or red[dst] itself for M = none
+int mnorm_slot(const hh_op* op, int dst) { return op->pkind == HH_PREC_NONE ? dst : dst + 1; }
 
 void read_dev(hh_op* op, const double* dsrc, double* hdst, int count) {
   HIPC(hipMemcpyAsync(op->status_h, dsrc, count * sizeof(double), hipMemcpyDeviceToHost,
@@ -634,10 +671,11 @@ void ensure_gmres(hh_op* op, int restart) {
   g.status_it = g.status + 8;
   g.sscale = g.status_it + 4 * (size_t)restart;
   if (!op->npart) op->npart = dalloc<double>((size_t)kMaxStreamBlocks * kMaxNorms);
-  dfree(op->gctrl);
-  op->gctrl = dalloc<int>(8);
-  HIPC(hipMemsetAsync(op->gctrl, 0, 8 * sizeof(int), op->ctx->stream));
-  g.ctrl = op->gctrl;
+  // the per-iteration statuses and the cycle's control words live in the reduction buffer,
+  // next to the residual norms: the end of a cycle reads them all with ONE copy (kRedReport)
+  g.status_it = op->red + kRedStatus;
+  g.ctrl = reinterpret_cast<int*>(op->red + kRedCtrl);
+  HIPC(hipMemsetAsync(g.ctrl, 0, 8 * sizeof(int), op->ctx->stream));
   g.restart = restart;
 }
 
@@ -714,6 +752,7 @@ HH_API int hh_ctx_create_ex(int device, int rank, int world, const unsigned char
     HIPC(hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, prio_greatest));
     HIPC(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
     HIPC(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
+    HIPC(hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming));
     c->dscratch = dalloc<double>(256);
     HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpinned), 256 * sizeof(double)));
     if (world > 1)
@@ -722,6 +761,7 @@ HH_API int hh_ctx_create_ex(int device, int rank, int world, const unsigned char
   } catch (...) {
     if (c->ev_in) (void)hipEventDestroy(c->ev_in);
     if (c->ev_halo) (void)hipEventDestroy(c->ev_halo);
+    if (c->ev_sync) (void)hipEventDestroy(c->ev_sync);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
     dfree(c->dscratch);
@@ -746,6 +786,7 @@ static void ctx_release(hh_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   c->comm.reset();
   (void)hipEventDestroy(c->ev_in);
+  if (c->ev_sync) (void)hipEventDestroy(c->ev_sync);
   (void)hipEventDestroy(c->ev_halo);
   (void)hipStreamDestroy(c->stream);
   (void)hipStreamDestroy(c->cstream);
@@ -947,8 +988,9 @@ HH_API int hh_op_create(hh_ctx* c, int n, int b, double cconst, double eta, doub
     cap = std::max(cap, (size_t)c->vslabs * 2048 * kMaxNorms);
     op->partials = dalloc<double>(cap);
     op->partials_cap = cap;
-    op->red = dalloc<double>(256);
-    HIPC(hipHostMalloc(reinterpret_cast<void**>(&op->status_h), 256 * sizeof(double)));
+    op->red = dalloc<double>(kRedDoubles);
+    HIPC(hipMemset(op->red, 0, kRedDoubles * sizeof(double)));
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&op->status_h), kRedDoubles * sizeof(double)));
     HIPC(hipDeviceSynchronize());
   } catch (...) {
     delete op;  // device memory of a failed create is reclaimed at process exit
@@ -985,10 +1027,8 @@ static void op_release(hh_op* op) {
   dfree(op->scrR);
   dfree(op->V);
   dfree(op->gbuf);
-  dfree(op->gctrl);
   dfree(op->npart);
   dfree(op->small_scr);
-  dfree(op->small_bar);
   dfree(op->small_ticks);
   dfree(op->sw_P);
   dfree(op->sw_y);
@@ -1384,6 +1424,14 @@ HH_API int hh_op_set_cycle_callback(hh_op* op, hh_gmres_cycle_callback cb, void*
   GUARD_END
 }
 
+HH_API int hh_op_set_history_callback(hh_op* op, hh_gmres_history_callback cb, void* user) {
+  GUARD_BEGIN
+  REQUIRE(op, "null op");
+  op->hist_cb = cb;
+  op->hist_user = user;
+  GUARD_END
+}
+
 HH_API int hh_op_set_stencil(hh_op* op, int points, double alpha, double c, double d) {
   GUARD_BEGIN
   REQUIRE(op, "null op");
@@ -1439,7 +1487,8 @@ HH_API int hh_op_small_cycle_profile(hh_op* op, int enable, double* phase_us) {
     int mhz = 100;  // s_memrealtime: a constant 100 MHz clock on gfx9
     (void)hipDeviceGetAttribute(&mhz, hipDeviceAttributeWallClockRate, op->ctx->device);
     const double khz = mhz > 0 ? (double)mhz : 100000.0;  // (the attribute is in kHz)
-    for (int q = 0; q < 8; ++q) phase_us[q] = t[q] * 1e3 / khz;
+    for (int q = 0; q < 7; ++q) phase_us[q] = t[q] * 1e3 / khz;
+    phase_us[7] = (double)t[7];  // shader-clock cycles over the same span (s_memtime)
   }
   if (enable && !op->small_ticks) op->small_ticks = dalloc<unsigned long long>(8);
   if (op->small_ticks) HIPC(hipMemset(op->small_ticks, 0, 8 * sizeof(unsigned long long)));
@@ -1634,9 +1683,14 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
                      (op->pkind == HH_PREC_NONE || op->pkind == HH_PREC_JACOBI) &&
                      (op->krylov_mode != 1) && small_cycle_eligible(op->n, restart) &&
                      (op->small_cycle == 1 || (size_t)op->n * op->n <= ((size_t)1 << 18));
-  if (small && !op->small_scr) {
-    op->small_scr = dalloc<double>(small_cycle_scratch_doubles(op->n));
-    op->small_bar = dalloc<unsigned>(kSmallBarWords);
+  unsigned* small_timeout = reinterpret_cast<unsigned*>(op->red + kRedTimeout);
+  if (small) {
+    if (!op->small_scr) {
+      const size_t nd = small_cycle_scratch_doubles(op->n);
+      op->small_scr = dalloc<double>(nd);
+      HIPC(hipMemsetAsync(op->small_scr, 0, nd * sizeof(double), s));  // (no stale tags)
+    }
+    HIPC(hipMemsetAsync(small_timeout, 0, sizeof(double), s));
   }
 
   for (long iteration = 0; iteration < maxiter; ++iteration) {
@@ -1649,7 +1703,8 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       }
     }
     // v[0] = psolve(r) / ||psolve(r)||, S[0] = ||psolve(r)|| (lazy scale); clears the stop flag
-    launch_gmres_start(g, op->red, 4, 5, s);
+    // (the whole-cycle kernel scales V[0] itself)
+    if (!small) launch_gmres_start(g, op->red, 4, mnorm_slot(op, 4), s);
     // The whole cycle is queued at once: the column kernel evaluates scipy's inner exit test
     // (presid <= ptol, breakdown, legacy maxiter) and raises the stop flag, after which the
     // kernels still queued in this cycle return immediately.  One host sync per cycle.
@@ -1669,16 +1724,27 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       sa.invc2 = op->const_c ? nullptr : sl.invc2;
       sa.invc2_const = op->invc2_const;
       sa.v0 = V;
+      sa.mnorm2 = op->red + mnorm_slot(op, 4);
+      sa.b = b;
       sa.x = x;
+      sa.red = op->red;
+      // the cycle's report goes straight to the pinned host mirror (same layout as red): no
+      // copy after the launch; ctrl[0] = 1 marks it complete
+      sa.report = op->status_h;
       sa.g = g;
+      sa.g.status_it = op->status_h + kRedStatus;
+      sa.g.ctrl = reinterpret_cast<int*>(op->status_h + kRedCtrl);
+      sa.g.ctrl[0] = 0;
       sa.eps = eps;
       sa.ptol = ptol;
-      sa.zbuf = op->small_scr;
-      sa.part = op->small_scr + 2 * (size_t)op->n * 2 * op->n;
-      sa.bar = op->small_bar;
-      sa.timeout_word = op->small_bar + 1;  // (words[4 ..]: the eight group counters)
+      sa.zbuf = reinterpret_cast<unsigned long long*>(op->small_scr);
+      sa.xbuf = sa.zbuf + 8 * (size_t)op->n * op->n;
+      sa.part = sa.xbuf + 4 * (size_t)op->n * op->n;
+      sa.sums = sa.part + 2 * (size_t)op->n * 2 * kSmallCols;
+      sa.seq = (++op->small_seq) & 0xffffffu;
+      if (sa.seq == 0) sa.seq = op->small_seq = 1;  // (tag 0 is the zeroed scratch)
+      sa.timeout_word = small_timeout;
       sa.phase_ticks = op->small_ticks;
-      HIPC(hipMemsetAsync(op->small_bar, 0, kSmallBarWords * sizeof(unsigned), s));
       launch_small_cycle(sa, op->const_c, op->pkind == HH_PREC_JACOBI, s);
       HIPC(hipGetLastError());
     }
@@ -1745,39 +1811,48 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     op->stop_flag = nullptr;  // (the SolveScope also clears it if anything above throws)
     // one sync: per-iteration statuses + the last column executed (the whole-cycle kernel has
     // already updated x: its true residual is queued behind it and read in the same sync)
-    if (small) residual(op, b, x, V, 4);  // r = b - A x; V[0] = M r for the next cycle
-    HIPC(hipMemcpyAsync(op->status_h, g.status_it, 4 * (size_t)restart * sizeof(double),
-                        hipMemcpyDeviceToHost, s));
-    HIPC(hipMemcpyAsync(op->status_h + 4 * restart, g.ctrl, 2 * sizeof(int),
-                        hipMemcpyDeviceToHost, s));
-    if (small) {
-      HIPC(hipMemcpyAsync(op->status_h + 4 * restart + 1, op->small_bar + 1, sizeof(unsigned),
+    // (the whole-cycle kernel has also computed the next cycle's residual, V[0] and norms,
+    // and written its report to the host mirror itself)
+    if (!small)
+      HIPC(hipMemcpyAsync(op->status_h, op->red, kRedReport * sizeof(double),
                           hipMemcpyDeviceToHost, s));
-      HIPC(hipMemcpyAsync(op->status_h + 4 * restart + 2, op->red + 4, sizeof(double),
-                          hipMemcpyDeviceToHost, s));
-    }
-    HIPC(hipStreamSynchronize(s));
+    spin_sync(c, s);
+    const double* sth = op->status_h + kRedStatus;
     int ctl[2];
-    std::memcpy(ctl, op->status_h + 4 * restart, 2 * sizeof(int));
-    if (small) {
+    std::memcpy(ctl, op->status_h + kRedCtrl, 2 * sizeof(int));
+    if (small && ctl[0] != 1) {
+      double w = 0.0;
+      read_dev(op, op->red + kRedTimeout, &w, 1);
       unsigned tmo = 0;
-      std::memcpy(&tmo, op->status_h + 4 * restart + 1, sizeof(unsigned));
-      REQUIRE(tmo == 0, "small-grid GMRES cycle: a grid barrier timed out (workgroups not "
+      std::memcpy(&tmo, &w, sizeof(unsigned));
+      REQUIRE(tmo == 0, "small-grid GMRES cycle: a grid-wide wait timed out (workgroups not "
                         "co-resident?); hh_op_set_small_cycle(op, 0) selects the regular cycle");
+      fail(HH_ERR_STATE, "small-grid GMRES cycle ended without its report");
     }
     col = ctl[1];
     REQUIRE(col >= 0 && col <= stop_col, "GMRES cycle state corrupt (last column %d)", col);
+    double rel[kMaxProj];
+    const long first = inner + 1;
     for (int k = 0; k <= col; ++k) {
-      const double pr = op->status_h[4 * k];
+      const double pr = sth[4 * k];
       inner += 1;
-      if (hist && inner - 1 < hist_cap) hist[inner - 1] = pr / bnrm2;
-      if (cb && cb(user, inner, pr / bnrm2) != 0) {
+      rel[k] = pr / bnrm2;
+      if (hist && inner - 1 < hist_cap) hist[inner - 1] = rel[k];
+      if (cb && cb(user, inner, rel[k]) != 0) {
         finish(inner, -1, 0.0);
         fail(HH_ERR_ABORTED, "gmres stopped by the per-iteration callback at iteration %ld", inner);
       }
     }
-    presid = op->status_h[4 * col];
-    breakdown = op->status_h[4 * col + 1] != 0.0;
+    if (op->hist_cb) {
+      const int r = op->hist_cb(op->hist_user, first, col + 1, rel);
+      if (r != 0) {
+        const long at = first - 1 + (r >= 1 && r <= col + 1 ? r : col + 1);
+        finish(at, -1, 0.0);
+        fail(HH_ERR_ABORTED, "gmres stopped by the history callback at iteration %ld", at);
+      }
+    }
+    presid = sth[4 * col];
+    breakdown = sth[4 * col + 1] != 0.0;
     op->stats.restarts++;
     if (!small) {  // (the whole-cycle kernel has solved and updated x itself)
       launch_gmres_solve(g, col, s);
@@ -1785,7 +1860,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       residual(op, b, x, V, 4);  // r = b - A x; V[0] = M r for the next cycle
       read_dev(op, op->red + 4, st, 1);
     } else {
-      st[0] = op->status_h[4 * restart + 2];
+      st[0] = op->status_h[4];  // (the residual queued behind the cycle kernel)
     }
     rnorm = std::sqrt(st[0]);
     if (legacy && inner == maxiter) {

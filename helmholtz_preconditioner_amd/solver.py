@@ -86,20 +86,24 @@ def gmres(A, b, x0=None, *, rtol=1e-5, atol=0., restart=None, maxiter=None, M=No
     cap = int(min(cap, 1 << 22))
     hist = np.zeros(max(cap, 1), dtype=np.float64)
     cb = _ffi.GMRES_CALLBACK(0)
+    hcb = _ffi.GMRES_HISTORY_CALLBACK(0)
     ccb = _ffi.GMRES_CYCLE_CALLBACK(0)
     # An exception raised by the user's callback propagates out of gmres, as in scipy: the
     # trampoline stores it and returns non-zero, hh_gmres stops at once (HH_ERR_ABORTED), and
     # the stored exception is re-raised here (ctypes would otherwise print and drop it).
     raised = []
     if callback is not None and callback_type in ('legacy', 'pr_norm'):
-        def _cb(_user, _it, rel):
-            try:
-                callback(rel)
-            except BaseException as e:  # noqa: BLE001 -- re-raised after hh_gmres returns
-                raised.append(e)
-                return 1
+        # one foreign call per restart cycle (hh_op_set_history_callback), the user's callback
+        # still once per inner iteration, in order, where scipy calls it
+        def _hcb(_user, _first, count, rel):
+            for i, r in enumerate(rel[:count]):  # (one conversion of the cycle's values)
+                try:
+                    callback(r)
+                except BaseException as e:  # noqa: BLE001 -- re-raised after hh_gmres returns
+                    raised.append(e)
+                    return i + 1
             return 0
-        cb = _ffi.GMRES_CALLBACK(_cb)
+        hcb = _ffi.GMRES_HISTORY_CALLBACK(_hcb)
     elif callback is not None:  # 'x': the iterate after every restart cycle (downloaded for
         def _ccb(_user, _cycle):  # numpy b, the DeviceVector itself otherwise)
             try:
@@ -111,6 +115,7 @@ def gmres(A, b, x0=None, *, rtol=1e-5, atol=0., restart=None, maxiter=None, M=No
         ccb = _ffi.GMRES_CYCLE_CALLBACK(_ccb)
     iters, info, rnorm, bnorm = ctypes.c_long(), ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
     check(lib.hh_op_set_cycle_callback(A.handle, ccb, None))
+    check(lib.hh_op_set_history_callback(A.handle, hcb, None))
     try:
         rc = lib.hh_gmres(A.handle, bv.handle, xv.handle, float(rtol), float(atol),
                           int(restart), int(maxiter), int(legacy), int(bool(reorth)),
@@ -121,6 +126,7 @@ def gmres(A, b, x0=None, *, rtol=1e-5, atol=0., restart=None, maxiter=None, M=No
         check(rc)
     finally:
         check(lib.hh_op_set_cycle_callback(A.handle, _ffi.GMRES_CYCLE_CALLBACK(0), None))
+        check(lib.hh_op_set_history_callback(A.handle, _ffi.GMRES_HISTORY_CALLBACK(0), None))
     A.last_solve = dict(iterations=iters.value, info=info.value, rnorm=rnorm.value,
                         bnorm=bnorm.value, stats=A.stats())
     x = xv.download() if host_in else xv

@@ -204,6 +204,17 @@ int hh_gmres(hh_op* op, const hh_vec* b, hh_vec* x, double rtol, double atol,
  * to continue, non-zero to stop (HH_ERR_ABORTED). */
 typedef int (*hh_gmres_cycle_callback)(void* user, long cycle);
 int hh_op_set_cycle_callback(hh_op* op, hh_gmres_cycle_callback cb, void* user);
+/* Batched form of hh_gmres's per-iteration callback for the following hh_gmres calls on `op`
+ * (NULL removes it): called once per restart cycle, when that cycle's statuses reach the host
+ * (the same point the per-iteration callback is called at), with the cycle's `count` values
+ * presid/||b|| of iterations first_iteration .. first_iteration + count - 1.  One call per
+ * cycle instead of one per iteration (a foreign-function caller such as ctypes pays its call
+ * overhead once).  Returns 0 to continue, or r in [1, count] when the caller stopped after the
+ * r-th value (any other non-zero value: after the last one); the solve then ends with
+ * HH_ERR_ABORTED and iterations = first_iteration - 1 + r. */
+typedef int (*hh_gmres_history_callback)(void* user, long first_iteration, int count,
+                                         const double* rel_presid);
+int hh_op_set_history_callback(hh_op* op, hh_gmres_history_callback cb, void* user);
 
 /* Global reductions per GMRES inner iteration (no reference counterpart: scipy runs on one
  * process).  mode 1: classical Gram-Schmidt with two -- the projections (+ |w|^2), then the norm
@@ -224,8 +235,9 @@ int hh_op_set_krylov_mode(hh_op* op, int mode);
 int hh_op_set_small_cycle(hh_op* op, int mode);
 /* Diagnostic: phase timing of the small-grid cycle kernel (workgroup 0's wall clock summed over
  * the following solves): phase_us (optional, 8 doubles) receives the totals so far in us
- * (0 stencil + partial sums, 1 grid barrier, 2 partial reduction, 3 lagged Givens step, 4 basis
- * update), then the counters restart (enable = 1) or stop (enable = 0). */
+ * (0 stencil + z hand-off, 5 partial sums, 6 their publication, 1 all-reduce, 3 coefficients +
+ * the neighbours' z, 2 basis update, 4 wait for the Givens step) and in [7] the shader-clock
+ * cycles over the same span; then the counters restart (enable = 1) or stop (enable = 0). */
 int hh_op_small_cycle_profile(hh_op* op, int enable, double* phase_us);
 /* Performance tuning of the stencil kernel used by HH_APPLY_A: variant in [0, 48) selects the
  * marching kernel's W/E exchange (LDS row / direct cached loads / wave shuffle), prefetch depth,

@@ -150,6 +150,58 @@ def test_callback_exception_propagates(op, callback_type):
     assert info == infor and np.max(np.abs(hist - histr) / histr) < 1e-6
 
 
+@pytest.mark.parametrize("small", ["on", "off"])
+def test_per_iteration_and_history_callbacks_agree(op, small):
+    """hh_gmres's per-iteration callback (raw ABI) and the batched history callback the shim
+    uses receive the same values in the same order; a stop request from either ends the solve
+    with HH_ERR_ABORTED at the iteration it names"""
+    import ctypes
+    F = H._ffi
+    A, R, _ = op
+    A.small_cycle(small)
+    f = np.ones(A.shape[0], complex)
+    bv, maxiter = A.vector(f), 23
+
+    def run(per_it_stop=0, hist_stop=0):
+        xv = A.vector()
+        per, batch = [], []
+
+        def _cb(_u, it, rel):
+            per.append((it, rel))
+            return 1 if it == per_it_stop else 0
+
+        def _hcb(_u, first, count, rel):
+            for i in range(count):
+                batch.append((first + i, rel[i]))
+                if first + i == hist_stop:
+                    return i + 1
+            return 0
+        cb, hcb = F.GMRES_CALLBACK(_cb), F.GMRES_HISTORY_CALLBACK(_hcb)
+        F.check(F.lib.hh_op_set_history_callback(A.handle, hcb, None))
+        hist = np.zeros(maxiter)
+        it, info = ctypes.c_long(), ctypes.c_int()
+        rn, bn = ctypes.c_double(), ctypes.c_double()
+        try:
+            rc = F.lib.hh_gmres(A.handle, bv.handle, xv.handle, 1e-12, 0.0, 5, maxiter, 1, 0,
+                                F.dptr(hist), maxiter, cb, None, ctypes.byref(it),
+                                ctypes.byref(info), ctypes.byref(rn), ctypes.byref(bn))
+        finally:
+            F.check(F.lib.hh_op_set_history_callback(A.handle, F.GMRES_HISTORY_CALLBACK(0),
+                                                     None))
+        return rc, it.value, per, batch, hist
+
+    rc, it, per, batch, hist = run()
+    assert rc == 0 and it == maxiter
+    assert per == batch and [p[0] for p in per] == list(range(1, maxiter + 1))
+    assert np.array_equal(np.array([p[1] for p in per]), hist)
+    rc, it, per, batch, _ = run(per_it_stop=7)
+    assert rc == F.HH_ERR_ABORTED and it == 7 and len(per) == 7
+    rc, it, per, batch, _ = run(hist_stop=8)
+    assert rc == F.HH_ERR_ABORTED and it == 8 and batch[-1][0] == 8
+    A.small_cycle("auto")
+    _still_works(A, R)
+
+
 def test_aborted_asis_sweep_leaves_no_constant_map(ctx):
     """Sweeping(reference=True) makes M a constant map (algo2_4(b), quirk Q1) for the
     duration of a solve only: after a solve aborted by its callback, a plain M x is

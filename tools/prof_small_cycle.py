@@ -19,6 +19,8 @@ p.add_argument("--n", type=int, default=128)
 p.add_argument("--iters", type=int, default=200)
 p.add_argument("--wave-num", type=float, default=8.0)
 p.add_argument("--precond", default="none")
+p.add_argument("--cb", default="lambda", choices=["lambda", "none"],
+               help="legacy callback (as bench.py) or none (host cost of the callback)")
 a = p.parse_args()
 n = a.n
 om, h, eta = H.problem_params(n, 12, a.wave_num, 2.0)
@@ -32,12 +34,18 @@ for mode in ("on", "off", "on"):
     ph = (ctypes.c_double * 8)()
     _ffi.check(_ffi.lib.hh_op_small_cycle_profile(A.handle, 1, ph))
     t0 = time.perf_counter()
-    H.gmres(A, f, rtol=1e-14, restart=20, maxiter=a.iters, M=M, callback=lambda r: None,
-            callback_type="legacy")
+    if a.cb == "lambda":
+        H.gmres(A, f, rtol=1e-14, restart=20, maxiter=a.iters, M=M, callback=lambda r: None,
+                callback_type="legacy")
+    else:  # (maxiter then counts cycles: iters // 20 of them)
+        H.gmres(A, f, rtol=1e-14, restart=20, maxiter=a.iters // 20, M=M)
     dt = time.perf_counter() - t0
     _ffi.check(_ffi.lib.hh_op_small_cycle_profile(A.handle, 0, ph))
-    per = [ph[q] / a.iters for q in range(5)]
+    per = [ph[q] / a.iters for q in (0, 5, 6, 1, 3, 2, 4)]
+    span = sum(ph[q] for q in range(7))
+    mhz = ph[7] / span if span > 0 else 0.0
     print(f"n={n} small_cycle={mode}: {a.iters / dt:9.1f} it/s ({dt / a.iters * 1e6:6.2f} us/it)"
           + ("" if mode == "off" else
-             "  phases us/it: stencil+dots %.2f allreduce %.2f - %.2f coef %.2f update+givens %.2f"
-             % tuple(per)), flush=True)
+             "  phases us/it: stencil %.2f dots %.2f publish %.2f allreduce %.2f coef+ghosts %.2f"
+             " update %.2f givens-wait %.2f  (shader clock %.0f MHz)"
+             % tuple(per + [mhz])), flush=True)
