@@ -13,7 +13,6 @@
 #include <complex>
 #include <cstdlib>
 #include <cstring>
-#include <thread>
 #include <limits>
 #include <memory>
 #include <string>
@@ -75,7 +74,6 @@ struct hh_ctx {
   hipStream_t stream = nullptr;   // compute
   hipStream_t cstream = nullptr;  // halo exchange + boundary rows (highest priority)
   hipEvent_t ev_in = nullptr, ev_halo = nullptr;
-  hipEvent_t ev_sync = nullptr;   // end of a GMRES cycle's queue (spin_sync)
   double* dscratch = nullptr;     // device scratch for host collectives
   double* hpinned = nullptr;      // pinned host staging
 };
@@ -618,26 +616,6 @@ void residual(hh_op* op, const double2* b, const double2* x, double2* v0, int ds
   }
 }
 
-// Waits for everything queued on `s` by polling an event (a busy host thread): the end of a
-// GMRES cycle is on the critical path of the next one, and a blocking stream synchronisation
-// adds the wake-up latency of the sleeping host thread to every cycle.
-void spin_sync(hh_ctx* c, hipStream_t s) {
-  static const int mode = [] {
-    const char* v = std::getenv("HH_SYNC_MODE");  // diagnostic: 0 block, 1 spin, 2 spin+yield
-    return v ? std::atoi(v) : 2;
-  }();
-  if (mode == 0) {
-    HIPC(hipStreamSynchronize(s));
-    return;
-  }
-  HIPC(hipEventRecord(c->ev_sync, s));
-  hipError_t e;
-  while ((e = hipEventQuery(c->ev_sync)) == hipErrorNotReady) {
-    if (mode == 2) std::this_thread::yield();
-  }
-  HIPC(e);
-}
-
 // where residual(op, .., dst) left |M r|^2: red[dst + 1], or red[dst] itself for M = none
 int mnorm_slot(const hh_op* op, int dst) { return op->pkind == HH_PREC_NONE ? dst : dst + 1; }
 
@@ -752,7 +730,6 @@ HH_API int hh_ctx_create_ex(int device, int rank, int world, const unsigned char
     HIPC(hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, prio_greatest));
     HIPC(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
     HIPC(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
-    HIPC(hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming));
     c->dscratch = dalloc<double>(256);
     HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpinned), 256 * sizeof(double)));
     if (world > 1)
@@ -761,7 +738,6 @@ HH_API int hh_ctx_create_ex(int device, int rank, int world, const unsigned char
   } catch (...) {
     if (c->ev_in) (void)hipEventDestroy(c->ev_in);
     if (c->ev_halo) (void)hipEventDestroy(c->ev_halo);
-    if (c->ev_sync) (void)hipEventDestroy(c->ev_sync);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
     dfree(c->dscratch);
@@ -786,7 +762,6 @@ static void ctx_release(hh_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   c->comm.reset();
   (void)hipEventDestroy(c->ev_in);
-  if (c->ev_sync) (void)hipEventDestroy(c->ev_sync);
   (void)hipEventDestroy(c->ev_halo);
   (void)hipStreamDestroy(c->stream);
   (void)hipStreamDestroy(c->cstream);
@@ -1816,7 +1791,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     if (!small)
       HIPC(hipMemcpyAsync(op->status_h, op->red, kRedReport * sizeof(double),
                           hipMemcpyDeviceToHost, s));
-    spin_sync(c, s);
+    HIPC(hipStreamSynchronize(s));
     const double* sth = op->status_h + kRedStatus;
     int ctl[2];
     std::memcpy(ctl, op->status_h + kRedCtrl, 2 * sizeof(int));
