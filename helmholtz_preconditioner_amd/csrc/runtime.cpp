@@ -168,6 +168,8 @@ struct hh_op {
   double2* sw_uF = nullptr;
   double2* sw_const = nullptr;  // as-is (quirk Q1): M x = algo2_4(b) for every x
   double2* sw_T = nullptr;      // dense transfer matrices (sweep_dense.hip), or null
+  unsigned long long* sw_chain = nullptr;  // granules of the persistent apply chain, or null
+  unsigned sw_seq = 0;                     // its launch sequence number
   double2* sw_u = nullptr;      // dense apply scratch (n^2)
   double2* sw_in = nullptr;     // dense apply: fixed input / output the captured graphs use
   double2* sw_out = nullptr;
@@ -447,6 +449,8 @@ void sweep_dense_release(hh_op* op) {
   for (auto& g : op->sw_graphs) (void)hipGraphExecDestroy(g.exec);
   op->sw_graphs.clear();
   dfree(op->sw_T);
+  dfree(op->sw_chain);
+  op->sw_chain = nullptr;
   dfree(op->sw_u);
   dfree(op->sw_in);
   dfree(op->sw_out);
@@ -457,6 +461,24 @@ void sweep_dense_release(hh_op* op) {
 // corrected: u = T u), backward sweeps.  r and out must differ.
 void sweep_apply(hh_op* op, const double2* r, double2* out, bool asis) {
   hipStream_t s = op->ctx->stream;
+  if (op->sw_T && op->sw_chain) {
+    // F0 (one batched launch) + the persistent chain (one cooperative launch): no graph needed
+    SweepArgs a = op->sweep;
+    a.stop = op->stop_flag;
+    ChainArgs c{};
+    c.gbuf = op->sw_chain;
+    c.timeout = reinterpret_cast<unsigned*>(op->red + kRedTimeout);
+    static const int diag = [] {
+      const char* e = std::getenv("HH_SWEEP_DIAG");
+      return e ? std::atoi(e) : 0;
+    }();
+    c.diag = diag;
+    c.seq = (++op->sw_seq) & 0xfffffu;
+    if (c.seq == 0) c.seq = op->sw_seq = 1;  // (tag 0 is the zeroed buffer)
+    launch_sweep_dense_apply(a, op->sw_T, r, out, op->sw_u, asis ? 1 : 0, s, &c);
+    HIPC(hipGetLastError());
+    return;
+  }
   if (op->sw_T) {
     // The chain is 2 (n - b) + 1 dependent GEMV launches: replayed from a graph captured once
     // per (mode, stop flag) on fixed buffers, so the host does not pay a launch per GEMV.
@@ -1068,6 +1090,18 @@ static void sweep_dense_configure(hh_op* op) {
     HIPC(hipStreamSynchronize(s));
     op->sw_in = dalloc<double2>((size_t)n * n);
     op->sw_out = dalloc<double2>((size_t)n * n);
+    int cus = 0;
+    HIPC(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, op->ctx->device));
+    // HH_SWEEP_CHAIN=1: the persistent chain (sweep_dense.hip sweep_chain_kernel); off by
+    // default until it beats the graph-replayed launches
+    static const bool chain_on = [] {
+      const char* e = std::getenv("HH_SWEEP_CHAIN");
+      return e && e[0] == '1';
+    }();
+    if (chain_on && sweep_chain_fits(n, cus)) {
+      op->sw_chain = dalloc<unsigned long long>(sweep_chain_granules());
+      HIPC(hipMemset(op->sw_chain, 0, sweep_chain_granules() * sizeof(unsigned long long)));
+    }
   } catch (...) {
     dfree(scr);
     sweep_dense_release(op);
@@ -1659,13 +1693,13 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
                      (op->krylov_mode != 1) && small_cycle_eligible(op->n, restart) &&
                      (op->small_cycle == 1 || (size_t)op->n * op->n <= ((size_t)1 << 18));
   unsigned* small_timeout = reinterpret_cast<unsigned*>(op->red + kRedTimeout);
+  HIPC(hipMemsetAsync(small_timeout, 0, sizeof(double), s));  // (the device wait-bound word)
   if (small) {
     if (!op->small_scr) {
       const size_t nd = small_cycle_scratch_doubles(op->n);
       op->small_scr = dalloc<double>(nd);
       HIPC(hipMemsetAsync(op->small_scr, 0, nd * sizeof(double), s));  // (no stale tags)
     }
-    HIPC(hipMemsetAsync(small_timeout, 0, sizeof(double), s));
   }
 
   for (long iteration = 0; iteration < maxiter; ++iteration) {
@@ -1795,6 +1829,16 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     const double* sth = op->status_h + kRedStatus;
     int ctl[2];
     std::memcpy(ctl, op->status_h + kRedCtrl, 2 * sizeof(int));
+    if (!small) {  // (the persistent sweep chain's wait bound)
+      unsigned tmo = 0;
+      std::memcpy(&tmo, op->status_h + kRedTimeout, sizeof(unsigned));
+      if (tmo != 0) {
+        HIPC(hipMemset(op->red + kRedTimeout, 0, sizeof(double)));
+        fail(HH_ERR_STATE, "sweeping preconditioner: the persistent apply chain timed out "
+                           "(workgroups not co-resident?); HH_SWEEP_CHAIN=0 selects one launch "
+                           "per GEMV");
+      }
+    }
     if (small && ctl[0] != 1) {
       double w = 0.0;
       read_dev(op, op->red + kRedTimeout, &w, 1);

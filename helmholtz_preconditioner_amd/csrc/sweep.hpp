@@ -33,8 +33,31 @@ size_t sweep_dense_scratch_per_block(int n, int b);    // setup scratch (double2
 int sweep_dense_chunks(int n);                          // setup blocks per system
 void launch_sweep_dense_setup(const SweepArgs& a, int s_base, int batch, double2* yscr,
                               double2* T, hipStream_t st);
-// out = M r (r and out distinct, u: n^2 scratch); asis: middle sweep u -= T u (quirk Q2)
+// The persistent form of the apply chain (sweep_dense.hip sweep_chain_kernel): one cooperative
+// launch for the 2 (n - b) dependent GEMVs after F0, when n <= 1024 and its ceil(n / 4)
+// workgroups (one per CU: 80-160 KB of LDS each) fit the device.
+struct ChainArgs {
+  const double2* T;
+  int n, b;
+  const double2* R1;        // operator's R1 = 1/s1 per column
+  const double2* tab_glob;  // per-layer table [n][4] (BS at 1, BN at 2)
+  const double2* r;
+  double2* u;               // u_m (u_b written by F0 before the launch)
+  double2* w;               // the result
+  double a_in, t_sign;      // FWD / MID epilogue: w = t_sign t + a_in u_{m-1}
+  const int* stop;          // GMRES cycle stop flag or nullptr
+  unsigned long long* gbuf;  // [2][pad][4] tagged granules of each step's output (zeroed once)
+  unsigned* timeout;        // set when a wait gives up
+  unsigned seq;             // launch sequence number (granule tags)
+  int diag;                 // diagnostic (HH_SWEEP_DIAG): 1 no matrix loads, 2 no input waits
+};
+bool sweep_chain_fits(int n, int device_cus);
+size_t sweep_chain_granules();  // u64 elements of ChainArgs::gbuf
+// out = M r (r and out distinct, u: n^2 scratch); asis: middle sweep u -= T u (quirk Q2).
+// chain non-null: the FWD/MID/BWD chain runs as one persistent launch (its gbuf, timeout, seq
+// taken from *chain); otherwise as one launch per GEMV.
 void launch_sweep_dense_apply(const SweepArgs& a, const double2* T, const double2* r,
-                              double2* out, double2* u, int asis, hipStream_t st);
+                              double2* out, double2* u, int asis, hipStream_t st,
+                              const ChainArgs* chain = nullptr);
 
 }  // namespace hh

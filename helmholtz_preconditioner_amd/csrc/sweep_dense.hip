@@ -29,6 +29,7 @@
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
 #include "sweep.hpp"
+#include "hh_error.hpp"
 
 #include <algorithm>
 #include <type_traits>
@@ -210,6 +211,211 @@ void launch_gemv(const GemvStep& g, int batch, int n, const double2* R1, const i
     hipLaunchKernelGGL(dense_gemv_kernel<32>, grid, dim3(256), 0, st, g, n, R1, stop);
 }
 
+// ---------------------------------------------------------------- persistent apply chain
+// The FWD+MID and BWD sweeps as ONE cooperative launch (2 (n - b) dependent GEMVs) instead of
+// one launch per GEMV: a launch boundary costs about as much as streaming a whole matrix.
+// Workgroup w owns rows 4w .. 4w+3 of every GEMV (one compute wave per row, the same lane
+// partition, FMA order and shuffle reduction as dense_gemv_kernel: bit-identical results); four
+// loader waves stream the NEXT step's matrix rows into the other LDS slot while the compute
+// waves wait for the current input.  Step s's outputs are handed to every workgroup as tagged
+// 8-byte granules {tag, 32-bit half} (MI355X_MICROARCH.md: the data is the flag -- no counter,
+// no fence); the tag carries the launch's sequence number and the step.  Two workgroup barriers
+// per step: A(s) -- slot s loaded, input s staged; B(s) -- every compute wave done with input s
+// (so the next input may overwrite it).  Every wait is bounded: on timeout the timeout word is
+// set and the grid drains.
+constexpr int kChainRows = 4;       // rows (compute waves) per workgroup
+constexpr int kChainThreads = 2 * kChainRows * 64;  // + as many loader waves
+constexpr unsigned kChainSpin = 1u << 22;
+
+// by-value select (a select of two lvalues would become a select of addresses: flat accesses)
+__device__ __forceinline__ double2 csel2(bool c, double2 a, double2 b) {
+  return make_double2(c ? a.x : b.x, c ? a.y : b.y);
+}
+
+__device__ __forceinline__ unsigned chain_tag(unsigned seq, int step) {
+  return (seq << 12) | ((unsigned)step & 0xfffu);
+}
+
+template <int J>
+__global__ __launch_bounds__(kChainThreads) void sweep_chain_kernel(const ChainArgs a) {
+  if (a.stop && *a.stop) return;
+  constexpr int PAD = 64 * J;  // padded row length (n <= PAD)
+  constexpr int PER = PAD / (kChainRows * 64);  // input elements per compute thread
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double2* slots = reinterpret_cast<double2*>(smem);  // [2][kChainRows][PAD]
+  double2* xs = slots + 2 * kChainRows * PAD;         // [PAD]
+  using gu64 = __attribute__((address_space(1))) unsigned long long;
+  const int n = a.n, b = a.b, S = 2 * (n - b);
+  const int t = threadIdx.x;
+  const bool loader = t >= kChainRows * 64;
+  const int wv = t >> 6, lane = t & 63;
+  const int row0 = blockIdx.x * kChainRows;
+  const double2 z = make_double2(0.0, 0.0);
+  auto mat_of = [&](int s) { return s < n - b ? b + s : n - 2 - (s - (n - b)); };
+
+  // loader: this step's matrix rows -> registers (issued together), then -> LDS slot
+  double2 lv[PER * 4];
+  auto load_rows = [&](int s) {
+    if (a.diag == 1) return;
+    const double2* Tm = a.T + (size_t)mat_of(s) * n * n;
+    const int lt = t - kChainRows * 64;
+#pragma unroll
+    for (int q = 0; q < PER * 4; ++q) {
+      const int e = lt + kChainRows * 64 * q;
+      const int r = e / PAD, k = e % PAD;
+      const double2* p = Tm + (size_t)min(row0 + r, n - 1) * n + min(k, n - 1);
+      lv[q] = make_double2(__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y));
+    }
+  };
+  auto store_rows = [&](int s) {
+    if (a.diag == 1) return;
+    double2* sl = slots + (size_t)(s & 1) * kChainRows * PAD;
+    const int lt = t - kChainRows * 64;
+#pragma unroll
+    for (int q = 0; q < PER * 4; ++q) sl[lt + kChainRows * 64 * q] = lv[q];
+  };
+  // loader: slot 0 now; step 1's rows stay in flight (registers) until B(0) -- each step's rows
+  // are requested a whole step before they are stored (at B(s-1)) and read (after A(s))
+  if (loader) {
+    load_rows(0);
+    store_rows(0);
+    if (S > 1) load_rows(1);
+  }
+  // compute threads: R1 of this thread's input elements (the backward sweep's scaling)
+  double2 r1v[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) r1v[q] = a.R1[min(t + kChainRows * 64 * q, n - 1)];
+  // compute threads: step 0's input u_b was written by the F0 launch before this one
+  if (!loader) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = t + kChainRows * 64 * q;
+      xs[e] = csel2(e < n, a.u[(size_t)b * n + min(e, n - 1)], z);
+    }
+  }
+  bool ok = true;
+  for (int s = 0; s < S; ++s) {
+    if (__syncthreads_or(!ok)) break;  // A(s)
+    const bool bwd = s >= n - b;
+    const int m = bwd ? n - 1 - (s - (n - b)) : b + 1 + s;  // 1-based sweep index of the step
+    if (!loader) {
+      // the epilogue's operands (independent of the chain) requested before the dot
+      const int i = row0 + wv;
+      const int ic = min(i, n - 1);
+      // (valid addresses always, selected by value)
+      const int mc = min(m, n - 1);
+      const double2 r_i = csel2(!bwd && m < n, a.r[(size_t)mc * n + ic], z);
+      const double2 BSm = csel2(!bwd && m < n, a.tab_glob[4 * mc + 1], z);
+      const double2 R1i = a.R1[ic];
+      const double2 w_old = csel2(bwd, a.w[(size_t)(m - 1) * n + ic], z);
+      const double2* sl = slots + ((size_t)(s & 1) * kChainRows + wv) * PAD;
+      double2 acc = z;
+#pragma unroll
+      for (int j = 0; j < J; ++j) acc = cfma(sl[lane + 64 * j], xs[lane + 64 * j], acc);
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        acc.x += __shfl_xor(acc.x, off);
+        acc.y += __shfl_xor(acc.y, off);
+      }
+      if (lane == 0 && i < n) {
+        double2 o, next;
+        if (!bwd) {  // FWD (m < n) / MID (m == n): w_{m-1} = t | u_{m-1} - t
+          o = cscale(acc, a.t_sign);
+          if (a.a_in != 0.0) o = cadd(o, cscale(xs[i], a.a_in));
+          a.w[(size_t)(m - 1) * n + i] = o;
+          if (m < n) {  // u_m = r_m - S_m t
+            next = csub(r_i, cmul(cmul(BSm, R1i), acc));
+            a.u[(size_t)m * n + i] = next;
+          } else {
+            next = o;  // the backward sweep starts from w_{n-1}
+          }
+        } else {  // BWD: w_{m-1} -= T_m (N_{m-1} w_m)
+          o = cadd(cscale(acc, -1.0), cscale(w_old, 1.0));
+          a.w[(size_t)(m - 1) * n + i] = o;
+          next = o;
+        }
+        if (s + 1 < S) {
+          const unsigned tg = chain_tag(a.seq, s + 1);
+          unsigned long long* gp = a.gbuf + ((size_t)((s + 1) & 1) * PAD + i) * 4;
+          const unsigned long long hx = (unsigned long long)__double_as_longlong(next.x);
+          const unsigned long long hy = (unsigned long long)__double_as_longlong(next.y);
+          const unsigned long long tt = (unsigned long long)tg << 32;
+          __hip_atomic_store((gu64*)gp, tt | (hx >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store((gu64*)(gp + 1), tt | (hx & 0xffffffffull), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store((gu64*)(gp + 2), tt | (hy >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store((gu64*)(gp + 3), tt | (hy & 0xffffffffull), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    __syncthreads();  // B(s): input s no longer read
+    if (s + 1 >= S) break;
+    if (loader) {
+      store_rows(s + 1);
+      if (s + 2 < S) load_rows(s + 2);
+      __syncthreads();  // S1(s) (the compute waves' sentinel barrier)
+    } else {
+      // input of step s+1 (BWD: scaled N R1).  First one granule per producing workgroup is
+      // polled (a few KB per poll instead of every row's granules), then every row's granules
+      // are read once and checked -- stragglers polled again.
+      const bool nb = s + 1 >= n - b;
+      const int mn = nb ? n - 1 - (s + 1 - (n - b)) : 1;
+      const double2 inc = a.tab_glob[4 * (mn - 1) + 2];
+      const unsigned tg = chain_tag(a.seq, s + 1);
+      const unsigned long long* gb = a.gbuf + (size_t)((s + 1) & 1) * PAD * 4;
+      const int nwg = gridDim.x;
+      unsigned spins = 0;
+      if (t < nwg && a.diag != 2) {
+        const unsigned long long* gp = gb + (size_t)min(t * kChainRows, n - 1) * 4 + 3;
+        while ((unsigned)(__hip_atomic_load((gu64*)gp, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT) >> 32) != tg) {
+          if (++spins > kChainSpin) {
+            ok = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();  // S1(s)
+      unsigned long long v[PER][4];
+      for (;;) {
+        bool all = true;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+          const int e = min(t + kChainRows * 64 * q, n - 1);
+          const unsigned long long* gp = gb + (size_t)e * 4;
+#pragma unroll
+          for (int h = 0; h < 4; ++h)
+            v[q][h] = __hip_atomic_load((gu64*)(gp + h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int q = 0; q < PER; ++q)
+#pragma unroll
+          for (int h = 0; h < 4; ++h) all = all && (unsigned)(v[q][h] >> 32) == tg;
+        if (all || !ok || a.diag == 2) break;
+        if (++spins > kChainSpin) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int e = t + kChainRows * 64 * q;
+        double2 x = make_double2(
+            __longlong_as_double((long long)((v[q][0] << 32) | (v[q][1] & 0xffffffffull))),
+            __longlong_as_double((long long)((v[q][2] << 32) | (v[q][3] & 0xffffffffull))));
+        if (nb) x = cmul(x, cmul(inc, r1v[q]));
+        xs[e] = csel2(e < n, x, z);
+      }
+    }
+  }
+  if (!ok && t == 0)
+    __hip_atomic_store((__attribute__((address_space(1))) unsigned*)a.timeout, 1u,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int B>
 void launch_setup_t(const SweepArgs& a, int s_base, int batch, double2* yscr, size_t yscr_block,
                     double2* T, hipStream_t st) {
@@ -239,8 +445,38 @@ void launch_sweep_dense_setup(const SweepArgs& a, int s_base, int batch, double2
   }
 }
 
+bool sweep_chain_fits(int n, int device_cus) {
+  return n >= 2 && n <= 1024 && (n + kChainRows - 1) / kChainRows <= device_cus;
+}
+size_t sweep_chain_granules() { return 2 * 1024 * 4; }
+
+template <int J>
+void launch_chain_t(const ChainArgs& c, hipStream_t st) {
+  constexpr int PAD = 64 * J;
+  const size_t lds = (2 * kChainRows + 1) * (size_t)PAD * sizeof(double2);
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&sweep_chain_kernel<J>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) {
+    (void)hipGetLastError();
+    fail(HH_ERR_HIP, "sweep chain: cannot enable %zu B of dynamic LDS (%s)", lds,
+         hipGetErrorString(attr));
+  }
+  ChainArgs arg = c;
+  void* params[] = {&arg};
+  const dim3 grid((c.n + kChainRows - 1) / kChainRows), block(kChainThreads);
+  // cooperative: the launch fails instead of hanging if the grid cannot be co-resident
+  const hipError_t e = hipLaunchCooperativeKernel(
+      reinterpret_cast<const void*>(&sweep_chain_kernel<J>), grid, block, params, (unsigned)lds, st);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    fail(HH_ERR_HIP, "sweep chain: cooperative launch of %u workgroups failed (%s)", grid.x,
+         hipGetErrorString(e));
+  }
+}
+
 void launch_sweep_dense_apply(const SweepArgs& a, const double2* T, const double2* r, double2* w,
-                              double2* u, int asis, hipStream_t st) {
+                              double2* u, int asis, hipStream_t st, const ChainArgs* chain) {
   const int n = a.n, b = a.b;
   const size_t N = n;
   const double2* R1 = a.tab_i + 2 * n;
@@ -254,6 +490,23 @@ void launch_sweep_dense_apply(const SweepArgs& a, const double2* T, const double
     g.a_old = 0.0; g.a_in = 0.0; g.a_t = 1.0;
     g.unext = u + (size_t)b * N; g.rnext = r + (size_t)b * N; g.S_c = BS(b); g.next_y = b - 1;
     launch_gemv(g, b, n, R1, a.stop, st);
+  }
+  if (chain) {  // FWD + MID + BWD as one persistent launch
+    ChainArgs c = *chain;
+    c.T = T;
+    c.n = n;
+    c.b = b;
+    c.R1 = R1;
+    c.tab_glob = a.tab_glob;
+    c.r = r;
+    c.u = u;
+    c.w = w;
+    c.a_in = in_w;
+    c.t_sign = t_sign;
+    c.stop = a.stop;
+    if (n <= 512) launch_chain_t<8>(c, st);
+    else launch_chain_t<16>(c, st);
+    return;
   }
   // FWD (m = b+1 .. n-1, 1-based) fused with the middle sweep; MID for m = n
   for (int m = b + 1; m <= n; ++m) {

@@ -1,0 +1,25 @@
+#!/bin/bash
+# sweeping preconditioner: parity tests, then apply timings (persistent chain vs one launch
+# per GEMV) and a kernel-trace profile of the n=1023 apply
+set -u
+TAG=${1:-r02sw}
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+fatal() { case $1 in 124|137|134|139) return 0;; *) return 1;; esac; }
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -8 "$OUT/$name.log" | cut -c1-600
+  if fatal $rc; then echo "FATAL rc=$rc in $name: stopping"; exit $rc; fi
+  return 0
+}
+PYT="python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu"
+HH_SWEEP_CHAIN=1 step t_sweep 400 $PYT tests/test_gpu_sweep.py -x
+HH_SWEEP_CHAIN=1 step bench_chain 300 python tools/bench_sweep.py --form dense 127 255 511 1023
+HH_SWEEP_CHAIN=0 step bench_launches 200 python tools/bench_sweep.py --form dense 1023
+step rocprof_launches 200 env HH_SWEEP_CHAIN=0 rocprofv3 --kernel-trace --stats -d "$OUT/prof_launches" -o run --output-format csv -- python3 tools/bench_sweep.py --form dense 1023
+echo done
