@@ -179,7 +179,8 @@ struct hh_op {
     hipGraphExec_t exec;
   };
   std::vector<SweepGraph> sw_graphs;  // the 2 (n - b) + 1 GEMV launches, captured once
-  int sw_mode = -1;             // -1 auto, 0 block-Thomas solves, 1 dense transfer matrices
+  int sw_mode = -1;  // -1 auto, 0 block-Thomas solves, 1 dense transfer matrices, 2 dense with
+                     // one launch per GEMV (no persistent chain)
   // tuning (hh_op_tune): stencil variant for the plain apply, rows per block override
   int variant = -1;
   int rpb_override = 0;
@@ -1053,6 +1054,25 @@ HH_API int hh_op_local_rows(hh_op* op, int* j_begin, int* j_end) {
   GUARD_END
 }
 
+// The persistent apply chain of the dense form (sweep_dense.hip sweep_chain_kernel) where it
+// fits, unless mode 2 (one launch per GEMV, replayed from a graph) or HH_SWEEP_CHAIN=0.
+static void sweep_chain_configure(hh_op* op) {
+  static const bool chain_env = [] {
+    const char* e = std::getenv("HH_SWEEP_CHAIN");
+    return !(e && e[0] == '0');
+  }();
+  int cus = 0;
+  HIPC(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, op->ctx->device));
+  const bool want = op->sw_T && op->sw_mode != 2 && chain_env && sweep_chain_fits(op->n, cus);
+  if (!want) {
+    dfree(op->sw_chain);
+    op->sw_chain = nullptr;
+  } else if (!op->sw_chain) {
+    op->sw_chain = dalloc<unsigned long long>(sweep_chain_granules());
+    HIPC(hipMemset(op->sw_chain, 0, sweep_chain_granules() * sizeof(unsigned long long)));
+  }
+}
+
 // Dense-transfer form of the sweeping preconditioner (sweep_dense.hip): decide, allocate, form.
 static void sweep_dense_configure(hh_op* op) {
   const int n = op->n, b = op->b;
@@ -1060,7 +1080,10 @@ static void sweep_dense_configure(hh_op* op) {
     sweep_dense_release(op);
     return;
   }
-  if (op->sw_T) return;
+  if (op->sw_T) {
+    sweep_chain_configure(op);
+    return;
+  }
   size_t free_b = 0, total_b = 0;
   HIPC(hipMemGetInfo(&free_b, &total_b));
   const size_t tbytes = sweep_dense_bytes(n);
@@ -1090,24 +1113,13 @@ static void sweep_dense_configure(hh_op* op) {
     HIPC(hipStreamSynchronize(s));
     op->sw_in = dalloc<double2>((size_t)n * n);
     op->sw_out = dalloc<double2>((size_t)n * n);
-    int cus = 0;
-    HIPC(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, op->ctx->device));
-    // HH_SWEEP_CHAIN=1: the persistent chain (sweep_dense.hip sweep_chain_kernel); off by
-    // default until it beats the graph-replayed launches
-    static const bool chain_on = [] {
-      const char* e = std::getenv("HH_SWEEP_CHAIN");
-      return e && e[0] == '1';
-    }();
-    if (chain_on && sweep_chain_fits(n, cus)) {
-      op->sw_chain = dalloc<unsigned long long>(sweep_chain_granules());
-      HIPC(hipMemset(op->sw_chain, 0, sweep_chain_granules() * sizeof(unsigned long long)));
-    }
   } catch (...) {
     dfree(scr);
     sweep_dense_release(op);
     throw;
   }
   dfree(scr);
+  sweep_chain_configure(op);
 }
 
 HH_API int hh_op_set_precond(hh_op* op, int kind, double beta, int sweeps, double damping) {
@@ -1531,7 +1543,7 @@ HH_API int hh_op_tune(hh_op* op, int variant, int rows_per_block, int grid_block
 HH_API int hh_op_sweep_mode(hh_op* op, int mode, int* active) {
   GUARD_BEGIN
   REQUIRE(op, "null op");
-  REQUIRE(mode >= -1 && mode <= 1, "mode must be -1, 0 or 1");
+  REQUIRE(mode >= -1 && mode <= 2, "mode must be -1, 0, 1 or 2");
   HIPC(hipSetDevice(op->ctx->device));
   op->sw_mode = mode;
   if (op->sw_P) sweep_dense_configure(op);  // already factored: switch now

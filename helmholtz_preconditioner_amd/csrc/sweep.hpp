@@ -49,7 +49,8 @@ struct ChainArgs {
   unsigned long long* gbuf;  // [2][pad][4] tagged granules of each step's output (zeroed once)
   unsigned* timeout;        // set when a wait gives up
   unsigned seq;             // launch sequence number (granule tags)
-  int diag;                 // diagnostic (HH_SWEEP_DIAG): 1 no matrix loads, 2 no input waits
+  int diag;                 // diagnostic (HH_SWEEP_DIAG): 1 no matrix loads, 2 no input waits,
+                            // 3 neither loads nor input reads, 4 no input reads
 };
 bool sweep_chain_fits(int n, int device_cus);
 size_t sweep_chain_granules();  // u64 elements of ChainArgs::gbuf

@@ -45,6 +45,27 @@ __device__ __forceinline__ void ufor(F&& f) {
   }
 }
 
+// Sum over the 64 lanes of a wave by DPP lane moves (no LDS round trips, unlike a shuffle
+// butterfly: 12 dependent ds_bpermute per double), fixed order; the total lands in lane 63.
+// Pairs, quads, 8 (half-row mirror), 16 (row mirror), then row 0 -> 1 and row 2 -> 3
+// (row_bcast:15), rows 0-1 -> 2-3 (row_bcast:31).  Lanes a move does not write read 0.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_mov(double x) {
+  const long long u = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(u & 0xffffffff), CTRL, ROWS, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, ROWS, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double wave_sum_to_63(double v) {
+  v += dpp_mov<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141, 0xf>(v);  // row_half_mirror
+  v += dpp_mov<0x140, 0xf>(v);  // row_mirror
+  v += dpp_mov<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+  v += dpp_mov<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
+  return v;
+}
+
 constexpr int kSetupThreads = 256;  // RHS columns per setup block
 
 // ------------------------------------------------------------------------------- setup
@@ -185,12 +206,9 @@ __global__ __launch_bounds__(256) void dense_gemv_kernel(const GemvStep g, const
     constexpr int j = decltype(jc)::value;
     acc = cfma(tv[j], xs[lane + 64 * j], acc);
   });
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    acc.x += __shfl_xor(acc.x, off);
-    acc.y += __shfl_xor(acc.y, off);
-  }
-  if (lane == 0) {
+  acc.x = wave_sum_to_63(acc.x);
+  acc.y = wave_sum_to_63(acc.y);
+  if (lane == 63) {
     double2* out = g.out + (size_t)y * n;
     double2 o = cscale(acc, g.a_t);
     if (g.a_in != 0.0) o = cadd(o, cscale(g.in[(size_t)y * n + i], g.a_in));
@@ -215,7 +233,7 @@ void launch_gemv(const GemvStep& g, int batch, int n, const double2* R1, const i
 // The FWD+MID and BWD sweeps as ONE cooperative launch (2 (n - b) dependent GEMVs) instead of
 // one launch per GEMV: a launch boundary costs about as much as streaming a whole matrix.
 // Workgroup w owns rows 4w .. 4w+3 of every GEMV (one compute wave per row, the same lane
-// partition, FMA order and shuffle reduction as dense_gemv_kernel: bit-identical results); four
+// partition, FMA order and DPP reduction as dense_gemv_kernel: bit-identical results); four
 // loader waves stream the NEXT step's matrix rows into the other LDS slot while the compute
 // waves wait for the current input.  Step s's outputs are handed to every workgroup as tagged
 // 8-byte granules {tag, 32-bit half} (MI355X_MICROARCH.md: the data is the flag -- no counter,
@@ -224,7 +242,8 @@ void launch_gemv(const GemvStep& g, int batch, int n, const double2* R1, const i
 // (so the next input may overwrite it).  Every wait is bounded: on timeout the timeout word is
 // set and the grid drains.
 constexpr int kChainRows = 4;       // rows (compute waves) per workgroup
-constexpr int kChainThreads = 2 * kChainRows * 64;  // + as many loader waves
+// + two groups of loader waves (group g loads the steps of parity g, two steps ahead)
+constexpr int kChainThreads = 3 * kChainRows * 64;
 constexpr unsigned kChainSpin = 1u << 22;
 
 // by-value select (a select of two lvalues would become a select of addresses: flat accesses)
@@ -248,6 +267,8 @@ __global__ __launch_bounds__(kChainThreads) void sweep_chain_kernel(const ChainA
   const int n = a.n, b = a.b, S = 2 * (n - b);
   const int t = threadIdx.x;
   const bool loader = t >= kChainRows * 64;
+  const int lgrp = loader ? (t - kChainRows * 64) / (kChainRows * 64) : 0;  // loader group
+  const int lt = (t - kChainRows * 64) % (kChainRows * 64);                // index in group
   const int wv = t >> 6, lane = t & 63;
   const int row0 = blockIdx.x * kChainRows;
   const double2 z = make_double2(0.0, 0.0);
@@ -256,9 +277,8 @@ __global__ __launch_bounds__(kChainThreads) void sweep_chain_kernel(const ChainA
   // loader: this step's matrix rows -> registers (issued together), then -> LDS slot
   double2 lv[PER * 4];
   auto load_rows = [&](int s) {
-    if (a.diag == 1) return;
+    if (a.diag == 1 || a.diag == 3) return;
     const double2* Tm = a.T + (size_t)mat_of(s) * n * n;
-    const int lt = t - kChainRows * 64;
 #pragma unroll
     for (int q = 0; q < PER * 4; ++q) {
       const int e = lt + kChainRows * 64 * q;
@@ -268,18 +288,22 @@ __global__ __launch_bounds__(kChainThreads) void sweep_chain_kernel(const ChainA
     }
   };
   auto store_rows = [&](int s) {
-    if (a.diag == 1) return;
+    if (a.diag == 1 || a.diag == 3) return;
     double2* sl = slots + (size_t)(s & 1) * kChainRows * PAD;
-    const int lt = t - kChainRows * 64;
 #pragma unroll
     for (int q = 0; q < PER * 4; ++q) sl[lt + kChainRows * 64 * q] = lv[q];
   };
-  // loader: slot 0 now; step 1's rows stay in flight (registers) until B(0) -- each step's rows
-  // are requested a whole step before they are stored (at B(s-1)) and read (after A(s))
+  // loader group g owns the steps of parity g: step s's rows are requested two steps ahead (at
+  // B(s-3)), stored into slot s & 1 at B(s-1) and read after A(s) -- two steps of load latency
+  // hidden, 2 x 64 KB per CU in flight
   if (loader) {
-    load_rows(0);
-    store_rows(0);
-    if (S > 1) load_rows(1);
+    if (lgrp == 0) {
+      load_rows(0);
+      store_rows(0);
+      if (S > 2) load_rows(2);
+    } else if (S > 1) {
+      load_rows(1);
+    }
   }
   // compute threads: R1 of this thread's input elements (the backward sweep's scaling)
   double2 r1v[PER];
@@ -293,31 +317,59 @@ __global__ __launch_bounds__(kChainThreads) void sweep_chain_kernel(const ChainA
       xs[e] = csel2(e < n, a.u[(size_t)b * n + min(e, n - 1)], z);
     }
   }
+  // The two roles run their own loops (disjoint register live ranges) through the same
+  // barrier sequence per step: A(s), B(s), S1(s) (not after the last step).  The barriers
+  // are bare s_barrier after the wave's LDS operations (no memory fence: a workgroup fence would
+  // make every wave wait for its outstanding global loads -- the loader's two-steps-ahead
+  // matrix rows -- at every barrier); the abort decision travels through an LDS word.
+  auto bar = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  __shared__ int abort_word;  // (accessed directly: a pointer to it would be a flat pointer)
+  if (t == 0) abort_word = 0;
+  __syncthreads();
   bool ok = true;
-  for (int s = 0; s < S; ++s) {
-    if (__syncthreads_or(!ok)) break;  // A(s)
-    const bool bwd = s >= n - b;
-    const int m = bwd ? n - 1 - (s - (n - b)) : b + 1 + s;  // 1-based sweep index of the step
-    if (!loader) {
-      // the epilogue's operands (independent of the chain) requested before the dot
-      const int i = row0 + wv;
-      const int ic = min(i, n - 1);
-      // (valid addresses always, selected by value)
-      const int mc = min(m, n - 1);
-      const double2 r_i = csel2(!bwd && m < n, a.r[(size_t)mc * n + ic], z);
-      const double2 BSm = csel2(!bwd && m < n, a.tab_glob[4 * mc + 1], z);
-      const double2 R1i = a.R1[ic];
-      const double2 w_old = csel2(bwd, a.w[(size_t)(m - 1) * n + ic], z);
+  if (loader) {
+    for (int s = 0; s < S; ++s) {
+      bar();  // A(s)
+      if (__builtin_nontemporal_load(&abort_word)) break;
+      bar();  // B(s)
+      if (s + 1 >= S) break;
+      if (((s + 1) & 1) == lgrp) {
+        store_rows(s + 1);
+        if (s + 3 < S) load_rows(s + 3);
+      }
+      bar();  // S1(s)
+    }
+  } else {
+    const int i = row0 + wv;
+    const int ic = min(i, n - 1);
+    const double2 R1i = a.R1[ic];
+    // the epilogue's operands of a step (independent of the chain): requested one step ahead
+    // (valid addresses always, selected by value)
+    auto epi_ops = [&](int s, double2& r_i, double2& BSm, double2& w_old) {
+      const bool bw = s >= n - b;
+      const int mm = bw ? n - 1 - (s - (n - b)) : b + 1 + s;
+      const int mc = min(mm, n - 1);
+      r_i = csel2(!bw && mm < n, a.r[(size_t)mc * n + ic], z);
+      BSm = csel2(!bw && mm < n, a.tab_glob[4 * mc + 1], z);
+      w_old = csel2(bw, a.w[(size_t)(mm - 1) * n + ic], z);
+    };
+    double2 r_i, BSm, w_old;
+    epi_ops(0, r_i, BSm, w_old);
+    for (int s = 0; s < S; ++s) {
+      if (!ok) abort_word = 1;
+      bar();  // A(s)
+      if (__builtin_nontemporal_load(&abort_word)) break;
+      const bool bwd = s >= n - b;
+      const int m = bwd ? n - 1 - (s - (n - b)) : b + 1 + s;  // 1-based sweep index of the step
       const double2* sl = slots + ((size_t)(s & 1) * kChainRows + wv) * PAD;
       double2 acc = z;
-#pragma unroll
+#pragma unroll 4
       for (int j = 0; j < J; ++j) acc = cfma(sl[lane + 64 * j], xs[lane + 64 * j], acc);
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        acc.x += __shfl_xor(acc.x, off);
-        acc.y += __shfl_xor(acc.y, off);
-      }
-      if (lane == 0 && i < n) {
+      acc.x = wave_sum_to_63(acc.x);
+      acc.y = wave_sum_to_63(acc.y);
+      if (lane == 63 && i < n) {
         double2 o, next;
         if (!bwd) {  // FWD (m < n) / MID (m == n): w_{m-1} = t | u_{m-1} - t
           o = cscale(acc, a.t_sign);
@@ -348,38 +400,31 @@ __global__ __launch_bounds__(kChainThreads) void sweep_chain_kernel(const ChainA
                              __HIP_MEMORY_SCOPE_AGENT);
         }
       }
-    }
-    __syncthreads();  // B(s): input s no longer read
-    if (s + 1 >= S) break;
-    if (loader) {
-      store_rows(s + 1);
-      if (s + 2 < S) load_rows(s + 2);
-      __syncthreads();  // S1(s) (the compute waves' sentinel barrier)
-    } else {
-      // input of step s+1 (BWD: scaled N R1).  First one granule per producing workgroup is
-      // polled (a few KB per poll instead of every row's granules), then every row's granules
-      // are read once and checked -- stragglers polled again.
+      bar();  // B(s): input s no longer read
+      if (s + 1 >= S) break;
+      // (w_old of a BWD step: written by this very lane in an earlier FWD step)
+      epi_ops(s + 1, r_i, BSm, w_old);
+      // input of step s+1 (BWD: scaled N R1): every row's granules, in flight together, polled
+      // until all carry the step's tag
       const bool nb = s + 1 >= n - b;
       const int mn = nb ? n - 1 - (s + 1 - (n - b)) : 1;
       const double2 inc = a.tab_glob[4 * (mn - 1) + 2];
       const unsigned tg = chain_tag(a.seq, s + 1);
       const unsigned long long* gb = a.gbuf + (size_t)((s + 1) & 1) * PAD * 4;
-      const int nwg = gridDim.x;
       unsigned spins = 0;
-      if (t < nwg && a.diag != 2) {
-        const unsigned long long* gp = gb + (size_t)min(t * kChainRows, n - 1) * 4 + 3;
-        while ((unsigned)(__hip_atomic_load((gu64*)gp, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT) >> 32) != tg) {
-          if (++spins > kChainSpin) {
-            ok = false;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      __syncthreads();  // S1(s)
+      // S1(s): the input polls start after the loader has issued its next rows (measured: 10.0
+      // vs 14.8 ms per n = 1023 apply without this barrier -- polls issued first, then stuck
+      // behind the rows in the CU's memory queue, repeat)
+      bar();
       unsigned long long v[PER][4];
       for (;;) {
+        if (a.diag >= 3) {  // (diagnostic: no input read at all)
+#pragma unroll
+          for (int q = 0; q < PER; ++q)
+#pragma unroll
+            for (int h = 0; h < 4; ++h) v[q][h] = 0;
+          break;
+        }
         bool all = true;
 #pragma unroll
         for (int q = 0; q < PER; ++q) {

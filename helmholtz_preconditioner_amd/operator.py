@@ -370,13 +370,14 @@ class Sweeping(DevicePreconditioner):
     sweep is sequential in the layer index).
     """
 
-    FORMS = {"auto": -1, "thomas": 0, "dense": 1}
+    FORMS = {"auto": -1, "thomas": 0, "dense": 1, "dense-launches": 2}
 
     def __init__(self, A: DeviceOperator, reference: bool = False, form: str = "auto"):
         """``form``: ``"dense"`` forms the n matrices T_m (n^3 x 16 B of HBM) at setup and
         applies M as a chain of GEMVs; ``"thomas"`` keeps O(n^2 b^2) block-Thomas factors
-        and solves; ``"auto"`` picks dense when n <= 2048 and it fits.  Same results to
-        rounding."""
+        and solves; ``"auto"`` picks dense when n <= 2048 and it fits; ``"dense-launches"``
+        is the dense form with one launch per GEMV instead of the persistent chain (n <= 1024).
+        Same results to rounding (the two dense forms bit for bit)."""
         self.kind = _ffi.HH_PREC_SWEEP_REF if reference else _ffi.HH_PREC_SWEEP
         if form not in self.FORMS:
             raise ValueError(f"form must be one of {sorted(self.FORMS)}")

@@ -269,7 +269,10 @@ int hh_op_sl_fusion(hh_op* op, int enable);
 /* Sweeping preconditioner form (speed / memory only; results agree to rounding):
  *   mode -1 (default) dense transfer matrices when n <= 2048 and the n^3 x 16 B fit in HBM,
  *           else block-Thomas solves;  0 block-Thomas solves (O(n^2 b^2) memory, every solve
- *           2n dependent steps);  1 dense transfer matrices (error if they do not fit).
+ *           2n dependent steps);  1 dense transfer matrices (error if they do not fit), their
+ *           GEMV chain as ONE persistent cooperative launch when n <= 1024 (else one launch per
+ *           GEMV);  2 dense, one launch per GEMV always (HH_SWEEP_CHAIN=0 does the same for
+ *           modes -1 and 1).  The dense forms give the same results bit for bit.
  * Applies at the next sweeping setup, or at once if the operator is already factored.
  * active (optional) receives 1 when the dense form is in use. */
 int hh_op_sweep_mode(hh_op* op, int mode, int* active);

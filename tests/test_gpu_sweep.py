@@ -156,3 +156,27 @@ def test_gmres_dense_sweeping_vs_oracle(ctx):
     assert info == infor == 0 and len(hist) == len(histr)
     assert np.max(np.abs(hist - histr) / histr) < 1e-6
     assert relerr(x, xr) < 1e-6
+
+
+@pytest.mark.parametrize("n,b,kind", [(13, 12, "c2"), (96, 12, "c1"), (300, 12, "c1"),
+                                      (1023, 12, "c1")])
+def test_sweep_persistent_chain_bit_identical_to_launches(ctx, n, b, kind):
+    """the dense apply as ONE persistent launch (form "dense", n <= 1024) against one launch per
+    GEMV (form "dense-launches"): same lane partition, FMA order and DPP reduction -- the same
+    bits, both modes, also inside a GMRES cycle (its stop flag ends the chain early)"""
+    om, h, eta = O.problem_params(n, b, 5.0, 2.0)
+    A = H.build_A_matrix(b, 81.0, eta, om, h, n, medium(kind, n), context=ctx)
+    x = rand_complex(n * n, n + 7)
+    for reference in (False, True):
+        yc = H.Sweeping(A, reference=reference, form="dense") @ x
+        yl = H.Sweeping(A, reference=reference, form="dense-launches") @ x
+        assert np.array_equal(yc, yl)
+    if n <= 300:
+        f = O.init_f1_mat(.5, .125, om, n).ravel()
+        out = []
+        for form in ("dense", "dense-launches"):
+            out.append(H.gmres(A, f, rtol=1e-3, restart=20, maxiter=60,
+                               M=H.Sweeping(A, form=form), callback=lambda r: None,
+                               callback_type="legacy", return_history=True))
+        (x1, i1, h1), (x2, i2, h2) = out
+        assert i1 == i2 and np.array_equal(h1, h2) and np.array_equal(x1, x2)

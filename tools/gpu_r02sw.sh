@@ -1,6 +1,6 @@
 #!/bin/bash
 # sweeping preconditioner: parity tests, then apply timings (persistent chain vs one launch
-# per GEMV) and a kernel-trace profile of the n=1023 apply
+# per GEMV)
 set -u
 TAG=${1:-r02sw}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -17,9 +17,8 @@ step() {  # step NAME SECONDS CMD...
   if fatal $rc; then echo "FATAL rc=$rc in $name: stopping"; exit $rc; fi
   return 0
 }
-PYT="python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu"
-HH_SWEEP_CHAIN=1 step t_sweep 400 $PYT tests/test_gpu_sweep.py -x
-HH_SWEEP_CHAIN=1 step bench_chain 300 python tools/bench_sweep.py --form dense 127 255 511 1023
-HH_SWEEP_CHAIN=0 step bench_launches 200 python tools/bench_sweep.py --form dense 1023
-step rocprof_launches 200 env HH_SWEEP_CHAIN=0 rocprofv3 --kernel-trace --stats -d "$OUT/prof_launches" -o run --output-format csv -- python3 tools/bench_sweep.py --form dense 1023
+PYT="python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu"
+step t_sweep 500 $PYT tests/test_gpu_sweep.py -x
+step bench_chain 300 python tools/bench_sweep.py --form dense 127 255 511 1023
+HH_SWEEP_CHAIN=0 step bench_launches 300 python tools/bench_sweep.py --form dense 127 255 511 1023
 echo done
