@@ -36,15 +36,6 @@ namespace {
 using gu32 = __attribute__((address_space(1))) unsigned;
 using gu64 = __attribute__((address_space(1))) unsigned long long;
 
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-  __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_sc1(const double* p) {
-  return __longlong_as_double(
-      (long long)__hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
 __device__ __forceinline__ double2 csel(bool c, double2 a, double2 b) {
   return make_double2(c ? a.x : b.x, c ? a.y : b.y);
 }
@@ -99,9 +90,11 @@ constexpr int kRunMax = (kSmallThreads + kRuns - 1) / kRuns;  // rows per run, a
 constexpr int kRedRuns = 2 * (kSmallThreads + kWave);
 struct ArArgs {
   unsigned long long* part;  // [2][G][2 kPStride]
-  unsigned long long* sums;  // [2][2 kPStride]
+  unsigned long long* sums;  // [kSmallRounds][2 kPStride]: one slot per round (the Givens
+                             // workgroup reads them at its own pace)
   unsigned* timeout;
   unsigned seq;
+  int G;                     // participating (row) workgroups
 };
 __device__ __forceinline__ unsigned gran_tag(unsigned seq, unsigned epoch) {
   return (seq << 8) | (epoch & 0xffu);
@@ -131,7 +124,7 @@ __device__ __forceinline__ bool ld_gran(const unsigned long long* p, unsigned ta
 }
 __device__ bool allreduce_rows(const ArArgs& ar, int par, unsigned epoch, int cols, l1* out,
                                l1* red) {
-  const int G = gridDim.x, g = blockIdx.x;
+  const int G = ar.G, g = blockIdx.x;
   const int t = threadIdx.x;
   const unsigned tag = gran_tag(ar.seq, epoch);
   const int run = (G + kRuns - 1) / kRuns;  // rows per summing thread (<= 16)
@@ -180,12 +173,12 @@ __device__ bool allreduce_rows(const ArArgs& ar, int par, unsigned epoch, int co
     if (t == 0) {
       double s = 0.0;
       for (int q = 0; q < kRuns; ++q) s += red[kRedRuns + q];
-      st_gran(ar.sums + (size_t)par * 2 * kPStride + 2 * c, tag, s);
+      st_gran(ar.sums + (size_t)epoch * 2 * kPStride + 2 * c, tag, s);
     }
   }
   if (t < cols) {
     double v = 0.0;
-    ok = ld_gran(ar.sums + (size_t)par * 2 * kPStride + 2 * t, tag, &v) && ok;
+    ok = ld_gran(ar.sums + (size_t)epoch * 2 * kPStride + 2 * t, tag, &v) && ok;
     out[t] = v;
   }
   if (__syncthreads_or(!ok)) {
@@ -273,7 +266,7 @@ __device__ bool finish_column(const Shared& sh, const SmallCycleArgs& a, int col
   sh.S[col] = cscale(Sc, c);
   sh.S[col + 1] = tmp;
   const double presid = hypot(tmp.x, tmp.y);
-  if (blockIdx.x == 0) {
+  {
     double* st = a.g.status_it + 4 * col;
     st[0] = presid;
     st[1] = brk;
@@ -285,17 +278,92 @@ __device__ bool finish_column(const Shared& sh, const SmallCycleArgs& a, int col
 }
 
 
+// Extra workgroup n ("Givens workgroup", one thread): follows the rounds' sums at its own
+// pace and keeps the Hessenberg books -- column j from the round-j sums, column j-1 completed
+// with |u_j| (krylov.hip gmres_lag_kernel / gmres_finish_column), rotations, presid, scipy's
+// exit tests -- so none of it sits on the row workgroups' critical path.  Per column it
+// publishes a verdict granule (0 continue / 1 stop), at the end the column the cycle solved for
+// and y_k / sigma_k.  Returns false on timeout.
+__device__ bool givens_role(const Shared& sh, const SmallCycleArgs& a) {
+  const int R1 = a.restart + 1;
+  const unsigned long long* sums = a.sums;
+  auto sum_at = [&](unsigned epoch, int c, double* v) {
+    return ld_gran(sums + (size_t)epoch * 2 * kPStride + 2 * c, gran_tag(a.seq, epoch), v);
+  };
+  const double mn = sqrt(*a.mnorm2);
+  sh.vs[0] = 1.0 / mn;
+  sh.ss[0] = 1.0 / mn;
+  for (int k = 0; k < R1; ++k) sh.S[k] = make_double2(k == 0 ? mn : 0.0, 0.0);
+  int col = -1;
+  for (int j = 0; j <= a.stop_col && col < 0; ++j) {
+    const int K = j + 1;
+    const unsigned epoch = j + 1;
+    double w2, u2 = 0.0;
+    if (!sum_at(epoch, 2 * K, &w2)) return false;
+    if (j >= 1 && !sum_at(epoch, 2 * K + 1, &u2)) return false;
+    const double vj = j >= 1 ? 1.0 / sqrt(u2) : sh.vs[0];
+    // column j of H and the Pythagorean terms (the row workgroups' expressions and order)
+    double rest = w2;
+    for (int k = 0; k <= j; ++k) {
+      double dx, dy;
+      if (!sum_at(epoch, 2 * k, &dx) || !sum_at(epoch, 2 * k + 1, &dy)) return false;
+      const double2 d = make_double2(dx, dy);
+      const double vk = k == j ? vj : sh.vs[k];
+      sh.H[(size_t)j * R1 + k] = cscale(cscale(d, vk), vj / sh.ss[j]);
+      rest -= cabs2(d) * vk * vk;
+    }
+    if (j >= 1) {
+      const int c = j - 1;
+      const bool stop = finish_column(sh, a, c, (1.0 / vj) * sh.vs[c] / sh.ss[c], vj);
+      st_gran(a.verdict + 2 * c, gran_tag(a.seq, c + 1), stop ? 1.0 : 0.0);
+      if (stop) {
+        col = c;
+        break;
+      }
+    }
+    sh.vs[j] = vj;
+    sh.h0s[j] = sqrt(w2) * (vj / sh.ss[j]);
+    sh.ss[j + 1] = 1.0 / sqrt(fmax(rest, fmax(w2 * 1e-28, 1e-300)));
+  }
+  if (col < 0) {  // ran to stop_col: the last column needs |u_{stop_col+1}| (one more round)
+    double u2;
+    if (!sum_at(a.stop_col + 2, 0, &u2)) return false;
+    const double sg = sqrt(u2);
+    col = a.stop_col;
+    finish_column(sh, a, col, sg * sh.vs[col] / sh.ss[col], 1.0 / sg);
+  }
+  // triangular solve (krylov.hip gmres_solve_kernel), y_k / sigma_k published for the x update
+  auto Hc = [&](int c, int k) -> l2& { return sh.H[(size_t)c * R1 + k]; };
+  if (Hc(col, col).x == 0.0 && Hc(col, col).y == 0.0) sh.S[col] = make_double2(0.0, 0.0);
+  l2* y = sh.coef;
+  for (int k = 0; k <= col; ++k) y[k] = sh.S[k];
+  for (int k = col; k > 0; --k) {
+    if (y[k].x != 0.0 || y[k].y != 0.0) {
+      y[k] = cdiv_smith(y[k], Hc(k, k));
+      const double2 tt = y[k];
+      for (int m = 0; m < k; ++m) y[m] = csub(y[m], cmul(tt, Hc(k, m)));
+    }
+  }
+  if (y[0].x != 0.0 || y[0].y != 0.0) y[0] = cdiv_smith(y[0], Hc(0, 0));
+  const unsigned ytag = gran_tag(a.seq, 0xff);
+  for (int k = 0; k <= col; ++k) {
+    const double2 c = cscale(y[k], sh.vs[k]);
+    st_gran(a.ycoef + 4 * k, ytag, c.x);
+    st_gran(a.ycoef + 4 * k + 2, ytag, c.y);
+  }
+  // (the coefficients' granules before the header: a reader that has the header polls them)
+  st_gran(a.ycoef + 4 * kMaxProj, ytag, (double)col);
+  return true;
+}
+
 template <bool CONSTC, bool JAC>
 __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kernel(SmallCycleArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int n = a.n, R = a.restart, R1 = R + 1;
+  const int n = a.n, R1 = a.restart + 1;
   const int g = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
-  // threads 0 .. nrow-1 own the row's columns; the last wave (lane `book`) keeps the books:
-  // it completes the previous Hessenberg column while the others update the basis
-  const int nrow = nt - kWave, book = nt - kWave;
   const bool act = t < n;
   const int tc = min(t, n - 1);
-  const unsigned G = gridDim.x;
+  const int G = n;  // row workgroups; workgroup n keeps the Givens books
   Shared sh;
   {
     using lc = HH_LDS char;
@@ -307,16 +375,21 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     };
     sh.U = (l2*)take(sizeof(double2) * (size_t)R1 * 3 * n);
     sh.zrow = (l2*)take(sizeof(double2) * n);
-    sh.H = (l2*)take(sizeof(double2) * (size_t)R * R1);
-    sh.Gr = (l2*)take(sizeof(double2) * 2 * (size_t)R);
+    sh.H = (l2*)take(sizeof(double2) * (size_t)a.restart * R1);
+    sh.Gr = (l2*)take(sizeof(double2) * 2 * (size_t)a.restart);
     sh.S = (l2*)take(sizeof(double2) * R1);
     sh.coef = (l2*)take(sizeof(double2) * R1);
     sh.vs = (l1*)take(sizeof(double) * R1);
     sh.ss = (l1*)take(sizeof(double) * R1);
-    sh.h0s = (l1*)take(sizeof(double) * R);
+    sh.h0s = (l1*)take(sizeof(double) * a.restart);
     sh.red = (l1*)take(sizeof(double) * (kRedRuns + kRuns));
     sh.sum = (l1*)take(sizeof(double) * kPStride);
     sh.ctl = (li*)take(sizeof(int) * 4);
+  }
+  if (g == G) {
+    if (t == 0 && !givens_role(sh, a))
+      __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
   }
   auto Urow = [&](int k, int r) -> l2* { return sh.U + ((size_t)k * 3 + r) * n; };
   const double2 z2 = make_double2(0.0, 0.0);
@@ -325,6 +398,7 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
   ar.sums = a.sums;
   ar.timeout = a.timeout_word;
   ar.seq = a.seq;
+  ar.G = G;
 
   // operator coefficients of this thread's point (stencil.hip's formulas; row g, column t)
   const double2 AW = a.tab_i[tc], AE = a.tab_i[n + tc], R1c = a.tab_i[2 * n + tc];
@@ -345,20 +419,18 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     const double2 u0 = a.v0[(size_t)min(max(gr, 0), n - 1) * n + tc];
     if (act) Urow(0, r)[t] = csel(gr >= 0 && gr < n, u0, z2);
   }
+  // gmres_start_kernel's scaling of V[0], on every workgroup
+  const double vs0 = 1.0 / sqrt(*a.mnorm2);
   if (t == 0) {
-    // gmres_start_kernel's scaling of V[0], on every workgroup
-    const double mn = sqrt(*a.mnorm2);
-    sh.vs[0] = 1.0 / mn;
-    sh.ss[0] = 1.0 / mn;
-    for (int k = 0; k < R1; ++k) sh.S[k] = make_double2(k == 0 ? mn : 0.0, 0.0);
-    sh.ctl[0] = sh.ctl[1] = sh.ctl[2] = sh.ctl[3] = 0;
+    sh.vs[0] = vs0;
+    sh.ctl[0] = 0;
   }
   __syncthreads();
 
   unsigned epoch = 0;
   // optional phase timing (workgroup 0, thread 0; s_memrealtime ticks): 0 stencil + z hand-off,
-  // 5 partial sums, 6 their publication, 1 all-reduce, 3 coefficients (+ the neighbours' z),
-  // 2 basis update, 4 the wait for the bookkeeping lane (Givens)
+  // 5 partial sums, 6 their publication, 1 all-reduce, 3 the neighbours' z (+ the verdict),
+  // 2 basis update (coefficients and the next scale inline), 4 the closing barrier
   const bool prof = a.phase_ticks != nullptr && g == 0 && t == 0;
   unsigned long long tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long tprev = prof ? wall_clock64() : 0;
@@ -371,6 +443,7 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     }
   };
   bool stopped = false;
+  double sj = vs0;  // scale of this iteration's SpMV input (every row thread holds it)
   for (int j = 0; j <= a.stop_col; ++j) {
     const int K = j + 1;
     const int cols = 2 * K + 2;
@@ -387,11 +460,10 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     Au = cfma(D, uC, Au);
     Au = cfma(E, uE, Au);
     Au = cfma(N, uN, Au);
-    const double sj = sh.ss[j];
     const double2 z = csel(act, JAC ? cscale(cdiv(Au, D), sj) : cscale(Au, sj), z2);
-    // hand the z row to the neighbours (sc1 stores); keep it in LDS for the partial sums
+    // hand the z row to the neighbours (tagged granules: no drain, they poll them); keep it in
+    // LDS for the partial sums
     const int par = epoch & 1;
-    // (tagged granules like the partial sums: no drain, the neighbours poll them)
     const unsigned rtag = gran_tag(a.seq, epoch + 1);
     unsigned long long* zout = a.zbuf + ((size_t)par * n + g) * 4 * n;
     if (act) {
@@ -479,6 +551,13 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
       }
     };
     if (act) load_ghosts();
+    // (and thread 0 the Givens workgroup's verdict on column j-2, checked after the all-reduce)
+    const unsigned long long* vp = a.verdict + 2 * max(j - 2, 0);
+    unsigned long long vg[2] = {0, 0};
+    if (t == 0 && j >= 2) {
+      vg[0] = __hip_atomic_load((gu64*)vp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      vg[1] = __hip_atomic_load((gu64*)(vp + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (!allreduce_rows(ar, par, epoch, cols, sh.sum, sh.red)) return;
     tick(1);
     double2 zl = z2, zh = z2;
@@ -503,94 +582,79 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
       zl = make_double2(dbl(zg[0], zg[1]), dbl(zg[2], zg[3]));
       zh = make_double2(dbl(zg[4], zg[5]), dbl(zg[6], zg[7]));
     }
-    // the lagged-normalisation step (krylov.hip gmres_lag_kernel), split: 1/|u_j| and the
-    // update coefficients first (one thread per basis vector) ...
-    const double vj = j >= 1 ? 1.0 / sqrt(sh.sum[2 * K + 1]) : sh.vs[0];
-    if (t <= j) {
-      const double vk = t == j ? vj : sh.vs[t];
-      const double2 d = make_double2(sh.sum[2 * t], sh.sum[2 * t + 1]);
-      sh.coef[t] = cscale(cscale(d, vk), vk);  // krylov.hip update_kernel's coefficient
-      sh.red[t] = cabs2(d) * vk * vk;  // the Pythagorean terms of the next input's scale
-      // column j of H (gmres_lag_kernel step (c)); the entries are untouched by the finishing
-      // of column j-1 below
-      sh.H[(size_t)j * R1 + t] = cscale(cscale(d, vk), vj / sh.ss[j]);
+    // the Givens workgroup's verdict on column j-2 (published two iterations ago, as a rule;
+    // every workgroup polls the same granule, so all stop at the same iteration)
+    if (t == 0 && j >= 2) {
+      const unsigned vtag = gran_tag(a.seq, j - 1);
+      double v = 0.0;
+      if ((unsigned)(vg[0] >> 32) == vtag && (unsigned)(vg[1] >> 32) == vtag)
+        v = __longlong_as_double((long long)((vg[0] << 32) | (vg[1] & 0xffffffffull)));
+      else if (!ld_gran(vp, vtag, &v))
+        zok = false;
+      sh.ctl[0] = v != 0.0 ? 1 : 0;
     }
-    if (__syncthreads_or(!zok)) {
+    // the lagged-normalisation step (krylov.hip gmres_lag_kernel / update_kernel) without a
+    // barrier of its own: every row thread forms the coefficients c_k = d_k / sigma_k^2 and the
+    // next input's Pythagorean scale (the same expressions, in the same order, on every thread)
+    const double vj = j >= 1 ? 1.0 / sqrt(sh.sum[2 * K + 1]) : vs0;
+    const double w2 = sh.sum[2 * K];
+    double rest = w2;
+    tick(3);
+    if (act) {
+      // u_{j+1} = z - sum_k c_k u_k on the own row and both ghost rows (neighbours' z from the
+      // all-reduce's round; beyond the grid the ghost stays zero); the three rows' chains
+      // interleaved, the loads of kStep basis vectors in flight together, terms in k order
+      constexpr int kStep = 4;
+      double2 w[3] = {zl, z, zh};
+      for (int k0 = 0; k0 < K; k0 += kStep) {
+        double2 cv[kStep], uv[3][kStep];
+        double tv[kStep];
+#pragma unroll
+        for (int i = 0; i < kStep; ++i) {
+          const int k = min(k0 + i, K - 1);
+          const double vk = k == j ? vj : sh.vs[k];
+          const double2 d = make_double2(sh.sum[2 * k], sh.sum[2 * k + 1]);
+          cv[i] = cscale(cscale(d, vk), vk);
+          tv[i] = cabs2(d) * vk * vk;
+#pragma unroll
+          for (int r = 0; r < 3; ++r) uv[r][i] = Urow(k, r)[t];
+        }
+#pragma unroll
+        for (int i = 0; i < kStep; ++i)
+          if (k0 + i < K) {
+            rest -= tv[i];
+#pragma unroll
+            for (int r = 0; r < 3; ++r) w[r] = csub(w[r], cmul(cv[i], uv[r][i]));
+          }
+      }
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int gr = g - 1 + r;
+        Urow(j + 1, r)[t] = csel(gr >= 0 && gr < n, w[r], z2);
+      }
+    }
+    if (t == 0) sh.vs[j] = vj;
+    sj = 1.0 / sqrt(fmax(rest, fmax(w2 * 1e-28, 1e-300)));
+    tick(2);
+    if (__syncthreads_or(!zok)) {  // (a neighbour's z or the verdict never arrived)
       if (t == 0)
         __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
-    tick(3);
-    if (t < nrow) {
-      // ... then u_{j+1} = z - sum_k c_k u_k on the own row and both ghost rows (neighbours'
-      // z from the all-reduce's round; beyond the grid the ghost stays zero)
-      if (act) {
-        // the three rows' chains interleaved (independent: 3x the FMA-latency overlap), the
-        // loads of kStep basis vectors in flight together; terms in k order per row
-        constexpr int kStep = 4;
-        double2 w[3] = {zl, z, zh};
-        for (int k0 = 0; k0 < K; k0 += kStep) {
-          double2 cv[kStep], uv[3][kStep];
-#pragma unroll
-          for (int i = 0; i < kStep; ++i) {
-            const int k = min(k0 + i, K - 1);
-            cv[i] = sh.coef[k];
-#pragma unroll
-            for (int r = 0; r < 3; ++r) uv[r][i] = Urow(k, r)[t];
-          }
-#pragma unroll
-          for (int i = 0; i < kStep; ++i)
-            if (k0 + i < K) {
-#pragma unroll
-              for (int r = 0; r < 3; ++r) w[r] = csub(w[r], cmul(cv[i], uv[r][i]));
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          const int gr = g - 1 + r;
-          Urow(j + 1, r)[t] = csel(gr >= 0 && gr < n, w[r], z2);
-        }
-      }
-      tick(2);
-    } else if (t == book) {
-      // ... while the bookkeeping lane completes column j-1 (its subdiagonal from |u_j|,
-      // rotations, presid, exit test) and starts column j
-      bool stop = false;
-      if (j >= 1) {
-        const int col = j - 1;
-        stop = finish_column(sh, a, col, (1.0 / vj) * sh.vs[col] / sh.ss[col], vj);
-      }
-      if (!stop) {
-        sh.vs[j] = vj;
-        const double f = vj / sh.ss[j];
-        const double w2 = sh.sum[2 * K];
-        double rest = w2;
-        for (int k0 = 0; k0 <= j; k0 += kBatch) {
-          double v[kBatch];
-#pragma unroll
-          for (int i = 0; i < kBatch; ++i) v[i] = sh.red[min(k0 + i, j)];
-#pragma unroll
-          for (int i = 0; i < kBatch; ++i)
-            if (k0 + i <= j) rest -= v[i];
-        }
-        sh.h0s[j] = sqrt(w2) * f;
-        sh.ss[j + 1] = 1.0 / sqrt(fmax(rest, fmax(w2 * 1e-28, 1e-300)));
-      }
-      sh.ctl[0] = stop ? 1 : 0;
-    }
-    __syncthreads();
     tick(4);
     if (sh.ctl[0]) {
       stopped = true;
       break;
     }
   }
-  if (prof)
+  if (prof) {
     for (int q = 0; q < 7; ++q) a.phase_ticks[q] += tk[q];
-  if (prof)  // shader-clock cycles over the loop (the effective clock: slot 7 / sum of slots)
+    // shader-clock cycles over the loop (the effective clock: slot 7 / sum of slots)
     a.phase_ticks[7] += __builtin_amdgcn_s_memtime() - cyc0;
+  }
   if (!stopped) {
-    // the cycle's last column needs |u_{stop_col+1}|: one more reduction round
+    // the cycle's last column needs |u_{stop_col+1}|: one more reduction round (for the Givens
+    // workgroup)
     const int last = a.stop_col + 1;
     const int par = epoch & 1;
     if (t == 0) {
@@ -601,31 +665,34 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     }
     epoch++;
     if (!allreduce_rows(ar, par, epoch, 1, sh.sum, sh.red)) return;
+  }
+  // the column the cycle solved for and y_k / sigma_k, from the Givens workgroup
+  {
+    const unsigned ytag = gran_tag(a.seq, 0xff);
+    bool ok = true;
     if (t == 0) {
-      const double sg = sqrt(sh.sum[0]);
-      const int col = a.stop_col;
-      finish_column(sh, a, col, sg * sh.vs[col] / sh.ss[col], 1.0 / sg);
+      double c = 0.0;
+      ok = ld_gran(a.ycoef + 4 * kMaxProj, ytag, &c);
+      sh.ctl[1] = (int)c;
     }
-    __syncthreads();
+    if (__syncthreads_or(!ok)) {
+      if (t == 0)
+        __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    const int col = sh.ctl[1];
+    if (t <= col) {
+      double cx = 0.0, cy = 0.0;
+      ok = ld_gran(a.ycoef + 4 * t, ytag, &cx) && ld_gran(a.ycoef + 4 * t + 2, ytag, &cy);
+      sh.coef[t] = make_double2(cx, cy);
+    }
+    if (__syncthreads_or(!ok)) {
+      if (t == 0)
+        __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
   }
-  // triangular solve (krylov.hip gmres_solve_kernel) on lane 0, then x += sum_k y_k v_k
   const int col = sh.ctl[1];
-  if (t == 0) {
-    auto Hc = [&](int c, int k) -> l2& { return sh.H[(size_t)c * R1 + k]; };
-    if (Hc(col, col).x == 0.0 && Hc(col, col).y == 0.0) sh.S[col] = z2;
-    l2* y = sh.coef;  // (in LDS: a dynamically indexed register array would go to scratch)
-    for (int k = 0; k <= col; ++k) y[k] = sh.S[k];
-    for (int k = col; k > 0; --k) {
-      if (y[k].x != 0.0 || y[k].y != 0.0) {
-        y[k] = cdiv_smith(y[k], Hc(k, k));
-        const double2 tt = y[k];
-        for (int m = 0; m < k; ++m) y[m] = csub(y[m], cmul(tt, Hc(k, m)));
-      }
-    }
-    if (y[0].x != 0.0 || y[0].y != 0.0) y[0] = cdiv_smith(y[0], Hc(0, 0));
-    for (int k = 0; k <= col; ++k) y[k] = cscale(y[k], sh.vs[k]);
-  }
-  __syncthreads();
   double2 xn = z2;
   if (act) {
     double2 acc = z2;
@@ -718,14 +785,16 @@ size_t small_cycle_lds_bytes(int n, int restart) {
 }
 
 size_t small_cycle_scratch_doubles(int n) {
-  // 8-byte granules: z rows [2][n][4n], x rows [n][4n], the all-reduce rows [2][n][2 kPStride]
-  // and sums [2][2 kPStride]
-  return 12 * (size_t)n * n + 4 * (size_t)kPStride * (n + 1);
+  // 8-byte granules: z rows [2][n][4n], x rows [n][4n], the all-reduce rows [2][n][2 kPStride],
+  // the sums of every round [kSmallRounds][2 kPStride], verdicts [kMaxProj][2], y [kMaxProj+1][4]
+  return 12 * (size_t)n * n + 4 * (size_t)kPStride * n + 2 * (size_t)kPStride * kSmallRounds +
+         2 * kMaxProj + 4 * (kMaxProj + 1);
 }
 
-bool small_cycle_eligible(int n, int restart) {
-  return n >= 1 && n <= kSmallThreads && restart >= 1 && restart < kMaxProj &&
-         small_cycle_lds_bytes(n, restart) <= (size_t)150 * 1024;
+bool small_cycle_eligible(int n, int restart, int device_cus) {
+  // n row workgroups + the Givens workgroup, one per CU (the LDS use allows no second)
+  return n >= 1 && n <= kSmallThreads && n + 1 <= device_cus && restart >= 1 &&
+         restart < kMaxProj && small_cycle_lds_bytes(n, restart) <= (size_t)150 * 1024;
 }
 
 template <bool C, bool J>
@@ -749,9 +818,9 @@ void launch_one(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds, hipS
 }
 
 void launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi, hipStream_t s) {
-  const int threads = (a.n + kWave - 1) / kWave * kWave + kWave;  // + the bookkeeping wave
+  const int threads = (a.n + kWave - 1) / kWave * kWave;
   const size_t lds = small_cycle_lds_bytes(a.n, a.restart);
-  const dim3 grid(a.n), block(threads);
+  const dim3 grid(a.n + 1), block(threads);  // + the Givens workgroup
   if (const_c) {
     if (jacobi) launch_one<true, true>(a, grid, block, lds, s);
     else launch_one<true, false>(a, grid, block, lds, s);

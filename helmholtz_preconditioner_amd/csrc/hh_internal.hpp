@@ -231,14 +231,17 @@ struct SmallCycleArgs {
   unsigned long long* zbuf;  // [2][n][4n] tagged granules of the z rows handed to the neighbours
   unsigned long long* xbuf;  // [n][4n] tagged granules of the new x rows (the residual)
   unsigned long long* part;  // [2][n][2 kSmallCols] tagged granules of the partial sums
-  unsigned long long* sums;  // [2][2 kSmallCols] tagged granules of the reduced sums
+  unsigned long long* sums;  // [kSmallRounds][2 kSmallCols] tagged granules of the reduced sums
+  unsigned long long* verdict;  // [kMaxProj][2] the Givens workgroup's per-column exit verdicts
+  unsigned long long* ycoef;    // [kMaxProj + 1][4] y_k / sigma_k, then the solved column
   unsigned seq;            // launch sequence number: the tags of this launch's granules
   unsigned* timeout_word;  // set when a wait gives up (zeroed at the start of a solve)
   unsigned long long* phase_ticks;  // optional [8]: workgroup 0's wall-clock ticks per phase
 };
 // columns of the small cycle's all-reduce rows: 2 K dot halves, |z|^2, |u_j|^2 (K <= kMaxProj)
 constexpr int kSmallCols = 2 * (kMaxProj + 1) + 2;
-bool small_cycle_eligible(int n, int restart);
+constexpr int kSmallRounds = kMaxProj + 8;  // all-reduce rounds per launch (<= restart + 3)
+bool small_cycle_eligible(int n, int restart, int device_cus);
 size_t small_cycle_lds_bytes(int n, int restart);
 size_t small_cycle_scratch_doubles(int n);
 void launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi, hipStream_t s);

@@ -639,6 +639,12 @@ void residual(hh_op* op, const double2* b, const double2* x, double2* v0, int ds
   }
 }
 
+int device_cus(hh_ctx* c) {
+  static int cus = 0;  // (one device model per process)
+  if (cus == 0) HIPC(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+  return cus;
+}
+
 // where residual(op, .., dst) left |M r|^2: red[dst + 1], or red[dst] itself for M = none
 int mnorm_slot(const hh_op* op, int dst) { return op->pkind == HH_PREC_NONE ? dst : dst + 1; }
 
@@ -1702,7 +1708,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
   const bool small = !reorth && op->small_cycle != 0 && c->world == 1 && op->slabs.size() == 1 &&
                      op->points == 5 &&
                      (op->pkind == HH_PREC_NONE || op->pkind == HH_PREC_JACOBI) &&
-                     (op->krylov_mode != 1) && small_cycle_eligible(op->n, restart) &&
+                     (op->krylov_mode != 1) && small_cycle_eligible(op->n, restart, device_cus(c)) &&
                      (op->small_cycle == 1 || (size_t)op->n * op->n <= ((size_t)1 << 18));
   unsigned* small_timeout = reinterpret_cast<unsigned*>(op->red + kRedTimeout);
   HIPC(hipMemsetAsync(small_timeout, 0, sizeof(double), s));  // (the device wait-bound word)
@@ -1762,6 +1768,8 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       sa.xbuf = sa.zbuf + 8 * (size_t)op->n * op->n;
       sa.part = sa.xbuf + 4 * (size_t)op->n * op->n;
       sa.sums = sa.part + 2 * (size_t)op->n * 2 * kSmallCols;
+      sa.verdict = sa.sums + (size_t)kSmallRounds * 2 * kSmallCols;
+      sa.ycoef = sa.verdict + 2 * kMaxProj;
       sa.seq = (++op->small_seq) & 0xffffffu;
       if (sa.seq == 0) sa.seq = op->small_seq = 1;  // (tag 0 is the zeroed scratch)
       sa.timeout_word = small_timeout;

@@ -229,7 +229,8 @@ int hh_op_set_krylov_mode(hh_op* op, int mode);
  * hh_gmres as ONE launch whose workgroups keep the Krylov basis on chip and meet once per inner
  * iteration (lagged normalisation as krylov mode 2), instead of five launches per iteration.
  * Applies on a single rank and slab, 5-point operator, M = none or Jacobi, without reorth, when
- * n <= 256 and the basis fits the LDS (3 n (restart + 1) x 16 B <= ~150 KB).  mode -1 (default):
+ * n <= 255 (n + 1 workgroups, one per CU) and the basis fits the LDS (3 n (restart + 1) x 16 B
+ * <= ~150 KB).  mode -1 (default):
  * used when it applies and n^2 <= 2^18; 1: whenever it applies; 0: never.  Results agree with the
  * regular cycle to rounding. */
 int hh_op_set_small_cycle(hh_op* op, int mode);
