@@ -332,28 +332,44 @@ __device__ bool givens_role(const Shared& sh, const SmallCycleArgs& a) {
     col = a.stop_col;
     finish_column(sh, a, col, sg * sh.vs[col] / sh.ss[col], 1.0 / sg);
   }
-  // triangular solve (krylov.hip gmres_solve_kernel), y_k / sigma_k published for the x update
+  sh.ctl[1] = col;
+  return true;
+}
+
+// The triangular solve (krylov.hip gmres_solve_kernel) on the Givens workgroup's first wave,
+// lane m holding y_m: for k = col .. 0, y_k /= H_kk (every lane, the same value), then lanes
+// m < k subtract y_k H_km in parallel -- the sequential solve's operations in its order, one
+// column step per iteration instead of one entry.  y_k / sigma_k published for the x update.
+__device__ void solve_and_publish(const Shared& sh, const SmallCycleArgs& a) {
+  const int R1 = a.restart + 1;
+  const int lane = threadIdx.x;
+  const int col = sh.ctl[1];
   auto Hc = [&](int c, int k) -> l2& { return sh.H[(size_t)c * R1 + k]; };
-  if (Hc(col, col).x == 0.0 && Hc(col, col).y == 0.0) sh.S[col] = make_double2(0.0, 0.0);
-  l2* y = sh.coef;
-  for (int k = 0; k <= col; ++k) y[k] = sh.S[k];
-  for (int k = col; k > 0; --k) {
-    if (y[k].x != 0.0 || y[k].y != 0.0) {
-      y[k] = cdiv_smith(y[k], Hc(k, k));
-      const double2 tt = y[k];
-      for (int m = 0; m < k; ++m) y[m] = csub(y[m], cmul(tt, Hc(k, m)));
+  const double2 hcc = Hc(col, col);
+  double2 y = make_double2(0.0, 0.0);
+  if (lane <= col) y = sh.S[lane];
+  if (lane == col && hcc.x == 0.0 && hcc.y == 0.0) y = make_double2(0.0, 0.0);
+  auto rl = [](double v, int k) {
+    const long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffff), k);
+    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), k);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  };
+  for (int k = col; k >= 0; --k) {
+    double2 yk = make_double2(rl(y.x, k), rl(y.y, k));
+    if (yk.x != 0.0 || yk.y != 0.0) {
+      yk = cdiv_smith(yk, Hc(k, k));
+      if (lane == k) y = yk;
+      if (lane < k) y = csub(y, cmul(yk, Hc(k, min(lane, k))));
     }
   }
-  if (y[0].x != 0.0 || y[0].y != 0.0) y[0] = cdiv_smith(y[0], Hc(0, 0));
   const unsigned ytag = gran_tag(a.seq, 0xff);
-  for (int k = 0; k <= col; ++k) {
-    const double2 c = cscale(y[k], sh.vs[k]);
-    st_gran(a.ycoef + 4 * k, ytag, c.x);
-    st_gran(a.ycoef + 4 * k + 2, ytag, c.y);
+  if (lane <= col) {
+    const double2 c = cscale(y, sh.vs[lane]);
+    st_gran(a.ycoef + 4 * lane, ytag, c.x);
+    st_gran(a.ycoef + 4 * lane + 2, ytag, c.y);
   }
-  // (the coefficients' granules before the header: a reader that has the header polls them)
-  st_gran(a.ycoef + 4 * kMaxProj, ytag, (double)col);
-  return true;
+  if (lane == 0) st_gran(a.ycoef + 4 * kMaxProj, ytag, (double)col);
 }
 
 template <bool CONSTC, bool JAC>
@@ -387,8 +403,15 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     sh.ctl = (li*)take(sizeof(int) * 4);
   }
   if (g == G) {
-    if (t == 0 && !givens_role(sh, a))
-      __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t >= kWave) return;
+    bool ok = true;
+    if (t == 0) ok = givens_role(sh, a);  // (lane 0; the wave reconverges after it)
+    if (__builtin_amdgcn_readfirstlane(ok ? 1 : 0) == 0) {
+      if (t == 0)
+        __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    solve_and_publish(sh, a);
     return;
   }
   auto Urow = [&](int k, int r) -> l2* { return sh.U + ((size_t)k * 3 + r) * n; };
@@ -696,7 +719,18 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
   double2 xn = z2;
   if (act) {
     double2 acc = z2;
-    for (int k = 0; k <= col; ++k) acc = cfma(sh.coef[k], Urow(k, 1)[t], acc);
+    for (int k0 = 0; k0 <= col; k0 += kBatch) {  // (loads in flight together, k order)
+      double2 cv[kBatch], uv[kBatch];
+#pragma unroll
+      for (int i = 0; i < kBatch; ++i) {
+        const int k = min(k0 + i, col);
+        cv[i] = sh.coef[k];
+        uv[i] = Urow(k, 1)[t];
+      }
+#pragma unroll
+      for (int i = 0; i < kBatch; ++i)
+        if (k0 + i <= col) acc = cfma(cv[i], uv[i], acc);
+    }
     double2* xp = a.x + (size_t)g * n + t;
     xn = cadd(*xp, acc);
     *xp = xn;
