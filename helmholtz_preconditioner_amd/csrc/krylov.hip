@@ -10,6 +10,8 @@
 // Every reduction is two-level and fixed-order (wave butterfly -> LDS -> per-block partial ->
 // one block per output summing partials in index order), so results are reproducible
 // run to run and identical on every rank after the RCCL allreduce.
+#include <cstdlib>
+
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
 
@@ -78,7 +80,11 @@ __global__ __launch_bounds__(kT) void multidot_kernel(const double2* __restrict_
 }
 
 // w_out = w - sum_k (s_k * (s_k * raw_k)) V_k; partials[blk][kMaxNorms]: [0] = |w_out|^2.
-template <int K, bool NT>
+// REV: the grid sweeps the vectors back to front.  The multidot before it swept them front to
+// back, so on a basis that (partly) fits the 256 MB Infinity Cache the update starts on the
+// lines the multidot left there last (and leaves the heads hot for the next multidot); each
+// element's arithmetic is unchanged, only the norm partials add in the reverse order.
+template <int K, bool NT, bool REV>
 __global__ __launch_bounds__(kT) void update_kernel(const double2* __restrict__ V, size_t ldv,
                                                     const double* __restrict__ raw,
                                                     const double* __restrict__ scale,
@@ -95,7 +101,11 @@ __global__ __launch_bounds__(kT) void update_kernel(const double2* __restrict__ 
   }
   double nrm = 0.0;
   const size_t stride = (size_t)gridDim.x * kT;
-  for (size_t p = (size_t)blockIdx.x * kT + threadIdx.x; p < len; p += stride) {
+  const size_t p0 = (size_t)blockIdx.x * kT + threadIdx.x;
+  const size_t steps = (len + stride - 1) / stride;
+  for (size_t i = 0; i < steps; ++i) {
+    const size_t p = (REV ? steps - 1 - i : i) * stride + p0;
+    if (p >= len) continue;
     double2 wv = w[p];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -379,6 +389,14 @@ int g_krylov_blocks = 0;
 constexpr size_t kSmallKrylovLen = (size_t)2 << 20;  // rank-local unknowns
 
 bool krylov_nt(size_t len) { return g_krylov_nt < 0 ? len > kSmallKrylovLen : g_krylov_nt != 0; }
+// back-to-front update sweeps with cached loads (HH_KRYLOV_REV=0 turns them off: diagnostic)
+bool krylov_rev() {
+  static const bool rev = [] {
+    const char* e = std::getenv("HH_KRYLOV_REV");
+    return !(e && e[0] == '0');
+  }();
+  return rev;
+}
 
 template <int K>
 void md_launch(const double2* V, size_t ldv, const double2* w, size_t len, double* part,
@@ -395,11 +413,14 @@ void up_launch(const double2* V, size_t ldv, const double* raw, const double* sc
                const double2* w, double2* wo, size_t len, double* part, int blocks,
                hipStream_t s, const int* stop) {
   if (krylov_nt(len))
-    hipLaunchKernelGGL((update_kernel<K, true>), dim3(blocks), dim3(kT), 0, s, V, ldv, raw, scale,
-                       w, wo, len, part, stop);
+    hipLaunchKernelGGL((update_kernel<K, true, false>), dim3(blocks), dim3(kT), 0, s, V, ldv, raw,
+                       scale, w, wo, len, part, stop);
+  else if (krylov_rev())
+    hipLaunchKernelGGL((update_kernel<K, false, true>), dim3(blocks), dim3(kT), 0, s, V, ldv, raw,
+                       scale, w, wo, len, part, stop);
   else
-    hipLaunchKernelGGL((update_kernel<K, false>), dim3(blocks), dim3(kT), 0, s, V, ldv, raw, scale,
-                       w, wo, len, part, stop);
+    hipLaunchKernelGGL((update_kernel<K, false, false>), dim3(blocks), dim3(kT), 0, s, V, ldv,
+                       raw, scale, w, wo, len, part, stop);
 }
 template <int K>
 void xu_launch(const double2* V, size_t ldv, const double2* y, double2* x, size_t len, int blocks,
