@@ -285,13 +285,14 @@ def make_precond(H, A, kind, sweeps):
 
 
 def timed_gmres(H, A, ctx, f_host, args, iters, wd=None):
-    """Warm-up (two iterations: the first restart cycle, first allreduces), then `iters`
-    timed legacy-counted inner iterations: (iterations, wall s max over ranks, history)."""
+    """Warm-up (one full restart cycle: first allreduces, and tens of ms of load so the clocks
+    have ramped), then `iters` timed legacy-counted inner iterations: (iterations, wall s max
+    over ranks, history)."""
     f = A.vector(f_host)
     M = make_precond(H, A, args.precond, args.sl_sweeps)
     if wd:
         wd.phase("gmres warm-up (first restart cycle, first in-solve allreduces)", 180)
-    H.gmres(A, f, rtol=1e-14, restart=args.restart, maxiter=2, M=M,
+    H.gmres(A, f, rtol=1e-14, restart=args.restart, maxiter=max(2, args.restart), M=M,
             callback=lambda r: None, callback_type="legacy")
     ctx.barrier()
     if wd:
