@@ -157,6 +157,14 @@ void launch_multidot(const double2* V, size_t ldv, int K, const double2* w, size
                      double* partials, int blocks, hipStream_t stream, const int* stop = nullptr);
 //   update: w_out = w - sum_k coef_k V_k, coef_k = scale_k^2 * raw_k (raw from reduced dots);
 //   acc |w_out|^2 into partials[blk][0]
+// Single-rank fused forms (one launch fewer each): the multidot whose last block also reduces
+// the `cols` partial columns into `out` (bit-identical to launch_reduce), and the update whose
+// last block also folds the norm partials and completes Hessenberg column `col` (bit-identical
+// to launch_gmres_column with norm partials).  `counter`: a zeroed device word per kernel,
+// re-armed by the kernel itself.
+void launch_multidot_reduced(const double2* V, size_t ldv, int K, const double2* w, size_t len,
+                             double* partials, int blocks, double* out, int cols,
+                             unsigned* counter, hipStream_t stream, const int* stop);
 void launch_update(const double2* V, size_t ldv, int K, const double* raw, const double* scale,
                    const double2* w, double2* w_out, size_t len, double* partials, int blocks,
                    hipStream_t stream, const int* stop = nullptr);
@@ -200,6 +208,11 @@ struct GivensState {
 // With norm_partials non-null, |w_new|^2 is instead summed from the update kernel's
 // `norm_count` block partials inside this launch (bit-identical to launch_reduce; single rank
 // only -- across ranks the norm needs the allreduce in between).
+void launch_update_column(const double2* V, size_t ldv, int K, const double* raw,
+                          const double* scale, const double2* w, double2* w_out, size_t len,
+                          double* partials, int blocks, hipStream_t stream, const int* stop,
+                          const GivensState& g, int col, const double* red_dots, double eps,
+                          double ptol, int stop_col, unsigned* counter);
 void launch_gmres_column(const GivensState& g, int col, const double* red_dots,
                          const double* red_norm, const double* norm_partials, int norm_count,
                          double eps, double ptol, int stop_col, hipStream_t stream);

@@ -29,8 +29,14 @@ __device__ __forceinline__ double2 ldnt(const double2* p) {
   }
 }
 
+using gu64k = __attribute__((address_space(1))) unsigned long long;
+using gu32k = __attribute__((address_space(1))) unsigned;
+
 // Block-reduce NV doubles held per thread; lane results land in partials[blk*width + k].
-template <int NV>
+// SC1: stored write-through at device scope (agent-scope relaxed atomic stores), for a last
+// block that reads them in the same launch (MI355X_MICROARCH.md's hand-off form: sc1 stores,
+// drained, then one lane's agent-scope ticket; no L2-writeback fence).
+template <int NV, bool SC1 = false>
 __device__ __forceinline__ void block_reduce_vec(double (&v)[NV], double* partials, int width) {
   __shared__ double red[NV][kT / kWave];
   const int lane = threadIdx.x & (kWave - 1);
@@ -47,16 +53,44 @@ __device__ __forceinline__ void block_reduce_vec(double (&v)[NV], double* partia
     double s = 0.0;
 #pragma unroll
     for (int w = 0; w < kT / kWave; ++w) s += red[k][w];
-    partials[(size_t)blockIdx.x * width + k] = s;
+    if constexpr (SC1)
+      __hip_atomic_store((gu64k*)(partials + (size_t)blockIdx.x * width + k),
+                         (unsigned long long)__double_as_longlong(s), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    else
+      partials[(size_t)blockIdx.x * width + k] = s;
   }
 }
 
+template <bool SC1 = false>
+__device__ double wave_reduce_like_block(const double* partials, int count, int width);
+__device__ void column_from_sums(const GivensState& g, int col, const double* rd, double rn0,
+                                 double eps, double ptol, int stop_col);
+
+// Last-block hand-off of a streaming kernel (single rank): every block has stored its partials;
+// it releases them (device-scope fence) and takes a ticket; the block holding the last ticket
+// acquires and does what the next, one-block kernel would have done -- one launch boundary
+// and one kernel start fewer per GMRES iteration.  The ticket counter is re-armed by that block.
+__device__ __forceinline__ bool last_block(unsigned* counter) {
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 partial stores landed
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add((gu32k*)counter, 1u, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  return last;
+}
+
 // partials[blk][2K+2]: [2k, 2k+1] = sum_p conj(V_k[p]) w[p];  [2K] = sum |w|^2.
-template <int K, bool NT>
+// FUSED: the last block also reduces the `cols` columns over all blocks into `out`, each column
+// by one wave in reduce_kernel's exact order (bit-identical to the separate reduce launch).
+template <int K, bool NT, bool FUSED>
 __global__ __launch_bounds__(kT) void multidot_kernel(const double2* __restrict__ V, size_t ldv,
                                                       const double2* __restrict__ w, size_t len,
                                                       double* __restrict__ partials,
-                                                      const int* stop) {
+                                                      const int* stop, double* out, int cols,
+                                                      unsigned* counter) {
   if (stop && *stop) return;
   double2 acc[K];
 #pragma unroll
@@ -76,7 +110,17 @@ __global__ __launch_bounds__(kT) void multidot_kernel(const double2* __restrict_
     v[2 * k + 1] = acc[k].y;
   }
   v[2 * K] = nrm;
-  block_reduce_vec<2 * K + 1>(v, partials, 2 * K + 2);
+  block_reduce_vec<2 * K + 1, FUSED>(v, partials, 2 * K + 2);
+  if constexpr (FUSED) {
+    if (last_block(counter)) {
+      const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+      for (int c = wave; c < cols; c += kT / kWave) {
+        const double r = wave_reduce_like_block<true>(partials + c, gridDim.x, 2 * K + 2);
+        if (lane == 0) out[c] = r;
+      }
+      if (threadIdx.x == 0) *counter = 0u;
+    }
+  }
 }
 
 // w_out = w - sum_k (s_k * (s_k * raw_k)) V_k; partials[blk][kMaxNorms]: [0] = |w_out|^2.
@@ -84,13 +128,22 @@ __global__ __launch_bounds__(kT) void multidot_kernel(const double2* __restrict_
 // back, so on a basis that (partly) fits the 256 MB Infinity Cache the update starts on the
 // lines the multidot left there last (and leaves the heads hot for the next multidot); each
 // element's arithmetic is unchanged, only the norm partials add in the reverse order.
-template <int K, bool NT, bool REV>
+// FUSED (single rank): the last block also folds the norm partials and completes the Hessenberg
+// column (gmres_column_kernel's work, bit-identical), one launch fewer per iteration.
+struct ColumnFuse {
+  GivensState g;
+  int col, stop_col;
+  const double* rd;
+  double eps, ptol;
+  unsigned* counter;
+};
+template <int K, bool NT, bool REV, bool FUSED>
 __global__ __launch_bounds__(kT) void update_kernel(const double2* __restrict__ V, size_t ldv,
                                                     const double* __restrict__ raw,
                                                     const double* __restrict__ scale,
                                                     const double2* w, double2* w_out, size_t len,
                                                     double* __restrict__ partials,
-                                                    const int* stop) {
+                                                    const int* stop, const ColumnFuse cf) {
   if (stop && *stop) return;
   double2 coef[K];
 #pragma unroll
@@ -116,7 +169,16 @@ __global__ __launch_bounds__(kT) void update_kernel(const double2* __restrict__ 
     nrm = fma(wv.x, wv.x, fma(wv.y, wv.y, nrm));
   }
   double v[1] = {nrm};
-  block_reduce_vec<1>(v, partials, kMaxNorms);
+  block_reduce_vec<1, FUSED>(v, partials, kMaxNorms);
+  if constexpr (FUSED) {
+    if (last_block(cf.counter)) {
+      if (threadIdx.x < kWave) {
+        const double rn0 = wave_reduce_like_block<true>(partials, gridDim.x, kMaxNorms);
+        if (threadIdx.x == 0) column_from_sums(cf.g, cf.col, cf.rd, rn0, cf.eps, cf.ptol, cf.stop_col);
+      }
+      if (threadIdx.x == 0) *cf.counter = 0u;
+    }
+  }
 }
 
 // x += sum_k y_k V_k.
@@ -218,14 +280,20 @@ __device__ void zlartg(double2 f, double2 g, double* c, double2* s, double2* r) 
 // wave in exactly reduce_kernel's order: the 256 strided partial sums of its threads, then its
 // LDS tree (steps 128 and 64 inside each lane's four sums, 32 .. 1 by shuffles).  Every lane
 // returns; lane 0's value is the result, bit-identical to reduce_kernel's out[0].
+template <bool SC1>
 __device__ double wave_reduce_like_block(const double* partials, int count, int width) {
   static_assert(kT == 4 * kWave, "four strided sums per lane emulate a 256-thread block");
-  const int l = threadIdx.x;
+  const int l = threadIdx.x & (kWave - 1);
   double s[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     double acc = 0.0;
-    for (int b = l + q * kWave; b < count; b += kT) acc += partials[(size_t)b * width];
+    for (int b = l + q * kWave; b < count; b += kT) {
+      const double* p = partials + (size_t)b * width;
+      acc += SC1 ? __longlong_as_double((long long)__hip_atomic_load(
+                       (gu64k*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                 : *p;
+    }
     s[q] = acc;
   }
   s[0] += s[2];  // off = 128: threads l and l + 64
@@ -284,6 +352,17 @@ __device__ void gmres_finish_column(const GivensState& g, int col, double h0, do
   if (presid <= ptol || brk != 0.0 || col >= stop_col) g.ctrl[0] = 1;
 }
 
+// column `col` from the reduced dots rd and |w_new|^2 = rn0 (lane 0)
+__device__ void column_from_sums(const GivensState& g, int col, const double* rd, double rn0,
+                                 double eps, double ptol, int stop_col) {
+  const int R1 = g.restart + 1;
+  double2* h = g.H + (size_t)col * R1;
+  for (int k = 0; k <= col; ++k) h[k] = cscale(make_double2(rd[2 * k], rd[2 * k + 1]), g.vscale[k]);
+  const double h0 = sqrt(rd[2 * (col + 1)]);
+  const double h1 = sqrt(rn0);
+  gmres_finish_column(g, col, h0, h1, 1.0 / h1, eps, ptol, stop_col);
+}
+
 __global__ void gmres_column_kernel(GivensState g, int col, const double* rd, const double* rn,
                                     const double* npart, int ncount, double eps, double ptol,
                                     int stop_col) {
@@ -294,12 +373,7 @@ __global__ void gmres_column_kernel(GivensState g, int col, const double* rd, co
   }
   if (threadIdx.x != 0) return;
   if (!npart) rn0 = rn[0];
-  const int R1 = g.restart + 1;
-  double2* h = g.H + (size_t)col * R1;
-  for (int k = 0; k <= col; ++k) h[k] = cscale(make_double2(rd[2 * k], rd[2 * k + 1]), g.vscale[k]);
-  const double h0 = sqrt(rd[2 * (col + 1)]);
-  const double h1 = sqrt(rn0);
-  gmres_finish_column(g, col, h0, h1, 1.0 / h1, eps, ptol, stop_col);
+  column_from_sums(g, col, rd, rn0, eps, ptol, stop_col);
 }
 
 // One-allreduce iteration j (lagged normalisation, world > 1; see runtime.cpp hh_gmres).  The
@@ -400,27 +474,45 @@ bool krylov_rev() {
 
 template <int K>
 void md_launch(const double2* V, size_t ldv, const double2* w, size_t len, double* part,
-               int blocks, hipStream_t s, const int* stop) {
+               int blocks, hipStream_t s, const int* stop, double* out, int cols,
+               unsigned* counter) {
+  const bool nt = krylov_nt(len);
+  if (counter) {
+    if (nt)
+      hipLaunchKernelGGL((multidot_kernel<K, true, true>), dim3(blocks), dim3(kT), 0, s, V, ldv,
+                         w, len, part, stop, out, cols, counter);
+    else
+      hipLaunchKernelGGL((multidot_kernel<K, false, true>), dim3(blocks), dim3(kT), 0, s, V, ldv,
+                         w, len, part, stop, out, cols, counter);
+  } else {
+    if (nt)
+      hipLaunchKernelGGL((multidot_kernel<K, true, false>), dim3(blocks), dim3(kT), 0, s, V, ldv,
+                         w, len, part, stop, out, cols, counter);
+    else
+      hipLaunchKernelGGL((multidot_kernel<K, false, false>), dim3(blocks), dim3(kT), 0, s, V,
+                         ldv, w, len, part, stop, out, cols, counter);
+  }
+}
+template <int K, bool FUSED>
+void up_launch_t(const double2* V, size_t ldv, const double* raw, const double* scale,
+                 const double2* w, double2* wo, size_t len, double* part, int blocks,
+                 hipStream_t s, const int* stop, const ColumnFuse& cf) {
   if (krylov_nt(len))
-    hipLaunchKernelGGL((multidot_kernel<K, true>), dim3(blocks), dim3(kT), 0, s, V, ldv, w, len,
-                       part, stop);
+    hipLaunchKernelGGL((update_kernel<K, true, false, FUSED>), dim3(blocks), dim3(kT), 0, s, V,
+                       ldv, raw, scale, w, wo, len, part, stop, cf);
+  else if (krylov_rev())
+    hipLaunchKernelGGL((update_kernel<K, false, true, FUSED>), dim3(blocks), dim3(kT), 0, s, V,
+                       ldv, raw, scale, w, wo, len, part, stop, cf);
   else
-    hipLaunchKernelGGL((multidot_kernel<K, false>), dim3(blocks), dim3(kT), 0, s, V, ldv, w, len,
-                       part, stop);
+    hipLaunchKernelGGL((update_kernel<K, false, false, FUSED>), dim3(blocks), dim3(kT), 0, s, V,
+                       ldv, raw, scale, w, wo, len, part, stop, cf);
 }
 template <int K>
 void up_launch(const double2* V, size_t ldv, const double* raw, const double* scale,
                const double2* w, double2* wo, size_t len, double* part, int blocks,
-               hipStream_t s, const int* stop) {
-  if (krylov_nt(len))
-    hipLaunchKernelGGL((update_kernel<K, true, false>), dim3(blocks), dim3(kT), 0, s, V, ldv, raw,
-                       scale, w, wo, len, part, stop);
-  else if (krylov_rev())
-    hipLaunchKernelGGL((update_kernel<K, false, true>), dim3(blocks), dim3(kT), 0, s, V, ldv, raw,
-                       scale, w, wo, len, part, stop);
-  else
-    hipLaunchKernelGGL((update_kernel<K, false, false>), dim3(blocks), dim3(kT), 0, s, V, ldv,
-                       raw, scale, w, wo, len, part, stop);
+               hipStream_t s, const int* stop, const ColumnFuse* cf) {
+  if (cf) up_launch_t<K, true>(V, ldv, raw, scale, w, wo, len, part, blocks, s, stop, *cf);
+  else up_launch_t<K, false>(V, ldv, raw, scale, w, wo, len, part, blocks, s, stop, ColumnFuse{});
 }
 template <int K>
 void xu_launch(const double2* V, size_t ldv, const double2* y, double2* x, size_t len, int blocks,
@@ -431,9 +523,9 @@ void xu_launch(const double2* V, size_t ldv, const double2* y, double2* x, size_
 template <int... Ks>
 struct KTable {
   using MD = void (*)(const double2*, size_t, const double2*, size_t, double*, int, hipStream_t,
-                      const int*);
+                      const int*, double*, int, unsigned*);
   using UP = void (*)(const double2*, size_t, const double*, const double*, const double2*,
-                      double2*, size_t, double*, int, hipStream_t, const int*);
+                      double2*, size_t, double*, int, hipStream_t, const int*, const ColumnFuse*);
   using XU = void (*)(const double2*, size_t, const double2*, double2*, size_t, int, hipStream_t);
   static constexpr MD md[] = {md_launch<Ks>...};
   static constexpr UP up[] = {up_launch<Ks>...};
@@ -461,13 +553,35 @@ int stream_blocks(size_t len) {
 
 void launch_multidot(const double2* V, size_t ldv, int K, const double2* w, size_t len,
                      double* partials, int blocks, hipStream_t stream, const int* stop) {
-  Table::md[K - 1](V, ldv, w, len, partials, blocks, stream, stop);
+  Table::md[K - 1](V, ldv, w, len, partials, blocks, stream, stop, nullptr, 0, nullptr);
+}
+
+void launch_multidot_reduced(const double2* V, size_t ldv, int K, const double2* w, size_t len,
+                             double* partials, int blocks, double* out, int cols,
+                             unsigned* counter, hipStream_t stream, const int* stop) {
+  Table::md[K - 1](V, ldv, w, len, partials, blocks, stream, stop, out, cols, counter);
 }
 
 void launch_update(const double2* V, size_t ldv, int K, const double* raw, const double* scale,
                    const double2* w, double2* w_out, size_t len, double* partials, int blocks,
                    hipStream_t stream, const int* stop) {
-  Table::up[K - 1](V, ldv, raw, scale, w, w_out, len, partials, blocks, stream, stop);
+  Table::up[K - 1](V, ldv, raw, scale, w, w_out, len, partials, blocks, stream, stop, nullptr);
+}
+
+void launch_update_column(const double2* V, size_t ldv, int K, const double* raw,
+                          const double* scale, const double2* w, double2* w_out, size_t len,
+                          double* partials, int blocks, hipStream_t stream, const int* stop,
+                          const GivensState& g, int col, const double* red_dots, double eps,
+                          double ptol, int stop_col, unsigned* counter) {
+  ColumnFuse cf{};
+  cf.g = g;
+  cf.col = col;
+  cf.stop_col = stop_col;
+  cf.rd = red_dots;
+  cf.eps = eps;
+  cf.ptol = ptol;
+  cf.counter = counter;
+  Table::up[K - 1](V, ldv, raw, scale, w, w_out, len, partials, blocks, stream, stop, &cf);
 }
 
 void launch_xupdate(const double2* V, size_t ldv, int K, const double2* y, double2* x,

@@ -157,6 +157,16 @@ struct hh_op {
   double* small_scr = nullptr;
   unsigned small_seq = 0;          // launch sequence number (the tags of its hand-off granules)
   unsigned long long* small_ticks = nullptr;  // phase timing of the small cycle (diagnostic)
+  // fused single-rank Krylov kernels (last-block reductions): their ticket counters
+  unsigned* kcount = nullptr;
+  // HH_KRYLOV_FUSE bit 0: multidot + reduce, bit 1: update + Givens column as last-block fused
+  // kernels.  Off by default: measured no faster at 1024^2 (update+column 8 975-9 077 vs 8 878-
+  // 9 105 it/s unfused; multidot+reduce 8 219 -- its last block's reduction is a serial chain
+  // of device-scope loads; profiles/r02c2e_fuse_ab.log)
+  int fuse_krylov = [] {
+    const char* e = std::getenv("HH_KRYLOV_FUSE");
+    return e ? std::atoi(e) : 0;
+  }();
   // timing hooks
   hipEvent_t tk0 = nullptr, tk1 = nullptr;
   // device stop flag of the GMRES cycle being queued (nullptr outside hh_gmres)
@@ -678,6 +688,10 @@ void ensure_gmres(hh_op* op, int restart) {
   g.status_it = g.status + 8;
   g.sscale = g.status_it + 4 * (size_t)restart;
   if (!op->npart) op->npart = dalloc<double>((size_t)kMaxStreamBlocks * kMaxNorms);
+  if (!op->kcount) {
+    op->kcount = dalloc<unsigned>(4);
+    HIPC(hipMemsetAsync(op->kcount, 0, 4 * sizeof(unsigned), op->ctx->stream));
+  }
   // the per-iteration statuses and the cycle's control words live in the reduction buffer,
   // next to the residual norms: the end of a cycle reads them all with ONE copy (kRedReport)
   g.status_it = op->red + kRedStatus;
@@ -1034,6 +1048,7 @@ static void op_release(hh_op* op) {
   dfree(op->npart);
   dfree(op->small_scr);
   dfree(op->small_ticks);
+  dfree(op->kcount);
   dfree(op->sw_P);
   dfree(op->sw_y);
   dfree(op->sw_uF);
@@ -1809,6 +1824,29 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       apply_MA(op, vcol, g.vscale + c2, w);  // w = M A v_col
       const int K = c2 + 1;
       // classical Gram-Schmidt: raw dots u_k^H w (+ |w|^2), then w -= sum h_k v_k, |w|^2
+      // single rank, no second pass, HH_KRYLOV_FUSE: the multidot's last block reduces the dots
+      // and / or the update's last block folds the norm and completes the column (bit-identical
+      // to the separate launches)
+      const int fuse = c->world == 1 && !reorth ? op->fuse_krylov : 0;
+      if (fuse) {
+        if (fuse & 1) {
+          launch_multidot_reduced(V, ldv, K, w, L, op->partials, blocks, op->red + 16, 2 * K + 1,
+                                  op->kcount, s, stp);
+        } else {
+          launch_multidot(V, ldv, K, w, L, op->partials, blocks, s, stp);
+          launch_reduce(op->partials, blocks, 2 * K + 2, 2 * K + 1, op->red + 16, s, stp);
+        }
+        if (fuse & 2) {
+          launch_update_column(V, ldv, K, op->red + 16, g.vscale, w, w, L, op->partials, blocks,
+                               s, stp, g, c2, op->red + 16, eps, ptol, stop_col, op->kcount + 1);
+        } else {
+          launch_update(V, ldv, K, op->red + 16, g.vscale, w, w, L, op->partials, blocks, s, stp);
+          launch_gmres_column(g, c2, op->red + 16, op->red + 8, op->partials, blocks, eps, ptol,
+                              stop_col, s);
+        }
+        HIPC(hipGetLastError());
+        continue;
+      }
       launch_multidot(V, ldv, K, w, L, op->partials, blocks, s, stp);
       launch_reduce(op->partials, blocks, 2 * K + 2, 2 * K + 1, op->red + 16, s, stp);
       allreduce_sum_dev(op, op->red + 16, 2 * K + 1);
