@@ -181,8 +181,8 @@ __global__ __launch_bounds__(kT) void update_kernel(const double2* __restrict__ 
   }
 }
 
-// x += sum_k y_k V_k.
-template <int K>
+// x += sum_k y_k V_k (NT: the basis is dead after this pass; non-temporal loads at 4096^2).
+template <int K, bool NT>
 __global__ __launch_bounds__(kT) void xupdate_kernel(const double2* __restrict__ V, size_t ldv,
                                                      const double2* __restrict__ y,
                                                      double2* __restrict__ x, size_t len) {
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(kT) void xupdate_kernel(const double2* __restrict__
   for (size_t p = (size_t)blockIdx.x * kT + threadIdx.x; p < len; p += stride) {
     double2 t = make_double2(0.0, 0.0);
 #pragma unroll
-    for (int k = 0; k < K; ++k) t = cfma(c[k], V[(size_t)k * ldv + p], t);
+    for (int k = 0; k < K; ++k) t = cfma(c[k], ldnt<NT>(V + (size_t)k * ldv + p), t);
     x[p] = cadd(x[p], t);
   }
 }
@@ -517,7 +517,10 @@ void up_launch(const double2* V, size_t ldv, const double* raw, const double* sc
 template <int K>
 void xu_launch(const double2* V, size_t ldv, const double2* y, double2* x, size_t len, int blocks,
                hipStream_t s) {
-  hipLaunchKernelGGL((xupdate_kernel<K>), dim3(blocks), dim3(kT), 0, s, V, ldv, y, x, len);
+  if (krylov_nt(len))
+    hipLaunchKernelGGL((xupdate_kernel<K, true>), dim3(blocks), dim3(kT), 0, s, V, ldv, y, x, len);
+  else
+    hipLaunchKernelGGL((xupdate_kernel<K, false>), dim3(blocks), dim3(kT), 0, s, V, ldv, y, x, len);
 }
 
 template <int... Ks>
