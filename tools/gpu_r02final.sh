@@ -26,6 +26,7 @@ if [ "$PART" = a ]; then
   step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5
   step bench 300 python bench.py
 else
+  step t_krylov 600 python -u -m pytest -q -x --timeout 300 --timeout-method thread -m gpu tests/test_gpu_gmres.py tests/test_gpu_krylov_modes.py tests/test_gpu_configs.py
   for c in 1 2 4 5; do step bench_config$c 240 python bench.py --config $c --no-cpu-baseline; done
   step rocprof 240 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --gmres-iters 40
   python3 tools/rocprof_timed_avg.py "$OUT/prof/run_kernel_trace.csv" "void hh::(anonymous namespace)::tile_kernel<0, false, 4" 200 > "$OUT/rocprof_timed.log" 2>&1 || true
