@@ -155,10 +155,7 @@ __global__ __launch_bounds__(kT) void update_kernel(const double2* __restrict__ 
   double nrm = 0.0;
   const size_t stride = (size_t)gridDim.x * kT;
   const size_t p0 = (size_t)blockIdx.x * kT + threadIdx.x;
-  const size_t steps = (len + stride - 1) / stride;
-  for (size_t i = 0; i < steps; ++i) {
-    const size_t p = (REV ? steps - 1 - i : i) * stride + p0;
-    if (p >= len) continue;
+  auto point = [&](size_t p) {
     double2 wv = w[p];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -167,6 +164,16 @@ __global__ __launch_bounds__(kT) void update_kernel(const double2* __restrict__ 
     }
     w_out[p] = wv;
     nrm = fma(wv.x, wv.x, fma(wv.y, wv.y, nrm));
+  };
+  if constexpr (REV) {
+    const size_t steps = (len + stride - 1) / stride;
+    for (size_t i = steps; i-- > 0;) {
+      const size_t p = i * stride + p0;
+      if (p < len) point(p);
+    }
+  } else {
+    // (the plain forward loop: the REV loop's form measured 4-8 % slower here for K >= 13)
+    for (size_t p = p0; p < len; p += stride) point(p);
   }
   double v[1] = {nrm};
   block_reduce_vec<1, FUSED>(v, partials, kMaxNorms);
