@@ -20,7 +20,12 @@ step() {  # step NAME SECONDS CMD...
   if fatal $rc; then echo "FATAL rc=$rc in $name: stopping"; exit $rc; fi
   return 0
 }
-if [ "$PART" = a ]; then
+if [ "$PART" = c ]; then  # Krylov re-check: GMRES/Krylov tests, bench, rocprof of the bench
+  step t_krylov 600 python -u -m pytest -q -x --timeout 300 --timeout-method thread -m gpu tests/test_gpu_gmres.py tests/test_gpu_krylov_modes.py tests/test_gpu_configs.py
+  step bench 300 python bench.py
+  step bench_config4 240 python bench.py --config 4 --no-cpu-baseline
+  step rocprof 240 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --gmres-iters 40
+elif [ "$PART" = a ]; then
   step t_all 900 python -u -m pytest -q -x --timeout 300 --timeout-method thread -m gpu tests
   step smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
   step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5
