@@ -67,6 +67,8 @@ struct Shared {  // LDS layout (carved from dynamic shared memory; see small_cyc
   l1* red;   // [kRedRuns + kRuns] segment sums of the partial sums, run sums of the reducer
   l1* sum;   // [PSTRIDE] reduced sums
   li* ctl;   // [4]: 0 stop, 1 last column, 2 abort
+  l1* gv;    // [2]: presid and breakdown of the last finished column (Givens workgroup; then
+             // workgroup 0, for the restart loop's decisions)
 };
 
 // All-reduce of `cols` doubles per workgroup with NO counter and NO flag: every value travels
@@ -224,7 +226,7 @@ __device__ __forceinline__ Rot zlartg_s(double2 f, double2 g) {
 // lane 0: complete column `col` with its subdiagonal h1 (krylov.hip gmres_finish_column); the
 // status of the column goes to status_it (workgroup 0 only).  Returns true when the cycle stops.
 __device__ bool finish_column(const Shared& sh, const SmallCycleArgs& a, int col, double h1,
-                              double inv_sigma_next) {
+                              double inv_sigma_next, double ptol, int stop_col) {
   const int R1 = a.restart + 1;
   l2* h = sh.H + (size_t)col * R1;
   const double h0 = sh.h0s[col];
@@ -274,7 +276,9 @@ __device__ bool finish_column(const Shared& sh, const SmallCycleArgs& a, int col
     st[3] = h1;
   }
   sh.ctl[1] = col;
-  return presid <= a.ptol || brk != 0.0 || col >= a.stop_col;
+  sh.gv[0] = presid;
+  sh.gv[1] = brk;
+  return presid <= ptol || brk != 0.0 || col >= stop_col;
 }
 
 
@@ -284,7 +288,7 @@ __device__ bool finish_column(const Shared& sh, const SmallCycleArgs& a, int col
 // exit tests -- so none of it sits on the row workgroups' critical path.  Per column it
 // publishes a verdict granule (0 continue / 1 stop), at the end the column the cycle solved for
 // and y_k / sigma_k.  Returns false on timeout.
-__device__ bool givens_role(const Shared& sh, const SmallCycleArgs& a) {
+__device__ bool givens_role(const Shared& sh, const SmallCycleArgs& a, int stop_col, double ptol) {
   const int R1 = a.restart + 1;
   const unsigned long long* sums = a.sums;
   auto sum_at = [&](unsigned epoch, int c, double* v) {
@@ -295,7 +299,7 @@ __device__ bool givens_role(const Shared& sh, const SmallCycleArgs& a) {
   sh.ss[0] = 1.0 / mn;
   for (int k = 0; k < R1; ++k) sh.S[k] = make_double2(k == 0 ? mn : 0.0, 0.0);
   int col = -1;
-  for (int j = 0; j <= a.stop_col && col < 0; ++j) {
+  for (int j = 0; j <= stop_col && col < 0; ++j) {
     const int K = j + 1;
     const unsigned epoch = j + 1;
     double w2, u2 = 0.0;
@@ -314,7 +318,8 @@ __device__ bool givens_role(const Shared& sh, const SmallCycleArgs& a) {
     }
     if (j >= 1) {
       const int c = j - 1;
-      const bool stop = finish_column(sh, a, c, (1.0 / vj) * sh.vs[c] / sh.ss[c], vj);
+      const bool stop =
+          finish_column(sh, a, c, (1.0 / vj) * sh.vs[c] / sh.ss[c], vj, ptol, stop_col);
       st_gran(a.verdict + 2 * c, gran_tag(a.seq, c + 1), stop ? 1.0 : 0.0);
       if (stop) {
         col = c;
@@ -327,10 +332,10 @@ __device__ bool givens_role(const Shared& sh, const SmallCycleArgs& a) {
   }
   if (col < 0) {  // ran to stop_col: the last column needs |u_{stop_col+1}| (one more round)
     double u2;
-    if (!sum_at(a.stop_col + 2, 0, &u2)) return false;
+    if (!sum_at(stop_col + 2, 0, &u2)) return false;
     const double sg = sqrt(u2);
-    col = a.stop_col;
-    finish_column(sh, a, col, sg * sh.vs[col] / sh.ss[col], 1.0 / sg);
+    col = stop_col;
+    finish_column(sh, a, col, sg * sh.vs[col] / sh.ss[col], 1.0 / sg, ptol, stop_col);
   }
   sh.ctl[1] = col;
   return true;
@@ -369,7 +374,11 @@ __device__ void solve_and_publish(const Shared& sh, const SmallCycleArgs& a) {
     st_gran(a.ycoef + 4 * lane, ytag, c.x);
     st_gran(a.ycoef + 4 * lane + 2, ytag, c.y);
   }
-  if (lane == 0) st_gran(a.ycoef + 4 * kMaxProj, ytag, (double)col);
+  // header: the column (+ 64 on a breakdown) and its presid, for the restart loop's decisions
+  if (lane == 0) {
+    st_gran(a.ycoef + 4 * kMaxProj, ytag, (double)(col + (sh.gv[1] != 0.0 ? 64 : 0)));
+    st_gran(a.ycoef + 4 * kMaxProj + 2, ytag, sh.gv[0]);
+  }
 }
 
 template <bool CONSTC, bool JAC>
@@ -401,11 +410,28 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     sh.red = (l1*)take(sizeof(double) * (kRedRuns + kRuns));
     sh.sum = (l1*)take(sizeof(double) * kPStride);
     sh.ctl = (li*)take(sizeof(int) * 4);
+    sh.gv = (l1*)take(sizeof(double) * 2);
+  }
+  // this cycle's stop column and inner tolerance: as given, or from the restart loop's state
+  // that the previous queued cycle left (a finished solve or a timeout: nothing to do)
+  int stop_col = a.stop_col;
+  double ptol = a.ptol;
+  if (a.outer) {
+    const double* o = a.outer;
+    if (o[6] != 0.0 || *a.timeout_word != 0u) {
+      if (g == 0 && t == 0) a.g.ctrl[0] = 2;
+      return;
+    }
+    ptol = o[0];
+    if (o[5] != 0.0) {  // legacy: maxiter caps the inner iterations
+      const double left = o[4] - o[3];
+      stop_col = left >= (double)a.restart ? a.restart - 1 : (int)left - 1;
+    }
   }
   if (g == G) {
     if (t >= kWave) return;
     bool ok = true;
-    if (t == 0) ok = givens_role(sh, a);  // (lane 0; the wave reconverges after it)
+    if (t == 0) ok = givens_role(sh, a, stop_col, ptol);  // (lane 0; the wave reconverges after it)
     if (__builtin_amdgcn_readfirstlane(ok ? 1 : 0) == 0) {
       if (t == 0)
         __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -467,7 +493,7 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
   };
   bool stopped = false;
   double sj = vs0;  // scale of this iteration's SpMV input (every row thread holds it)
-  for (int j = 0; j <= a.stop_col; ++j) {
+  for (int j = 0; j <= stop_col; ++j) {
     const int K = j + 1;
     const int cols = 2 * K + 2;
     // z = M A (s_j u_j) on the own row (zero Dirichlet rows beyond the grid are zero ghosts)
@@ -678,7 +704,7 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
   if (!stopped) {
     // the cycle's last column needs |u_{stop_col+1}|: one more reduction round (for the Givens
     // workgroup)
-    const int last = a.stop_col + 1;
+    const int last = stop_col + 1;
     const int par = epoch & 1;
     if (t == 0) {
       const l2* ul = Urow(last, 1);
@@ -694,9 +720,13 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     const unsigned ytag = gran_tag(a.seq, 0xff);
     bool ok = true;
     if (t == 0) {
-      double c = 0.0;
+      double c = 0.0, pr = 0.0;
       ok = ld_gran(a.ycoef + 4 * kMaxProj, ytag, &c);
-      sh.ctl[1] = (int)c;
+      if (ok && g == 0) ok = ld_gran(a.ycoef + 4 * kMaxProj + 2, ytag, &pr);
+      const int cb = (int)c;
+      sh.ctl[1] = cb & 63;
+      sh.gv[0] = pr;
+      sh.gv[1] = cb >= 64 ? 1.0 : 0.0;
     }
     if (__syncthreads_or(!ok)) {
       if (t == 0)
@@ -803,6 +833,26 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     a.red[5] = sh.sum[1];
     a.report[4] = sh.sum[0];  // (host: this cycle's report)
     a.report[5] = sh.sum[1];
+    if (a.outer) {
+      // scipy's restart-loop decisions (the end of iterative.py's outer loop, exactly as
+      // runtime.cpp hh_gmres takes them)
+      // for the cycle queued behind this one
+      double* o = a.outer;
+      const double presid = sh.gv[0];
+      const double rn = sqrt(sh.sum[0]);
+      const double inner = o[3] + (double)(col + 1);
+      const bool done = (o[5] != 0.0 && inner >= o[4]) || rn <= o[2] || sh.gv[1] != 0.0;
+      double pmf = o[1];
+      if (!done) {
+        pmf = presid <= o[0] ? fmax(a.eps, 0.25 * pmf) : fmin(1.0, 1.5 * pmf);
+        o[0] = presid * fmin(pmf, o[2] / rn);
+        o[1] = pmf;
+      }
+      o[3] = inner;
+      o[6] = done ? 1.0 : 0.0;
+      a.report[6] = o[6];
+      a.report[7] = o[0];
+    }
     a.g.ctrl[1] = col;
     a.g.ctrl[0] = 1;
   }
@@ -815,7 +865,7 @@ size_t small_cycle_lds_bytes(int n, int restart) {
   auto al = [](size_t b) { return (b + 15) / 16 * 16; };
   return al(16 * R1 * 3 * n) + al(16 * (size_t)n) + al(16 * (size_t)restart * R1) +
          al(32 * (size_t)restart) + 2 * al(16 * R1) + 2 * al(8 * R1) + al(8 * (size_t)restart) +
-         al(8 * (size_t)(kRedRuns + kRuns)) + al(8 * kPStride) + al(16);
+         al(8 * (size_t)(kRedRuns + kRuns)) + al(8 * kPStride) + al(16) + al(16);
 }
 
 size_t small_cycle_scratch_doubles(int n) {

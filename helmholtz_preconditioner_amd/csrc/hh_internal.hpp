@@ -250,7 +250,15 @@ struct SmallCycleArgs {
   unsigned seq;            // launch sequence number: the tags of this launch's granules
   unsigned* timeout_word;  // set when a wait gives up (zeroed at the start of a solve)
   unsigned long long* phase_ticks;  // optional [8]: workgroup 0's wall-clock ticks per phase
+  // optional (device) scipy's restart-loop state, so that several cycles can be queued behind
+  // each other: [0] ptol, [1] ptol_max_factor, [2] atol, [3] inner iterations so far,
+  // [4] maxiter, [5] legacy (maxiter caps inner iterations), [6] done.  A launch that finds
+  // `done` (or the timeout word) set returns at once with ctrl[0] = 2; otherwise it takes
+  // stop_col / ptol from here and, after its residual, takes scipy's decisions for the next
+  // cycle (report[6] = done, report[7] = the next ptol).  nullptr: stop_col / ptol as given.
+  double* outer;
 };
+constexpr int kOuterDoubles = 8;
 // columns of the small cycle's all-reduce rows: 2 K dot halves, |z|^2, |u_j|^2 (K <= kMaxProj)
 constexpr int kSmallCols = 2 * (kMaxProj + 1) + 2;
 constexpr int kSmallRounds = kMaxProj + 8;  // all-reduce rounds per launch (<= restart + 3)

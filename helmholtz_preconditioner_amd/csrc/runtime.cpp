@@ -88,6 +88,11 @@ constexpr int kRedStatus = 256;
 constexpr int kRedCtrl = 384;
 constexpr int kRedTimeout = 388;
 constexpr int kRedReport = 389;
+constexpr int kRedOuter = 400;  // [400, 408): the small cycle's restart-loop state (device only)
+// whole-cycle launches queued behind each other (one host sync per batch); each reports into its
+// own slot of the host mirror, status_h + (1 + i) kRedDoubles
+constexpr int kSmallBatch = 8;
+static_assert(kRedOuter >= kRedReport && kRedOuter + kOuterDoubles <= kRedDoubles, "red layout");
 }  // namespace
 
 namespace {
@@ -1008,7 +1013,8 @@ HH_API int hh_op_create(hh_ctx* c, int n, int b, double cconst, double eta, doub
     op->partials_cap = cap;
     op->red = dalloc<double>(kRedDoubles);
     HIPC(hipMemset(op->red, 0, kRedDoubles * sizeof(double)));
-    HIPC(hipHostMalloc(reinterpret_cast<void**>(&op->status_h), kRedDoubles * sizeof(double)));
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&op->status_h),
+                       (1 + kSmallBatch) * kRedDoubles * sizeof(double)));
     HIPC(hipDeviceSynchronize());
   } catch (...) {
     delete op;  // device memory of a failed create is reclaimed at process exit
@@ -1668,9 +1674,15 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
           "partials workspace too small for %d streaming blocks", blocks);
   double st[8];
 
-  // red[4] = |b|^2 (= |r|^2 while x0 == 0), red[2] = |x0|^2
+  // red[4] = |b|^2 (= |r|^2 while x0 == 0), red[2] = |x0|^2; and (one host sync for all of
+  // them) V[0] = M b, red[5] = |M b|^2 -- except for the as-is sweep, whose M needs b first
   norm2(op, b, 4);
   norm2(op, x, 2);
+  const bool mb_early = op->pkind != HH_PREC_SWEEP_REF;
+  if (mb_early) {
+    apply_M(op, b, V);
+    norm2(op, V, 5);
+  }
   read_dev(op, op->red, st, 6);
   const double bnrm2 = std::sqrt(st[4]);
   const bool x_any = st[2] > 0.0;
@@ -1706,10 +1718,12 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     op->sw_const = c;
   }
   // Mb_nrm2 = ||psolve(b)||; V[0] = M b, red[5] = |M b|^2 (= |M r|^2 while x0 == 0)
-  apply_M(op, b, V);
-  norm2(op, V, 5);
-  read_dev(op, op->red + 5, st, 1);
-  const double Mb_nrm2 = std::sqrt(st[0]);
+  if (!mb_early) {
+    apply_M(op, b, V);
+    norm2(op, V, 5);
+    read_dev(op, op->red + 5, st + 5, 1);
+  }
+  const double Mb_nrm2 = std::sqrt(st[5]);
   double ptol_max_factor = 1.0;
   double ptol = Mb_nrm2 * std::min(ptol_max_factor, atol / bnrm2);
   double presid = 0.0, rnorm = 0.0;
@@ -1735,18 +1749,149 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     }
   }
 
-  for (long iteration = 0; iteration < maxiter; ++iteration) {
-    if (iteration == 0) {
-      if (x_any) residual(op, b, x, V, 4);  // V[0] = M (b - A x0); red[4..5]
-      read_dev(op, op->red + 4, st, 1);
-      if (std::sqrt(st[0]) < atol) {
-        finish(0, 0, std::sqrt(st[0]));
-        return HH_OK;
+  double r0 = bnrm2;  // (x0 = 0: r = b)
+  if (x_any) {
+    residual(op, b, x, V, 4);  // V[0] = M (b - A x0); red[4..5]
+    read_dev(op, op->red + 4, st, 1);
+    r0 = std::sqrt(st[0]);
+  }
+  if (r0 < atol) {  // (scipy's test before the first cycle)
+    finish(0, 0, r0);
+    return HH_OK;
+  }
+  // replays one finished cycle's per-iteration statuses to the host callbacks (in order)
+  auto replay = [&](const double* sth, int col) {
+    double rel[kMaxProj];
+    const long first = inner + 1;
+    for (int k = 0; k <= col; ++k) {
+      const double pr = sth[4 * k];
+      inner += 1;
+      rel[k] = pr / bnrm2;
+      if (hist && inner - 1 < hist_cap) hist[inner - 1] = rel[k];
+      if (cb && cb(user, inner, rel[k]) != 0) {
+        finish(inner, -1, 0.0);
+        fail(HH_ERR_ABORTED, "gmres stopped by the per-iteration callback at iteration %ld", inner);
       }
     }
+    if (op->hist_cb) {
+      const int r = op->hist_cb(op->hist_user, first, col + 1, rel);
+      if (r != 0) {
+        const long at = first - 1 + (r >= 1 && r <= col + 1 ? r : col + 1);
+        finish(at, -1, 0.0);
+        fail(HH_ERR_ABORTED, "gmres stopped by the history callback at iteration %ld", at);
+      }
+    }
+  };
+  if (small) {
+    // Small grids: whole-cycle launches (gmres_small.hip), up to kSmallBatch queued behind each
+    // other -- scipy's restart-loop decisions are taken on the device from the state below
+    // (bitwise the host's expressions), so a cycle starts a kernel boundary after the previous
+    // one instead of a host round trip.  One sync per batch; the host then replays each cycle's
+    // report: callbacks in order, legacy maxiter, the x callback (which limits a batch to one
+    // cycle, x being observed after every cycle).  A launch queued behind a finished solve
+    // returns at once (ctrl = 2).  An exception raised by a callback ends the solve after the
+    // batch (x is then up to kSmallBatch - 1 cycles further; the Python shim returns no x then).
+    double* outer_h = op->status_h + kRedOuter;  // (pinned staging for the upload)
+    outer_h[0] = ptol;
+    outer_h[1] = ptol_max_factor;
+    outer_h[2] = atol;
+    outer_h[3] = 0.0;
+    outer_h[4] = (double)maxiter;
+    outer_h[5] = legacy ? 1.0 : 0.0;
+    outer_h[6] = 0.0;
+    outer_h[7] = 0.0;
+    double* outer = op->red + kRedOuter;
+    HIPC(hipMemcpyAsync(outer, outer_h, kOuterDoubles * sizeof(double), hipMemcpyHostToDevice, s));
+    const int cap = op->cycle_cb ? 1 : kSmallBatch;
+    const Slab& sl = op->slabs[0];
+    long iteration = 0;
+    bool done = false;
+    while (!done && iteration < maxiter) {
+      // (legacy: maxiter caps inner iterations, so no more cycles than those left can run)
+      const long cycles_left =
+          legacy ? (maxiter - inner + restart - 1) / restart : maxiter - iteration;
+      const int P = (int)std::min<long>(cap, cycles_left);
+      for (int i = 0; i < P; ++i) {
+        double* rep = op->status_h + (size_t)(1 + i) * kRedDoubles;
+        SmallCycleArgs sa{};
+        sa.n = op->n;
+        sa.restart = restart;
+        sa.stop_col = restart - 1;  // (from `outer`)
+        sa.tab_i = op->tab_i;
+        sa.tab_j = sl.tab_j;
+        sa.invc2 = op->const_c ? nullptr : sl.invc2;
+        sa.invc2_const = op->invc2_const;
+        sa.v0 = V;
+        sa.mnorm2 = op->red + mnorm_slot(op, 4);
+        sa.b = b;
+        sa.x = x;
+        sa.red = op->red;
+        // the cycle's report goes straight to its slot of the pinned host mirror (same layout
+        // as red): no copy after the launch; ctrl[0] = 1 marks it complete
+        sa.report = rep;
+        sa.g = g;
+        sa.g.status_it = rep + kRedStatus;
+        sa.g.ctrl = reinterpret_cast<int*>(rep + kRedCtrl);
+        sa.g.ctrl[0] = 0;
+        sa.eps = eps;
+        sa.ptol = ptol;  // (from `outer`)
+        sa.zbuf = reinterpret_cast<unsigned long long*>(op->small_scr);
+        sa.xbuf = sa.zbuf + 8 * (size_t)op->n * op->n;
+        sa.part = sa.xbuf + 4 * (size_t)op->n * op->n;
+        sa.sums = sa.part + 2 * (size_t)op->n * 2 * kSmallCols;
+        sa.verdict = sa.sums + (size_t)kSmallRounds * 2 * kSmallCols;
+        sa.ycoef = sa.verdict + 2 * kMaxProj;
+        sa.seq = (++op->small_seq) & 0xffffffu;
+        if (sa.seq == 0) sa.seq = op->small_seq = 1;  // (tag 0 is the zeroed scratch)
+        sa.timeout_word = small_timeout;
+        sa.phase_ticks = op->small_ticks;
+        sa.outer = outer;
+        launch_small_cycle(sa, op->const_c, op->pkind == HH_PREC_JACOBI, s);
+        HIPC(hipGetLastError());
+      }
+      HIPC(hipStreamSynchronize(s));
+      for (int i = 0; i < P && !done; ++i) {
+        const double* rep = op->status_h + (size_t)(1 + i) * kRedDoubles;
+        int ctl[2];
+        std::memcpy(ctl, rep + kRedCtrl, 2 * sizeof(int));
+        if (ctl[0] != 1) {
+          double w = 0.0;
+          read_dev(op, op->red + kRedTimeout, &w, 1);
+          unsigned tmo = 0;
+          std::memcpy(&tmo, &w, sizeof(unsigned));
+          REQUIRE(tmo == 0, "small-grid GMRES cycle: a grid-wide wait timed out (workgroups not "
+                            "co-resident?); hh_op_set_small_cycle(op, 0) selects the regular cycle");
+          fail(HH_ERR_STATE, ctl[0] == 2 ? "small-grid GMRES: a queued cycle found the solve "
+                                           "finished before the host did"
+                                         : "small-grid GMRES cycle ended without its report");
+        }
+        const int col = ctl[1];
+        REQUIRE(col >= 0 && col < restart, "GMRES cycle state corrupt (last column %d)", col);
+        const double* sth = rep + kRedStatus;
+        replay(sth, col);
+        presid = sth[4 * col];
+        op->stats.restarts++;
+        ++iteration;
+        rnorm = std::sqrt(rep[4]);
+        if (legacy && inner == maxiter) {
+          finish(inner, rnorm <= atol ? 0 : (int)std::min<long>(maxiter, 0x7fffffff), rnorm);
+          return HH_OK;
+        }
+        if (op->cycle_cb && op->cycle_cb(op->cycle_user, op->stats.restarts) != 0) {
+          finish(inner, -1, rnorm);
+          fail(HH_ERR_ABORTED, "gmres stopped by the cycle callback after cycle %ld",
+               op->stats.restarts);
+        }
+        done = rep[6] != 0.0;  // (rnorm <= atol, breakdown, or legacy maxiter)
+      }
+    }
+    finish(inner, rnorm <= atol ? 0 : (int)std::min<long>(maxiter, 0x7fffffff), rnorm);
+    return HH_OK;
+  }
+
+  for (long iteration = 0; iteration < maxiter; ++iteration) {
     // v[0] = psolve(r) / ||psolve(r)||, S[0] = ||psolve(r)|| (lazy scale); clears the stop flag
-    // (the whole-cycle kernel scales V[0] itself)
-    if (!small) launch_gmres_start(g, op->red, 4, mnorm_slot(op, 4), s);
+    launch_gmres_start(g, op->red, 4, mnorm_slot(op, 4), s);
     // The whole cycle is queued at once: the column kernel evaluates scipy's inner exit test
     // (presid <= ptol, breakdown, legacy maxiter) and raises the stop flag, after which the
     // kernels still queued in this cycle return immediately.  One host sync per cycle.
@@ -1755,44 +1900,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     const long left = legacy ? maxiter - inner : (long)restart;
     const int stop_col = (int)std::min<long>(restart - 1, left - 1);
     op->stop_flag = g.ctrl;
-    if (small) {
-      const Slab& sl = op->slabs[0];
-      SmallCycleArgs sa{};
-      sa.n = op->n;
-      sa.restart = restart;
-      sa.stop_col = stop_col;
-      sa.tab_i = op->tab_i;
-      sa.tab_j = sl.tab_j;
-      sa.invc2 = op->const_c ? nullptr : sl.invc2;
-      sa.invc2_const = op->invc2_const;
-      sa.v0 = V;
-      sa.mnorm2 = op->red + mnorm_slot(op, 4);
-      sa.b = b;
-      sa.x = x;
-      sa.red = op->red;
-      // the cycle's report goes straight to the pinned host mirror (same layout as red): no
-      // copy after the launch; ctrl[0] = 1 marks it complete
-      sa.report = op->status_h;
-      sa.g = g;
-      sa.g.status_it = op->status_h + kRedStatus;
-      sa.g.ctrl = reinterpret_cast<int*>(op->status_h + kRedCtrl);
-      sa.g.ctrl[0] = 0;
-      sa.eps = eps;
-      sa.ptol = ptol;
-      sa.zbuf = reinterpret_cast<unsigned long long*>(op->small_scr);
-      sa.xbuf = sa.zbuf + 8 * (size_t)op->n * op->n;
-      sa.part = sa.xbuf + 4 * (size_t)op->n * op->n;
-      sa.sums = sa.part + 2 * (size_t)op->n * 2 * kSmallCols;
-      sa.verdict = sa.sums + (size_t)kSmallRounds * 2 * kSmallCols;
-      sa.ycoef = sa.verdict + 2 * kMaxProj;
-      sa.seq = (++op->small_seq) & 0xffffffu;
-      if (sa.seq == 0) sa.seq = op->small_seq = 1;  // (tag 0 is the zeroed scratch)
-      sa.timeout_word = small_timeout;
-      sa.phase_ticks = op->small_ticks;
-      launch_small_cycle(sa, op->const_c, op->pkind == HH_PREC_JACOBI, s);
-      HIPC(hipGetLastError());
-    }
-    for (int c2 = 0; c2 <= stop_col && lagged && !small; ++c2) {
+    for (int c2 = 0; c2 <= stop_col && lagged; ++c2) {
       // ONE allreduce per inner iteration (lagged normalisation, gmres_lag_kernel): the norm of
       // the vector the previous update wrote (u_c2, its partials kept in npart) travels with
       // this iteration's raw dots; the Hessenberg subdiagonal of column c2-1 is completed from
@@ -1817,7 +1925,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         launch_gmres_lag(g, c2 + 1, nullptr, op->red + 8, true, eps, ptol, stop_col, s);
       }
     }
-    for (int c2 = 0; c2 <= stop_col && !lagged && !small; ++c2) {
+    for (int c2 = 0; c2 <= stop_col && !lagged; ++c2) {
       double2* vcol = V + (size_t)c2 * ldv;
       double2* w = V + (size_t)(c2 + 1) * ldv;
       const int* stp = g.ctrl;
@@ -1876,18 +1984,14 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       HIPC(hipGetLastError());
     }
     op->stop_flag = nullptr;  // (the SolveScope also clears it if anything above throws)
-    // one sync: per-iteration statuses + the last column executed (the whole-cycle kernel has
-    // already updated x: its true residual is queued behind it and read in the same sync)
-    // (the whole-cycle kernel has also computed the next cycle's residual, V[0] and norms,
-    // and written its report to the host mirror itself)
-    if (!small)
-      HIPC(hipMemcpyAsync(op->status_h, op->red, kRedReport * sizeof(double),
-                          hipMemcpyDeviceToHost, s));
+    // one sync: per-iteration statuses + the last column executed
+    HIPC(hipMemcpyAsync(op->status_h, op->red, kRedReport * sizeof(double), hipMemcpyDeviceToHost,
+                        s));
     HIPC(hipStreamSynchronize(s));
     const double* sth = op->status_h + kRedStatus;
     int ctl[2];
     std::memcpy(ctl, op->status_h + kRedCtrl, 2 * sizeof(int));
-    if (!small) {  // (the persistent sweep chain's wait bound)
+    {  // (the persistent sweep chain's wait bound)
       unsigned tmo = 0;
       std::memcpy(&tmo, op->status_h + kRedTimeout, sizeof(unsigned));
       if (tmo != 0) {
@@ -1897,48 +2001,16 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
                            "per GEMV");
       }
     }
-    if (small && ctl[0] != 1) {
-      double w = 0.0;
-      read_dev(op, op->red + kRedTimeout, &w, 1);
-      unsigned tmo = 0;
-      std::memcpy(&tmo, &w, sizeof(unsigned));
-      REQUIRE(tmo == 0, "small-grid GMRES cycle: a grid-wide wait timed out (workgroups not "
-                        "co-resident?); hh_op_set_small_cycle(op, 0) selects the regular cycle");
-      fail(HH_ERR_STATE, "small-grid GMRES cycle ended without its report");
-    }
     col = ctl[1];
     REQUIRE(col >= 0 && col <= stop_col, "GMRES cycle state corrupt (last column %d)", col);
-    double rel[kMaxProj];
-    const long first = inner + 1;
-    for (int k = 0; k <= col; ++k) {
-      const double pr = sth[4 * k];
-      inner += 1;
-      rel[k] = pr / bnrm2;
-      if (hist && inner - 1 < hist_cap) hist[inner - 1] = rel[k];
-      if (cb && cb(user, inner, rel[k]) != 0) {
-        finish(inner, -1, 0.0);
-        fail(HH_ERR_ABORTED, "gmres stopped by the per-iteration callback at iteration %ld", inner);
-      }
-    }
-    if (op->hist_cb) {
-      const int r = op->hist_cb(op->hist_user, first, col + 1, rel);
-      if (r != 0) {
-        const long at = first - 1 + (r >= 1 && r <= col + 1 ? r : col + 1);
-        finish(at, -1, 0.0);
-        fail(HH_ERR_ABORTED, "gmres stopped by the history callback at iteration %ld", at);
-      }
-    }
+    replay(sth, col);
     presid = sth[4 * col];
     breakdown = sth[4 * col + 1] != 0.0;
     op->stats.restarts++;
-    if (!small) {  // (the whole-cycle kernel has solved and updated x itself)
-      launch_gmres_solve(g, col, s);
-      launch_xupdate(V, ldv, col + 1, g.ycoef, x, L, blocks, s);
-      residual(op, b, x, V, 4);  // r = b - A x; V[0] = M r for the next cycle
-      read_dev(op, op->red + 4, st, 1);
-    } else {
-      st[0] = op->status_h[4];  // (the residual queued behind the cycle kernel)
-    }
+    launch_gmres_solve(g, col, s);
+    launch_xupdate(V, ldv, col + 1, g.ycoef, x, L, blocks, s);
+    residual(op, b, x, V, 4);  // r = b - A x; V[0] = M r for the next cycle
+    read_dev(op, op->red + 4, st, 1);
     rnorm = std::sqrt(st[0]);
     if (legacy && inner == maxiter) {
       finish(inner, rnorm <= atol ? 0 : (int)std::min<long>(maxiter, 0x7fffffff), rnorm);

@@ -101,3 +101,51 @@ def test_small_cycle_converging_and_x0(ctx):
     assert info5 == infor0 and len(hist5) == len(histr0)
     assert np.max(np.abs(hist5 - histr0) / histr0) < TOL
     assert relerr(x5, xr0) < TOL
+
+
+@pytest.mark.parametrize("case", ["cycles", "converge", "xcb"])
+def test_small_cycle_queued_cycles(ctx, case):
+    """Whole-cycle launches are queued several at a time, scipy's restart-loop decisions taken
+    on the device (runtime.cpp kSmallBatch): maxiter counting restart cycles across batches, a
+    solve that converges inside a batch (the launches queued behind it return at once, and the
+    next solve starts clean), and the x callback (one cycle per batch) -- all as the regular
+    cycle runs them."""
+    n, b, C, wn = 48, 6, 61.0, 2.0
+    om, h, eta = O.problem_params(n, b, wn, 2.0)
+    A = H.build_A_matrix(b, C, eta, om, h, n, medium("c2", n), context=ctx)
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    kw = {"cycles": dict(rtol=1e-12, restart=5, maxiter=9),
+          "converge": dict(rtol=1e-4, restart=10, maxiter=400, M="jacobi"),
+          "xcb": dict(rtol=1e-4, restart=10, maxiter=400, M="jacobi")}[case]
+    out = []
+    for mode in ("on", "off"):
+        A.small_cycle(mode)
+        calls = []
+        if case == "xcb":
+            x, info = H.gmres(A, f, callback=lambda xk: calls.append(np.array(xk)),
+                              callback_type="x", **kw)
+            hist = None
+        else:
+            x, info, hist = H.gmres(A, f, callback=lambda r: None, callback_type="pr_norm",
+                                    return_history=True, **kw)
+        out.append((x, info, hist, calls))
+        if case == "converge":  # a second solve after the skipped launches: same again
+            x2, info2, hist2 = H.gmres(A, f, callback=lambda r: None, callback_type="pr_norm",
+                                       return_history=True, **kw)
+            assert info2 == info and np.array_equal(hist2, hist) and np.array_equal(x2, x)
+    A.small_cycle("auto")
+    (x1, i1, h1, c1), (x2, i2, h2, c2) = out
+    assert i1 == i2
+    if case == "cycles":
+        assert i1 == 9 and len(h1) == len(h2) == 45
+    if case == "converge":
+        assert i1 == 0 and len(h1) == len(h2) and len(h1) > 10
+    if h1 is not None:
+        # (hundreds of iterations in two summation orders: rounding grows past 1e-9 -- the
+        # 1e-6 contract of DESIGN 6)
+        assert np.all(np.abs(h1 - h2) <= 1e-6 * np.abs(h2))
+    if case == "xcb":
+        assert len(c1) == len(c2) > 4
+        for u, v in zip(c1, c2):
+            assert np.linalg.norm(u - v) <= 1e-6 * np.linalg.norm(v)
+    assert np.linalg.norm(x1 - x2) <= 1e-6 * np.linalg.norm(x2)

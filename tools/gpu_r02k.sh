@@ -17,7 +17,7 @@ step() {  # step NAME SECONDS CMD...
   return 0
 }
 PYT="python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu"
-step t_small 300 $PYT tests/test_gpu_small_cycle.py tests/test_gpu_errors.py tests/test_gpu_krylov_modes.py -x
+step t_small 600 $PYT tests/test_gpu_small_cycle.py tests/test_gpu_errors.py tests/test_gpu_krylov_modes.py tests/test_gpu_gmres.py tests/test_gpu_driver.py tests/test_gpu_sweep.py tests/test_gpu_variants.py tests/test_gpu_configs.py -x
 step prof_small 120 python tools/prof_small_cycle.py
 step bench_c1 200 python bench.py --config 1 --no-cpu-baseline --steps 200
 step rocprof_c1 200 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c1" -o run --output-format csv -- python3 tools/prof_small_cycle.py --iters 100
