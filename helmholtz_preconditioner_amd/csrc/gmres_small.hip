@@ -30,6 +30,9 @@
 #include "hh_complex.hpp"
 #include "hh_error.hpp"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace hh {
 namespace {
 
@@ -40,7 +43,12 @@ __device__ __forceinline__ double2 csel(bool c, double2 a, double2 b) {
   return make_double2(c ? a.x : b.x, c ? a.y : b.y);
 }
 
-constexpr int kSmallThreads = 256;    // block size cap for the grid's rows (n <= 256)
+constexpr int kSmallThreads = 256;    // grid rows at most (n <= 256)
+// Block size: P = min(4, 512 / npad) copies of the row's npad threads.  The stencil, x update
+// and residual need one thread per column; with P >= 3 the basis update gives each of the three
+// rows (ghost, own, ghost) a thread group of its own and the partial sums get more segments,
+// so all four SIMDs of the CU work instead of one or two waves (npad = 128: 2 waves).
+constexpr int kSmallBlock = 512;
 constexpr int kPStride = kSmallCols;  // partial-sum columns (global layout)
 constexpr unsigned kSpinLimit = 1u << 22;  // ~1 s of polling: a barrier wait is microseconds
 
@@ -69,6 +77,9 @@ struct Shared {  // LDS layout (carved from dynamic shared memory; see small_cyc
   li* ctl;   // [4]: 0 stop, 1 last column, 2 abort
   l1* gv;    // [2]: presid and breakdown of the last finished column (Givens workgroup; then
              // workgroup 0, for the restart loop's decisions)
+  l1* st;    // [R][4]: the columns' statuses (Givens workgroup), copied to the host-mapped
+             // status_it only after y is published: a store to host memory holds the storing
+             // wave's next vmcnt wait for a PCIe round trip (~3 us per column on the books)
 };
 
 // All-reduce of `cols` doubles per workgroup with NO counter and NO flag: every value travels
@@ -191,6 +202,13 @@ __device__ bool allreduce_rows(const ArArgs& ar, int par, unsigned epoch, int co
   return true;
 }
 
+// fixed-order wave sum (xor butterfly; addition commutes, so every lane gets the same bits)
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = kWave / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
 // LAPACK zlartg main branch (krylov.hip), by value: each branch yields all three results (no
 // output pointers -- a branch-selected store target would become a scratch slot)
 struct Rot {
@@ -223,128 +241,173 @@ __device__ __forceinline__ Rot zlartg_s(double2 f, double2 g) {
   return o;
 }
 
-// lane 0: complete column `col` with its subdiagonal h1 (krylov.hip gmres_finish_column); the
-// status of the column goes to status_it (workgroup 0 only).  Returns true when the cycle stops.
+// lane k's double, on every lane
+__device__ __forceinline__ double rlane(double v, int k) {
+  const long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffff), k);
+  const int hi = __builtin_amdgcn_readlane((int)(u >> 32), k);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double2 rlane2(double2 v, int k) {
+  return make_double2(rlane(v.x, k), rlane(v.y, k));
+}
+
+// The Givens workgroup's wave: complete column `col` with its subdiagonal h1 (krylov.hip
+// gmres_finish_column) -- every lane computes the same values, lane 0 stores them.  Lane k
+// holds rotation k and entry k of the column, so the chain of previous rotations reads its
+// operands by readlane instead of waiting on an LDS round trip per step.  The status of the
+// column goes to sh.st.  Returns true (on every lane) when the cycle stops.
 __device__ bool finish_column(const Shared& sh, const SmallCycleArgs& a, int col, double h1,
                               double inv_sigma_next, double ptol, int stop_col) {
   const int R1 = a.restart + 1;
+  const int lane = threadIdx.x;
+  const bool l0 = lane == 0;
   l2* h = sh.H + (size_t)col * R1;
   const double h0 = sh.h0s[col];
-  h[col + 1] = make_double2(h1, 0.0);
+  double2 hsub = make_double2(h1, 0.0);
   double brk = 0.0;
   if (h1 <= a.eps * h0) {
-    h[col + 1] = make_double2(0.0, 0.0);
+    hsub = make_double2(0.0, 0.0);
     brk = 1.0;
-  } else {
+  } else if (l0) {
     sh.vs[col + 1] = inv_sigma_next;
   }
-  // the previous rotations, in order; the running entry is carried in registers and the next
-  // step's operands are loaded one step ahead (the chain never waits on an LDS round trip)
-  if (col > 0) {
-    double2 n0 = h[0];
-    double c = sh.Gr[0].x;
-    double2 s = sh.Gr[1], n1 = h[1];
-    for (int k = 0; k < col; ++k) {
-      const int kn = min(k + 1, col - 1);
-      const double cn = sh.Gr[2 * kn].x;
-      const double2 sn = sh.Gr[2 * kn + 1], n1n = h[kn + 1];
-      h[k] = cadd(cscale(n0, c), cmul(s, n1));
-      n0 = cadd(cmul(make_double2(-s.x, s.y), n0), cscale(n1, c));
-      c = cn;
-      s = sn;
-      n1 = n1n;
-    }
-    h[col] = n0;
+  double ck = 0.0;
+  double2 sk = make_double2(0.0, 0.0), hk = make_double2(0.0, 0.0);
+  if (lane < col) {
+    ck = sh.Gr[2 * lane].x;
+    sk = sh.Gr[2 * lane + 1];
   }
-  const Rot rot = zlartg_s(h[col], h[col + 1]);
+  if (lane <= col) hk = h[lane];
+  // the previous rotations, in order, the running entry carried
+  double2 n0 = rlane2(hk, 0);
+  for (int k = 0; k < col; ++k) {
+    const double c = rlane(ck, k);
+    const double2 s = rlane2(sk, k), n1 = rlane2(hk, k + 1);
+    const double2 hn = cadd(cscale(n0, c), cmul(s, n1));
+    if (l0) h[k] = hn;
+    n0 = cadd(cmul(make_double2(-s.x, s.y), n0), cscale(n1, c));
+  }
+  const Rot rot = zlartg_s(n0, hsub);
   const double c = rot.c;
   const double2 s = rot.s;
-  sh.Gr[2 * col] = make_double2(c, 0.0);
-  sh.Gr[2 * col + 1] = s;
-  h[col] = rot.r;
-  h[col + 1] = make_double2(0.0, 0.0);
   const double2 Sc = sh.S[col];
   const double2 tmp = cmul(make_double2(-s.x, s.y), Sc);
-  sh.S[col] = cscale(Sc, c);
-  sh.S[col + 1] = tmp;
   const double presid = hypot(tmp.x, tmp.y);
-  {
-    double* st = a.g.status_it + 4 * col;
+  if (l0) {
+    sh.Gr[2 * col] = make_double2(c, 0.0);
+    sh.Gr[2 * col + 1] = s;
+    h[col] = rot.r;
+    h[col + 1] = make_double2(0.0, 0.0);
+    sh.S[col] = cscale(Sc, c);
+    sh.S[col + 1] = tmp;
+    l1* st = sh.st + 4 * col;
     st[0] = presid;
     st[1] = brk;
     st[2] = h0;
     st[3] = h1;
+    sh.ctl[1] = col;
+    sh.gv[0] = presid;
+    sh.gv[1] = brk;
   }
-  sh.ctl[1] = col;
-  sh.gv[0] = presid;
-  sh.gv[1] = brk;
   return presid <= ptol || brk != 0.0 || col >= stop_col;
 }
 
 
-// Extra workgroup n ("Givens workgroup", one thread): follows the rounds' sums at its own
+
+// Extra workgroup n ("Givens workgroup", its first wave): follows the rounds' sums at its own
 // pace and keeps the Hessenberg books -- column j from the round-j sums, column j-1 completed
 // with |u_j| (krylov.hip gmres_lag_kernel / gmres_finish_column), rotations, presid, scipy's
 // exit tests -- so none of it sits on the row workgroups' critical path.  Per column it
 // publishes a verdict granule (0 continue / 1 stop), at the end the column the cycle solved for
-// and y_k / sigma_k.  Returns false on timeout.
+// and y_k / sigma_k.  A round's 2K + 2 sums are fetched by one lane each (one load latency per
+// round, not one per column: the books then keep up with the rows, and the cycle's tail waits
+// on one round trip); lane 0 does the arithmetic.  Returns false on timeout (wave-uniform).
 __device__ bool givens_role(const Shared& sh, const SmallCycleArgs& a, int stop_col, double ptol) {
   const int R1 = a.restart + 1;
-  const unsigned long long* sums = a.sums;
-  auto sum_at = [&](unsigned epoch, int c, double* v) {
-    return ld_gran(sums + (size_t)epoch * 2 * kPStride + 2 * c, gran_tag(a.seq, epoch), v);
+  const int lane = threadIdx.x;
+  const bool l0 = lane == 0;
+  // optional span timing (lane 0; slots 12 sum waits, 13 per-round work, 14 last column + solve)
+  const bool prof = a.phase_ticks != nullptr && l0;
+  unsigned long long tp = prof ? wall_clock64() : 0;
+  auto span = [&](int slot) {
+    if (prof) {
+      const unsigned long long now = wall_clock64();
+      a.phase_ticks[slot] += now - tp;
+      tp = now;
+    }
   };
-  const double mn = sqrt(*a.mnorm2);
-  sh.vs[0] = 1.0 / mn;
-  sh.ss[0] = 1.0 / mn;
-  for (int k = 0; k < R1; ++k) sh.S[k] = make_double2(k == 0 ? mn : 0.0, 0.0);
+  auto fetch = [&](unsigned epoch, int cols) {  // sums of round `epoch` into sh.sum[0 .. cols)
+    span(13);
+    bool ok = true;
+    if (lane < cols) {
+      double v = 0.0;
+      ok = ld_gran(a.sums + (size_t)epoch * 2 * kPStride + 2 * lane, gran_tag(a.seq, epoch), &v);
+      sh.sum[lane] = v;
+    }
+    const bool all = __ballot(!ok) == 0;
+    span(12);
+    return all;
+  };
+  if (l0) {
+    const double mn = sqrt(*a.mnorm2);
+    sh.vs[0] = 1.0 / mn;
+    sh.ss[0] = 1.0 / mn;
+    for (int k = 0; k < R1; ++k) sh.S[k] = make_double2(k == 0 ? mn : 0.0, 0.0);
+  }
   int col = -1;
   for (int j = 0; j <= stop_col && col < 0; ++j) {
     const int K = j + 1;
     const unsigned epoch = j + 1;
-    double w2, u2 = 0.0;
-    if (!sum_at(epoch, 2 * K, &w2)) return false;
-    if (j >= 1 && !sum_at(epoch, 2 * K + 1, &u2)) return false;
+    if (!fetch(epoch, 2 * K + 2)) return false;  // dots, |z|^2, |u_j|^2
+    // column j of H, entry k on lane k, and the Pythagorean terms (the row workgroups'
+    // expressions; `rest` summed in their k order)
+    const double w2 = sh.sum[2 * K], u2 = sh.sum[2 * K + 1];
     const double vj = j >= 1 ? 1.0 / sqrt(u2) : sh.vs[0];
-    // column j of H and the Pythagorean terms (the row workgroups' expressions and order)
-    double rest = w2;
-    for (int k = 0; k <= j; ++k) {
-      double dx, dy;
-      if (!sum_at(epoch, 2 * k, &dx) || !sum_at(epoch, 2 * k + 1, &dy)) return false;
-      const double2 d = make_double2(dx, dy);
-      const double vk = k == j ? vj : sh.vs[k];
-      sh.H[(size_t)j * R1 + k] = cscale(cscale(d, vk), vj / sh.ss[j]);
-      rest -= cabs2(d) * vk * vk;
+    double tv = 0.0;
+    if (lane <= j) {
+      const double2 d = make_double2(sh.sum[2 * lane], sh.sum[2 * lane + 1]);
+      const double vk = lane == j ? vj : sh.vs[lane];
+      sh.H[(size_t)j * R1 + lane] = cscale(cscale(d, vk), vj / sh.ss[j]);
+      tv = cabs2(d) * vk * vk;
     }
+    double rest = w2;
+    for (int k = 0; k <= j; ++k) rest -= rlane(tv, k);
+    bool stop = false;
     if (j >= 1) {
       const int c = j - 1;
-      const bool stop =
-          finish_column(sh, a, c, (1.0 / vj) * sh.vs[c] / sh.ss[c], vj, ptol, stop_col);
-      st_gran(a.verdict + 2 * c, gran_tag(a.seq, c + 1), stop ? 1.0 : 0.0);
-      if (stop) {
-        col = c;
-        break;
+      stop = finish_column(sh, a, c, (1.0 / vj) * sh.vs[c] / sh.ss[c], vj, ptol, stop_col);
+      if (l0) st_gran(a.verdict + 2 * c, gran_tag(a.seq, c + 1), stop ? 1.0 : 0.0);
+      if (stop) col = c;
+    }
+    if (l0) {
+      if (!stop) {
+        sh.vs[j] = vj;
+        sh.h0s[j] = sqrt(w2) * (vj / sh.ss[j]);
+        sh.ss[j + 1] = 1.0 / sqrt(fmax(rest, fmax(w2 * 1e-28, 1e-300)));
       }
     }
-    sh.vs[j] = vj;
-    sh.h0s[j] = sqrt(w2) * (vj / sh.ss[j]);
-    sh.ss[j + 1] = 1.0 / sqrt(fmax(rest, fmax(w2 * 1e-28, 1e-300)));
   }
   if (col < 0) {  // ran to stop_col: the last column needs |u_{stop_col+1}| (one more round)
-    double u2;
-    if (!sum_at(stop_col + 2, 0, &u2)) return false;
-    const double sg = sqrt(u2);
+    if (!fetch(stop_col + 2, 1)) return false;
     col = stop_col;
+    const double sg = sqrt(sh.sum[0]);
     finish_column(sh, a, col, sg * sh.vs[col] / sh.ss[col], 1.0 / sg, ptol, stop_col);
   }
-  sh.ctl[1] = col;
+  if (l0) sh.ctl[1] = col;
+  span(14);
   return true;
+}
+__device__ __forceinline__ void givens_tail_tick(const SmallCycleArgs& a, unsigned long long t0) {
+  if (a.phase_ticks != nullptr && threadIdx.x == 0) a.phase_ticks[14] += wall_clock64() - t0;
 }
 
 // The triangular solve (krylov.hip gmres_solve_kernel) on the Givens workgroup's first wave,
-// lane m holding y_m: for k = col .. 0, y_k /= H_kk (every lane, the same value), then lanes
-// m < k subtract y_k H_km in parallel -- the sequential solve's operations in its order, one
-// column step per iteration instead of one entry.  y_k / sigma_k published for the x update.
+// lane m holding y_m: for k = col .. 0, y_k *= 1 / H_kk (the reciprocals formed on all lanes at
+// once, Smith's division: one division latency instead of one per step), then lanes m < k
+// subtract y_k H_km in parallel (the next step's H entries loaded a step ahead) -- the
+// sequential solve's order, one column step per iteration instead of one entry.
+// y_k / sigma_k published for the x update.
 __device__ void solve_and_publish(const Shared& sh, const SmallCycleArgs& a) {
   const int R1 = a.restart + 1;
   const int lane = threadIdx.x;
@@ -354,19 +417,18 @@ __device__ void solve_and_publish(const Shared& sh, const SmallCycleArgs& a) {
   double2 y = make_double2(0.0, 0.0);
   if (lane <= col) y = sh.S[lane];
   if (lane == col && hcc.x == 0.0 && hcc.y == 0.0) y = make_double2(0.0, 0.0);
-  auto rl = [](double v, int k) {
-    const long long u = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffff), k);
-    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), k);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-  };
+  double2 rd = make_double2(0.0, 0.0);
+  if (lane <= col) rd = cdiv_smith(make_double2(1.0, 0.0), Hc(lane, lane));
+  double2 hk = Hc(col, min(lane, col));
   for (int k = col; k >= 0; --k) {
-    double2 yk = make_double2(rl(y.x, k), rl(y.y, k));
+    const double2 hn = Hc(max(k - 1, 0), min(lane, max(k - 1, 0)));  // (next step's, ahead)
+    double2 yk = make_double2(rlane(y.x, k), rlane(y.y, k));
     if (yk.x != 0.0 || yk.y != 0.0) {
-      yk = cdiv_smith(yk, Hc(k, k));
+      yk = cmul(yk, make_double2(rlane(rd.x, k), rlane(rd.y, k)));
       if (lane == k) y = yk;
-      if (lane < k) y = csub(y, cmul(yk, Hc(k, min(lane, k))));
+      if (lane < k) y = csub(y, cmul(yk, hk));
     }
+    hk = hn;
   }
   const unsigned ytag = gran_tag(a.seq, 0xff);
   if (lane <= col) {
@@ -379,16 +441,28 @@ __device__ void solve_and_publish(const Shared& sh, const SmallCycleArgs& a) {
     st_gran(a.ycoef + 4 * kMaxProj, ytag, (double)(col + (sh.gv[1] != 0.0 ? 64 : 0)));
     st_gran(a.ycoef + 4 * kMaxProj + 2, ytag, sh.gv[0]);
   }
+  // the columns' statuses to the host-mapped report, off the critical path now
+  if (lane <= col) {
+    double* st = a.g.status_it + 4 * lane;
+    for (int q = 0; q < 4; ++q) st[q] = sh.st[4 * lane + q];
+  }
 }
 
 template <bool CONSTC, bool JAC>
-__global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kernel(SmallCycleArgs a) {
+__global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCycleArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = a.n, R1 = a.restart + 1;
   const int g = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
   const bool act = t < n;
   const int tc = min(t, n - 1);
+  // row-split mode (block of >= 3 npad threads): thread (lrow, lcol) updates basis row lrow
+  // (0 ghost g-1, 1 own, 2 ghost g+1) at column lcol
+  const int npad = (n + kWave - 1) / kWave * kWave;
+  const bool split = nt >= 3 * npad;
+  const int lrow = t / npad, lcol = min(t - lrow * npad, n - 1);
+  const bool ract = split && lrow < 3 && t - lrow * npad < n;
   const int G = n;  // row workgroups; workgroup n keeps the Givens books
+  const unsigned long long t_launch = a.phase_ticks != nullptr ? wall_clock64() : 0;
   Shared sh;
   {
     using lc = HH_LDS char;
@@ -411,6 +485,7 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     sh.sum = (l1*)take(sizeof(double) * kPStride);
     sh.ctl = (li*)take(sizeof(int) * 4);
     sh.gv = (l1*)take(sizeof(double) * 2);
+    sh.st = (l1*)take(sizeof(double) * 4 * (size_t)a.restart);
   }
   // this cycle's stop column and inner tolerance: as given, or from the restart loop's state
   // that the previous queued cycle left (a finished solve or a timeout: nothing to do)
@@ -430,14 +505,15 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
   }
   if (g == G) {
     if (t >= kWave) return;
-    bool ok = true;
-    if (t == 0) ok = givens_role(sh, a, stop_col, ptol);  // (lane 0; the wave reconverges after it)
-    if (__builtin_amdgcn_readfirstlane(ok ? 1 : 0) == 0) {
+    const bool ok = givens_role(sh, a, stop_col, ptol);  // (wave-uniform)
+    if (!ok) {
       if (t == 0)
         __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
+    const unsigned long long ts = a.phase_ticks != nullptr ? wall_clock64() : 0;
     solve_and_publish(sh, a);
+    givens_tail_tick(a, ts);
     return;
   }
   auto Urow = [&](int k, int r) -> l2* { return sh.U + ((size_t)k * 3 + r) * n; };
@@ -461,6 +537,10 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
   const double2 M = cscale(cmul(OM, R1c), ic);
   const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
   const double2 D = csub(M, sum4);
+  // this point's x and b, for the cycle's tail (x += V y, r = b - A x): loaded now, off the tail's
+  // critical path (only this thread writes x[g][t])
+  const double2 x_old = a.x[(size_t)g * n + tc];
+  const double2 b_pt = a.b[(size_t)g * n + tc];
 
   // u_0 = the (unnormalised) V[0] = M r of the regular cycle, own and ghost rows
   for (int r = 0; r < 3; ++r) {
@@ -483,6 +563,7 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
   const bool prof = a.phase_ticks != nullptr && g == 0 && t == 0;
   unsigned long long tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long tprev = prof ? wall_clock64() : 0;
+  if (prof) a.phase_ticks[8] += tprev - t_launch;
   const unsigned long long cyc0 = prof ? __builtin_amdgcn_s_memtime() : 0;
   auto tick = [&](int ph) {
     if (prof) {
@@ -528,7 +609,7 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     // |z|^2 and |u_j|^2 both factors are the same vector (cfma_conj(v, v) = |v|^2 + 0 i).
     {
       const int nq = K + 2;
-      const int seg = max(1, min(nt / nq, 16));
+      const int seg = max(1, min(min(nt / nq, 16), kRedRuns / (2 * nq)));  // (sh.red holds them)
       const int q = t / seg, sgi = t % seg;
       const int len = (n - sgi + seg - 1) / seg;
       double2 acc = z2;
@@ -588,18 +669,24 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     // all-reduce (their latency hides behind it), and checked after it -- as a rule they have
     // arrived (the all-reduce needed the neighbours' partial sums, stored after them); any that
     // have not are polled until they carry the round's tag
+    // (row-split mode: the ghost-row threads load their own row's four granules only)
     const int glo = min(max(g - 1, 0), n - 1), ghi = min(g + 1, n - 1);
-    const unsigned long long* zlo = a.zbuf + ((size_t)par * n + glo) * 4 * n + 4 * tc;
-    const unsigned long long* zhi = a.zbuf + ((size_t)par * n + ghi) * 4 * n + 4 * tc;
+    const bool zwait = split ? ract && lrow != 1 : act;
+    const int zc = split ? lcol : tc;
+    const unsigned long long* zlo =
+        a.zbuf + ((size_t)par * n + (split && lrow == 2 ? ghi : glo)) * 4 * n + 4 * zc;
+    const unsigned long long* zhi = a.zbuf + ((size_t)par * n + ghi) * 4 * n + 4 * zc;
     unsigned long long zg[8];
     auto load_ghosts = [&] {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         zg[i] = __hip_atomic_load((gu64*)(zlo + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        zg[4 + i] = __hip_atomic_load((gu64*)(zhi + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        zg[4 + i] = split ? zg[i]
+                          : __hip_atomic_load((gu64*)(zhi + i), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
       }
     };
-    if (act) load_ghosts();
+    if (zwait) load_ghosts();
     // (and thread 0 the Givens workgroup's verdict on column j-2, checked after the all-reduce)
     const unsigned long long* vp = a.verdict + 2 * max(j - 2, 0);
     unsigned long long vg[2] = {0, 0};
@@ -611,7 +698,7 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     tick(1);
     double2 zl = z2, zh = z2;
     bool zok = true;
-    if (act) {
+    if (zwait) {
       unsigned spins = 0;
       for (;;) {
         bool all = true;
@@ -649,7 +736,35 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     const double w2 = sh.sum[2 * K];
     double rest = w2;
     tick(3);
-    if (act) {
+    if (split) {
+      // one row per thread group: the same terms in the same order as the three-row form below
+      // (identical bits), a quarter of the LDS loads and FMAs per thread
+      if (ract) {
+        constexpr int kStep = 8;
+        double2 w = lrow == 1 ? sh.zrow[lcol] : zl;
+        for (int k0 = 0; k0 < K; k0 += kStep) {
+          double2 cv[kStep], uv[kStep];
+          double tv[kStep];
+#pragma unroll
+          for (int i = 0; i < kStep; ++i) {
+            const int k = min(k0 + i, K - 1);
+            const double vk = k == j ? vj : sh.vs[k];
+            const double2 d = make_double2(sh.sum[2 * k], sh.sum[2 * k + 1]);
+            cv[i] = cscale(cscale(d, vk), vk);
+            tv[i] = cabs2(d) * vk * vk;
+            uv[i] = Urow(k, lrow)[lcol];
+          }
+#pragma unroll
+          for (int i = 0; i < kStep; ++i)
+            if (k0 + i < K) {
+              rest -= tv[i];
+              w = csub(w, cmul(cv[i], uv[i]));
+            }
+        }
+        const int gr = g - 1 + lrow;
+        Urow(j + 1, lrow)[lcol] = csel(gr >= 0 && gr < n, w, z2);
+      }
+    } else if (act) {
       // u_{j+1} = z - sum_k c_k u_k on the own row and both ghost rows (neighbours' z from the
       // all-reduce's round; beyond the grid the ghost stays zero); the three rows' chains
       // interleaved, the loads of kStep basis vectors in flight together, terms in k order
@@ -700,17 +815,27 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     for (int q = 0; q < 7; ++q) a.phase_ticks[q] += tk[q];
     // shader-clock cycles over the loop (the effective clock: slot 7 / sum of slots)
     a.phase_ticks[7] += __builtin_amdgcn_s_memtime() - cyc0;
+    tprev = wall_clock64();
   }
+  auto tail_tick = [&](int slot) {  // head / tail spans (slots 8 .. 11)
+    if (prof) {
+      const unsigned long long now = wall_clock64();
+      a.phase_ticks[slot] += now - tprev;
+      tprev = now;
+    }
+  };
   if (!stopped) {
     // the cycle's last column needs |u_{stop_col+1}|: one more reduction round (for the Givens
     // workgroup)
     const int last = stop_col + 1;
     const int par = epoch & 1;
-    if (t == 0) {
+    if (t < kWave) {  // (wave 0: strided partial sums, then the butterfly)
       const l2* ul = Urow(last, 1);
       double s = 0.0;
-      for (int p = 0; p < n; ++p) s = fma(ul[p].x, ul[p].x, fma(ul[p].y, ul[p].y, s));
-      st_gran(ar.part + ((size_t)par * G + g) * 2 * kPStride, gran_tag(a.seq, epoch + 1), s);
+      for (int p = t; p < n; p += kWave) s = fma(ul[p].x, ul[p].x, fma(ul[p].y, ul[p].y, s));
+      s = wave_sum(s);
+      if (t == 0)
+        st_gran(ar.part + ((size_t)par * G + g) * 2 * kPStride, gran_tag(a.seq, epoch + 1), s);
     }
     epoch++;
     if (!allreduce_rows(ar, par, epoch, 1, sh.sum, sh.red)) return;
@@ -745,6 +870,7 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
       return;
     }
   }
+  tail_tick(9);
   const int col = sh.ctl[1];
   double2 xn = z2;
   if (act) {
@@ -761,9 +887,8 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
       for (int i = 0; i < kBatch; ++i)
         if (k0 + i <= col) acc = cfma(cv[i], uv[i], acc);
     }
-    double2* xp = a.x + (size_t)g * n + t;
-    xn = cadd(*xp, acc);
-    *xp = xn;
+    xn = cadd(x_old, acc);
+    a.x[(size_t)g * n + t] = xn;
   }
   // The next cycle's start (runtime.cpp residual): r = b - A x, V[0] = M r, |r|^2 and |M r|^2,
   // in two more rounds -- the x rows to the neighbours (tagged granules), then a two-column
@@ -779,11 +904,30 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
   if (act) {
     const unsigned long long* xlo = a.xbuf + (size_t)min(max(g - 1, 0), n - 1) * 4 * n + 4 * tc;
     const unsigned long long* xhi = a.xbuf + (size_t)min(g + 1, n - 1) * 4 * n + 4 * tc;
-    double v[4];
-    xok = ld_gran(xlo, xtag, &v[0]) && ld_gran(xlo + 2, xtag, &v[1]) &&
-          ld_gran(xhi, xtag, &v[2]) && ld_gran(xhi + 2, xtag, &v[3]);
-    xl = make_double2(v[0], v[1]);
-    xh = make_double2(v[2], v[3]);
+    // the eight granules in flight together, polled until all carry the round's tag
+    unsigned long long xg[8];
+    unsigned spins = 0;
+    for (;;) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        xg[i] = __hip_atomic_load((gu64*)(xlo + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        xg[4 + i] = __hip_atomic_load((gu64*)(xhi + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      bool all = true;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) all = all && (unsigned)(xg[i] >> 32) == xtag;
+      if (all) break;
+      if (++spins > kSpinLimit) {
+        xok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    auto dbl = [](unsigned long long hi, unsigned long long lo) {
+      return __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
+    };
+    xl = make_double2(dbl(xg[0], xg[1]), dbl(xg[2], xg[3]));
+    xh = make_double2(dbl(xg[4], xg[5]), dbl(xg[6], xg[7]));
     sh.zrow[t] = xn;
   }
   if (__syncthreads_or(!xok)) {
@@ -791,6 +935,7 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
       __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
+  tail_tick(10);
   double r2 = 0.0, m2 = 0.0;
   if (act) {
     const double2 xC = sh.zrow[tc];
@@ -803,31 +948,30 @@ __global__ __launch_bounds__(kSmallThreads + kWave) void gmres_small_cycle_kerne
     Ax = cfma(D, xC, Ax);
     Ax = cfma(E, xE, Ax);
     Ax = cfma(N, xN, Ax);
-    const double2 rr = csub(a.b[(size_t)g * n + t], Ax);
+    const double2 rr = csub(b_pt, Ax);
     const double2 mr = JAC ? cdiv(rr, D) : rr;
     a.v0[(size_t)g * n + t] = mr;
     r2 = cabs2(rr);
     m2 = cabs2(mr);
   }
-  // row sums in point order (two threads, the loads in flight in batches)
-  sh.red[2 * t] = r2;
-  sh.red[2 * t + 1] = m2;
+  // row sums: per wave by butterfly, then the waves in order
+  {
+    const double r2w = wave_sum(r2), m2w = wave_sum(m2);
+    if ((t & (kWave - 1)) == 0) {
+      sh.red[2 * (t / kWave)] = r2w;
+      sh.red[2 * (t / kWave) + 1] = m2w;
+    }
+  }
   __syncthreads();
   const int par = epoch & 1;
   epoch++;
   if (t < 2) {
     double sacc = 0.0;
-    for (int p0 = 0; p0 < n; p0 += kBatch) {
-      double v[kBatch];
-#pragma unroll
-      for (int i = 0; i < kBatch; ++i) v[i] = sh.red[2 * min(p0 + i, n - 1) + t];
-#pragma unroll
-      for (int i = 0; i < kBatch; ++i)
-        if (p0 + i < n) sacc += v[i];
-    }
+    for (int q = 0; q < (n + kWave - 1) / kWave; ++q) sacc += sh.red[2 * q + t];
     st_gran(ar.part + ((size_t)par * G + g) * 2 * kPStride + 2 * t, xtag, sacc);
   }
   if (!allreduce_rows(ar, par, epoch, 2, sh.sum, sh.red)) return;
+  tail_tick(11);
   if (g == 0 && t == 0) {
     a.red[4] = sh.sum[0];  // (device: the next cycle's |r|^2, |M r|^2)
     a.red[5] = sh.sum[1];
@@ -865,7 +1009,8 @@ size_t small_cycle_lds_bytes(int n, int restart) {
   auto al = [](size_t b) { return (b + 15) / 16 * 16; };
   return al(16 * R1 * 3 * n) + al(16 * (size_t)n) + al(16 * (size_t)restart * R1) +
          al(32 * (size_t)restart) + 2 * al(16 * R1) + 2 * al(8 * R1) + al(8 * (size_t)restart) +
-         al(8 * (size_t)(kRedRuns + kRuns)) + al(8 * kPStride) + al(16) + al(16);
+         al(8 * (size_t)(kRedRuns + kRuns)) + al(8 * kPStride) + al(16) + al(16) +
+         al(32 * (size_t)restart);
 }
 
 size_t small_cycle_scratch_doubles(int n) {
@@ -902,7 +1047,10 @@ void launch_one(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds, hipS
 }
 
 void launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi, hipStream_t s) {
-  const int threads = (a.n + kWave - 1) / kWave * kWave;
+  const int npad = (a.n + kWave - 1) / kWave * kWave;
+  // (HH_SMALL_WIDE=0: one copy, the round-2 r02qc shape, for A/B timing)
+  static const bool wide = !(getenv("HH_SMALL_WIDE") && atoi(getenv("HH_SMALL_WIDE")) == 0);
+  const int threads = npad * (wide ? std::max(1, std::min(4, kSmallBlock / npad)) : 1);
   const size_t lds = small_cycle_lds_bytes(a.n, a.restart);
   const dim3 grid(a.n + 1), block(threads);  // + the Givens workgroup
   if (const_c) {

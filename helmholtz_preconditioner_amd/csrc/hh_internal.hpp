@@ -249,7 +249,7 @@ struct SmallCycleArgs {
   unsigned long long* ycoef;    // [kMaxProj + 1][4] y_k / sigma_k, then the solved column
   unsigned seq;            // launch sequence number: the tags of this launch's granules
   unsigned* timeout_word;  // set when a wait gives up (zeroed at the start of a solve)
-  unsigned long long* phase_ticks;  // optional [8]: workgroup 0's wall-clock ticks per phase
+  unsigned long long* phase_ticks;  // optional [kSmallTicks]: workgroup 0's wall-clock ticks
   // optional (device) scipy's restart-loop state, so that several cycles can be queued behind
   // each other: [0] ptol, [1] ptol_max_factor, [2] atol, [3] inner iterations so far,
   // [4] maxiter, [5] legacy (maxiter caps inner iterations), [6] done.  A launch that finds
@@ -259,6 +259,8 @@ struct SmallCycleArgs {
   double* outer;
 };
 constexpr int kOuterDoubles = 8;
+constexpr int kSmallTicks = 16;  // phase_ticks: 7 loop phases, shader clock, 4 head / tail spans,
+                                 // 3 Givens-workgroup spans
 // columns of the small cycle's all-reduce rows: 2 K dot halves, |z|^2, |u_j|^2 (K <= kMaxProj)
 constexpr int kSmallCols = 2 * (kMaxProj + 1) + 2;
 constexpr int kSmallRounds = kMaxProj + 8;  // all-reduce rounds per launch (<= restart + 3)

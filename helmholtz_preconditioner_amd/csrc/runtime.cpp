@@ -1538,12 +1538,26 @@ HH_API int hh_op_small_cycle_profile(hh_op* op, int enable, double* phase_us) {
     for (int q = 0; q < 7; ++q) phase_us[q] = t[q] * 1e3 / khz;
     phase_us[7] = (double)t[7];  // shader-clock cycles over the same span (s_memtime)
   }
-  if (enable && !op->small_ticks) op->small_ticks = dalloc<unsigned long long>(8);
-  if (op->small_ticks) HIPC(hipMemset(op->small_ticks, 0, 8 * sizeof(unsigned long long)));
+  if (enable && !op->small_ticks) op->small_ticks = dalloc<unsigned long long>(kSmallTicks);
+  if (op->small_ticks)
+    HIPC(hipMemset(op->small_ticks, 0, kSmallTicks * sizeof(unsigned long long)));
   if (!enable) {
     dfree(op->small_ticks);
     op->small_ticks = nullptr;
   }
+  GUARD_END
+}
+
+HH_API int hh_op_small_cycle_tail_profile(hh_op* op, double* tail_us) {
+  GUARD_BEGIN
+  REQUIRE(op && tail_us, "null argument");
+  REQUIRE(op->small_ticks, "small-cycle profiling is not enabled (hh_op_small_cycle_profile)");
+  HIPC(hipSetDevice(op->ctx->device));
+  unsigned long long t[kSmallTicks];
+  HIPC(hipMemcpy(t, op->small_ticks, sizeof(t), hipMemcpyDeviceToHost));
+  int khz = 100000;
+  (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, op->ctx->device);
+  for (int q = 0; q < 7; ++q) tail_us[q] = t[8 + q] * 1e3 / (khz > 0 ? khz : 100000);
   GUARD_END
 }
 

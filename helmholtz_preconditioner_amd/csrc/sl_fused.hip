@@ -940,11 +940,264 @@ __device__ __forceinline__ void sl2_tile9(const StencilArgs& a, const int t) {
   __syncthreads();  // LDS reuse by the block's next tile
 }
 
+// sl2_tile9 with sl2_tile_v2's instruction cuts (the round-1 form is VALU-issue-bound: ~400
+// vector instructions per point-row, a third of them v_readlane of a four-row ring of PML table
+// values spilled from SGPRs):
+//  * the band's row tables (rows rb-2 .. re+1) staged in LDS once per tile, read by broadcast;
+//  * the second sweep takes the shifted mass Mb, the shifted diagonal Db and 1/|Db|^2 of its
+//    row from the first sweep (the values it would recompute: one IEEE division per point,
+//    no second mass / diagonal / four-coefficient sum);
+//  * interior tiles run without masks (EDGE = false).
+// Same separable arithmetic term for term: bit-identical to the two-launch path.
+// T and z1 reach the second sweep as plain values, as in the two-launch path (where they make a
+// round trip through HBM): without the empty asm, a mask-free tile lets the compiler fuse the
+// multiply that produced them into their consumers (e.g. zN - zC -> fma), one rounding fewer
+__device__ __forceinline__ double2 opaque(double2 v) {
+  asm volatile("" : "+v"(v.x), "+v"(v.y));
+  return v;
+}
+struct Sl9Lds {
+  double2 lv[4][kStencilThreads + 2];  // v rows, slot(row) = (row - rb + 2) & 3
+  double2 lyv[kStencilThreads + 2];    // Y of v on the first-sweep row
+  double2 lz[kStencilThreads + 2];     // z1 row entering the second sweep
+  double2 lyz[kStencilThreads + 2];    // Y of z1 on the second-sweep row
+  double2 ltab[kSl2MaxBand + 4][4];
+};
+template <bool CONSTC, bool NTU, bool EDGE>
+__device__ __forceinline__ void sl2_tile9_v2(const StencilArgs& a, const int t, Sl9Lds& L) {
+  constexpr int TPB = kStencilThreads;
+  constexpr int WO = TPB - 2;
+  auto& lv = L.lv;
+  auto& lyv = L.lyv;
+  auto& lz = L.lz;
+  auto& lyz = L.lyz;
+  auto& ltab = L.ltab;
+  const int tx = t % a.tiles_x;
+  const int ty = t / a.tiles_x;
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int n = a.n, nl = a.nl;
+  const int i0 = tx * WO;
+  const int c = i0 + tid - 1;
+  const bool cin = !EDGE || (c >= 0 && c < n);
+  const int cc = EDGE ? min(max(c, 0), n - 1) : c;
+  const bool outl = tid >= 1 && tid <= TPB - 2 && cin;
+  const int rb = __builtin_amdgcn_readfirstlane(a.row_begin + ty * a.row_step);
+  const int re = __builtin_amdgcn_readfirstlane(min(rb + a.rows_per_block, a.row_end));
+  int ie = lane < kWave / 2 ? i0 - 2 : i0 + TPB - 1;
+  const bool lw = !EDGE || i0 - 2 >= 0;
+  const bool le = !EDGE || i0 + TPB - 1 < n;
+  if constexpr (EDGE) ie = min(max(ie, 0), n - 1);
+  const double2 z2 = make_double2(0.0, 0.0);
+  const Stencil9W w = a.w9;
+
+  auto rowp = [&](int r) -> const double2* {
+    return r < 0 ? a.halo_lo + (size_t)(r + 2) * n
+                 : (r >= nl ? a.halo_hi + (size_t)(r - nl) * n : a.u + (size_t)r * n);
+  };
+  auto load_v = [&](int r) -> double2 {
+    const double2* p = rowp(r) + cc;
+    if constexpr (NTU)
+      return make_double2(__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y));
+    else
+      return *p;
+  };
+  auto load_in = [&](int r, RowIn& v) {
+    if constexpr (!CONSTC) {
+      const double* q = r < 0 ? a.invc2_halo + (size_t)(r + 2) * n
+                              : (r >= nl ? a.invc2_halo + (size_t)(r - nl + 2) * n
+                                         : a.invc2 + (size_t)r * n);
+      v.ic = __builtin_nontemporal_load(q + cc);
+    } else {
+      v.ic = a.invc2_const;
+    }
+    v.e = rowp(r)[ie];
+  };
+  {  // PML row tables of the band (tab_j_ext rows rb-2 .. re+1) into LDS
+    const int cnt = (re - rb + 4) * 4;
+    for (int k = tid; k < cnt; k += TPB) {
+      const int rr = min(rb - 2 + k / 4, nl + 1);
+      (&ltab[0][0])[k] = a.tab_j[4 * rr + (k & 3)];
+    }
+  }
+  auto tab = [&](int r) -> const double2* { return ltab[r - rb + 2]; };
+  const double2 AW = a.tab_i[cc], AE = a.tab_i[n + cc], R1 = a.tab_i[2 * n + cc];
+  const double2 R1e = a.tab_i[2 * n + ie];  // the edge lanes' halo column
+  const double sin = a.in_scale ? *a.in_scale : 1.0;
+  auto xdiff = [&](double2 R2, double2 uW, double2 uC, double2 uE) {
+    return cmul(R2, cfma(AE, csub(uE, uC), cmul(AW, csub(uW, uC))));
+  };
+  auto ydiff = [&](double2 R, double2 BS, double2 BN, double2 uS, double2 uC, double2 uN) {
+    return cmul(R, cfma(BN, csub(uN, uC), cmul(BS, csub(uS, uC))));
+  };
+  auto op9 = [&](double2 Mo, double2 Xm, double2 Xc, double2 Xp, double2 Yc, double2 Yw,
+                 double2 Ye, double2 Hm, double2 Hc, double2 Hp, double2 uS, double2 uC,
+                 double2 uN) {
+    const double2 lap = cadd(Xc, Yc);
+    const double2 avg = cadd(cadd(Xm, Xp), cadd(Yw, Ye));
+    const double2 edges = cadd(Hc, cadd(uS, uN));
+    const double2 corners = cadd(Hm, Hp);
+    const double2 mix = cadd(cadd(cscale(uC, w.c), cscale(edges, w.d)), cscale(corners, w.e));
+    return cfma(Mo, mix, cadd(cscale(lap, w.alpha), cscale(avg, w.g)));
+  };
+
+  double2 Xvm, Xvc, Hvm, Hvc;  // v: X, H of rows s-1, s
+  double2 Xzm, Xzc, Hzm, Hzc;  // z1: X, H of rows r-1, r
+  // first sweep on row s: row s+1 (vN, its edge eN) enters the v ring; T, z1 and the row's
+  // shifted mass, diagonal and 1/|Db|^2 out
+  auto stage1 = [&](int s, double2 vS, double2 vC, double2 vN, double2 eN, const RowIn& in,
+                    double2& T, double2& z1, double2& Mbo, double2& Dbo, double& invo)
+      __attribute__((always_inline)) {
+    const double2* tb = tab(s);
+    const double2 BS = tb[1], BN = tb[2];
+    double2* lS = lv[(s - 1 - rb + 2) & 3];
+    double2* lC = lv[(s - rb + 2) & 3];
+    double2* lN = lv[(s + 1 - rb + 2) & 3];
+    const double2 Yc = ydiff(R1, BS, BN, vS, vC, vN);
+    lN[tid + 1] = EDGE ? csel(cin, vN, z2) : vN;
+    lyv[tid + 1] = EDGE ? csel(cin, Yc, z2) : Yc;
+    if (tid == 0) {
+      const double2 e = EDGE ? csel(lw, eN, z2) : eN;
+      lN[0] = e;
+      lyv[0] = ydiff(R1e, BS, BN, lS[0], lC[0], e);
+    }
+    if (tid == TPB - 1) {
+      const double2 e = EDGE ? csel(le, eN, z2) : eN;
+      lN[TPB + 1] = e;
+      lyv[TPB + 1] = ydiff(R1e, BS, BN, lS[TPB + 1], lC[TPB + 1], e);
+    }
+    __syncthreads();
+    const double2 vNW = lN[tid], vNE = lN[tid + 2];
+    const double2 Yw = lyv[tid], Ye = lyv[tid + 2];
+    const double2 Xp = xdiff(tab(s + 1)[0], vNW, vN, vNE);
+    const double2 Hp = cadd(vNW, vNE);
+    const double2 R2 = tb[0], OM = tb[3];
+    const double2 W = cmul(AW, R2);
+    const double2 E = cmul(AE, R2);
+    const double2 S = cmul(BS, R1);
+    const double2 N = cmul(BN, R1);
+    const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
+    const double2 M = cscale(cmul(OM, R1), in.ic);
+    const double2 Mb = cmul(M, a.mshift);
+    const double2 Db = stencil9_diag(Mb, sum4, w);
+    T = opaque(cscale(op9(M, Xvm, Xvc, Xp, Yc, Yw, Ye, Hvm, Hvc, Hp, vS, vC, vN), sin));
+    const double inv = 1.0 / fma(Db.x, Db.x, Db.y * Db.y);  // = cdiv(T, Db), split
+    const double2 q = cscale(make_double2(fma(T.x, Db.x, T.y * Db.y) * inv,
+                                          fma(T.y, Db.x, -T.x * Db.y) * inv), a.damping);
+    if constexpr (EDGE) z1 = opaque(csel(cin && a.j0 + s >= 0 && a.j0 + s < n, q, z2));
+    else z1 = opaque(q);
+    Xvm = Xvc;
+    Xvc = Xp;
+    Hvm = Hvc;
+    Hvc = Hp;
+    Mbo = Mb;
+    Dbo = Db;
+    invo = inv;
+  };
+  // second sweep on row r: w = z1 + damp (T - A_beta z1) / Db; z1 row r+1 enters
+  auto stage2 = [&](int r, double2 zS, double2 zC, double2 zN, double2 T, double2 Mb,
+                    double2 Db, double inv) __attribute__((always_inline)) -> double2 {
+    const double2* tb = tab(r);
+    const double2 Yc = ydiff(R1, tb[1], tb[2], zS, zC, zN);
+    lz[tid + 1] = zN;
+    lyz[tid + 1] = Yc;
+    __syncthreads();
+    const double2 zNW = lz[tid], zNE = lz[tid + 2];
+    const double2 Yw = lyz[tid], Ye = lyz[tid + 2];
+    const double2 Xp = xdiff(tab(r + 1)[0], zNW, zN, zNE);
+    const double2 Hp = cadd(zNW, zNE);
+    const double2 Au = op9(Mb, Xzm, Xzc, Xp, Yc, Yw, Ye, Hzm, Hzc, Hp, zS, zC, zN);
+    Xzm = Xzc;
+    Xzc = Xp;
+    Hzm = Hzc;
+    Hzc = Hp;
+    const double2 d = csub(T, Au);
+    const double2 q = make_double2(fma(d.x, Db.x, d.y * Db.y) * inv,
+                                   fma(d.y, Db.x, -d.x * Db.y) * inv);
+    return cadd(zC, cscale(q, a.damping));
+  };
+
+  // rings of four by row, slot(row) = (row - rb + 2) & 3: v rows r .. r+3, z1 rows r-1 .. r+1,
+  // T / Mb / Db / 1/|Db|^2 rows r, r+1, row inputs rows r .. r+3 (r+3 in flight)
+  double2 V[4], Z[4], TT[4], MB[4], DB[4];
+  double INV[4];
+  RowIn IN[4];
+  if (tid == 0) {  // halo slots of the z1 rows: only lanes 0 / TPB-1 read them, for outputs
+    lz[0] = z2;    // nobody stores
+    lyz[0] = z2;
+  }
+  if (tid == TPB - 1) {
+    lz[TPB + 1] = z2;
+    lyz[TPB + 1] = z2;
+  }
+  V[0] = load_v(rb - 2);
+  V[1] = load_v(rb - 1);
+  V[2] = load_v(rb);
+  V[3] = load_v(rb + 1);
+  RowIn inm2;
+  load_in(rb - 2, inm2);  // edges of row rb-2 (the ring's first row)
+  load_in(rb - 1, IN[1]);
+  load_in(rb, IN[2]);
+  load_in(rb + 1, IN[3]);
+  load_in(rb + 2, IN[0]);
+  // rows rb-2 and rb-1 enter the v ring; X, H of both from it
+  lv[0][tid + 1] = EDGE ? csel(cin, V[0], z2) : V[0];
+  lv[1][tid + 1] = EDGE ? csel(cin, V[1], z2) : V[1];
+  if (tid == 0) {
+    lv[0][0] = EDGE ? csel(lw, inm2.e, z2) : inm2.e;
+    lv[1][0] = EDGE ? csel(lw, IN[1].e, z2) : IN[1].e;
+  }
+  if (tid == TPB - 1) {
+    lv[0][TPB + 1] = EDGE ? csel(le, inm2.e, z2) : inm2.e;
+    lv[1][TPB + 1] = EDGE ? csel(le, IN[1].e, z2) : IN[1].e;
+  }
+  __syncthreads();  // (also publishes the table rows)
+  Xvm = xdiff(tab(rb - 2)[0], lv[0][tid], V[0], lv[0][tid + 2]);
+  Hvm = cadd(lv[0][tid], lv[0][tid + 2]);
+  Xvc = xdiff(tab(rb - 1)[0], lv[1][tid], V[1], lv[1][tid + 2]);
+  Hvc = cadd(lv[1][tid], lv[1][tid + 2]);
+  stage1(rb - 1, V[0], V[1], V[2], IN[2].e, IN[1], TT[1], Z[1], MB[1], DB[1], INV[1]);
+  V[0] = load_v(rb + 2);
+  __syncthreads();  // lyv is rewritten by the next first sweep
+  stage1(rb, V[1], V[2], V[3], IN[3].e, IN[2], TT[2], Z[2], MB[2], DB[2], INV[2]);
+  // the second sweep's register ring starts with X, H of z1 rows rb-1 and rb
+  lz[tid + 1] = Z[1];
+  lyz[tid + 1] = Z[2];
+  __syncthreads();
+  Xzm = xdiff(tab(rb - 1)[0], lz[tid], Z[1], lz[tid + 2]);
+  Hzm = cadd(lz[tid], lz[tid + 2]);
+  Xzc = xdiff(tab(rb)[0], lyz[tid], Z[2], lyz[tid + 2]);
+  Hzc = cadd(lyz[tid], lyz[tid + 2]);
+  __syncthreads();
+
+  for (int r0 = rb; r0 < re; r0 += 4) {
+    unroll<0, 4>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      const int r = r0 + k;
+      const bool live = r < re;
+      V[(k + 1) & 3] = load_v(min(r + 3, re + 1));
+      load_in(min(r + 3, re + 1), IN[(k + 1) & 3]);
+      stage1(min(r + 1, re), V[(k + 2) & 3], V[(k + 3) & 3], V[k & 3], IN[k & 3].e,
+             IN[(k + 3) & 3], TT[(k + 3) & 3], Z[(k + 3) & 3], MB[(k + 3) & 3], DB[(k + 3) & 3],
+             INV[(k + 3) & 3]);
+      const double2 wv = stage2(min(r, re), Z[(k + 1) & 3], Z[(k + 2) & 3], Z[(k + 3) & 3],
+                                TT[(k + 2) & 3], MB[(k + 2) & 3], DB[(k + 2) & 3],
+                                INV[(k + 2) & 3]);
+      if (outl && live) {
+        double2* p = a.out0 + (size_t)r * n + c;
+        __builtin_nontemporal_store(wv.x, &p->x);
+        __builtin_nontemporal_store(wv.y, &p->y);
+      }
+    });
+  }
+  __syncthreads();  // LDS reuse by the block's next tile
+}
+
 // SHAPE (5-point): 0 = sl2_tile (two barriers per row), 1 = sl2_tile_1b (one barrier per row),
 // 2 = sl2_wave (wave strips, no barrier), 3 = sl2_tile_v2 (one barrier, LDS tables, mask-free
 // interior tiles).  The 9-point operator has sl2_tile9 only.
 template <bool CONSTC, bool NTU, int TPB, bool S9, int SHAPE = 0, int PF = 1>
-__global__ __launch_bounds__(TPB) void sl2_kernel(const StencilArgs a) {
+__global__ __launch_bounds__(TPB, (S9 && SHAPE == 4) ? 3 : 1) void sl2_kernel(const StencilArgs a) {
   if (a.stop && *a.stop) return;  // queued GMRES cycle already stopped
   const int L = blockIdx.x;
   const int q = L >> 3, Q = gridDim.x >> 3;
@@ -952,7 +1205,17 @@ __global__ __launch_bounds__(TPB) void sl2_kernel(const StencilArgs a) {
   for (int tt = q; tt < a.tiles_per_xcd; tt += Q) {
     const int t = (L & 7) * a.tiles_per_xcd + tt;
     if (t >= ntiles) break;  // uniform per block
-    if constexpr (S9) sl2_tile9<CONSTC, NTU, TPB>(a, t);
+    if constexpr (S9 && (SHAPE == 3 || SHAPE == 4)) {  // (4: at 3 waves per SIMD)
+      const int tx = t % a.tiles_x, ty = t / a.tiles_x;
+      const int i0 = tx * (TPB - 2);
+      const int rb = a.row_begin + ty * a.row_step;
+      const int re = min(rb + a.rows_per_block, a.row_end);
+      const bool interior = i0 - 2 >= 0 && i0 + TPB - 1 < a.n && a.j0 + rb - 1 >= 0 &&
+                            a.j0 + re < a.n;
+      __shared__ Sl9Lds lds9;
+      if (interior) sl2_tile9_v2<CONSTC, NTU, false>(a, t, lds9);
+      else sl2_tile9_v2<CONSTC, NTU, true>(a, t, lds9);
+    } else if constexpr (S9) sl2_tile9<CONSTC, NTU, TPB>(a, t);
     else if constexpr (SHAPE == 1) sl2_tile_1b<CONSTC, NTU, TPB>(a, t);
     else if constexpr (SHAPE == 2) sl2_wave<CONSTC, NTU>(a, t);
     else if constexpr (SHAPE == 3) {
@@ -976,10 +1239,10 @@ template <int TPB, bool NTU, int SHAPE = 0, int PF = 1>
 void launch_t(bool const_c, const StencilArgs& a, int blocks, hipStream_t s) {
   const bool s9 = a.tab_r2x != nullptr;  // 9-point operator (the tables themselves are unused)
   if (const_c) {
-    if (s9) hipLaunchKernelGGL((sl2_kernel<true, NTU, TPB, true>), dim3(blocks), dim3(TPB), 0, s, a);
+    if (s9) hipLaunchKernelGGL((sl2_kernel<true, NTU, TPB, true, SHAPE == 3 ? (PF == 2 ? 4 : 3) : 0>), dim3(blocks), dim3(TPB), 0, s, a);
     else hipLaunchKernelGGL((sl2_kernel<true, NTU, TPB, false, SHAPE, PF>), dim3(blocks), dim3(TPB), 0, s, a);
   } else {
-    if (s9) hipLaunchKernelGGL((sl2_kernel<false, NTU, TPB, true>), dim3(blocks), dim3(TPB), 0, s, a);
+    if (s9) hipLaunchKernelGGL((sl2_kernel<false, NTU, TPB, true, SHAPE == 3 ? (PF == 2 ? 4 : 3) : 0>), dim3(blocks), dim3(TPB), 0, s, a);
     else hipLaunchKernelGGL((sl2_kernel<false, NTU, TPB, false, SHAPE, PF>), dim3(blocks), dim3(TPB), 0, s, a);
   }
 }
@@ -1012,10 +1275,14 @@ void launch_sl2(bool const_c, const StencilArgs& a_in, hipStream_t stream, int v
     pf2 = shape == 3 && ((variant - kSl2Variant) & 8) != 0;
   }
   const bool lds_family = variant == 6 || variant == 18 || variant == 30 || variant == 42;
-  if (a.tab_r2x) {  // the 9-point operator has the two-barrier LDS shape only (round-1 default:
-    shape = 0;      // NT v on rows up to 4608 points)
-    pf2 = false;
-    if (!lds_family) ntu = n <= 4608;
+  if (a.tab_r2x) {  // the 9-point operator: shape 3 = sl2_tile9_v2 with v through the cache
+    // (the PF-2 bit, set by default, selects its instantiation held to 3 waves per SIMD:
+    // 163-167 VGPRs, no scratch; without it 167-171, 2 waves), any other shape = the round-1
+    // two-barrier form (sl2_tile9; NT v on rows up to 4608 points unless the variant says)
+    if (lds_family || (sl2_variant(variant) && shape != 3)) {
+      if (!sl2_variant(variant)) ntu = n <= 4608;
+      shape = 0;
+    }
   }
   const int rows = a.row_end - a.row_begin;
   if (shape == 3 && a.rows_per_block > kSl2MaxBand) {  // LDS table capacity of the shape

@@ -240,6 +240,13 @@ int hh_op_set_small_cycle(hh_op* op, int mode);
  * the neighbours' z, 2 basis update, 4 wait for the Givens step) and in [7] the shader-clock
  * cycles over the same span; then the counters restart (enable = 1) or stop (enable = 0). */
 int hh_op_small_cycle_profile(hh_op* op, int enable, double* phase_us);
+/* Diagnostic, with hh_op_small_cycle_profile enabled: workgroup 0's wall clock outside the
+ * inner iterations, summed over the cycles so far, in us: [0] launch start
+ * to the first iteration, [1] the last column's round + the Givens workgroup's solve (y received),
+ * [2] the x update and the x rows' hand-off, [3] the next cycle's residual and its all-reduce;
+ * the Givens workgroup's [4] waits for the rounds' sums, [5] per-round Hessenberg work, [6] last
+ * column, triangular solve and publication of y (tail_us: 7 doubles). */
+int hh_op_small_cycle_tail_profile(hh_op* op, double* tail_us);
 /* Performance tuning of the stencil kernel used by HH_APPLY_A: variant in [0, 48) selects the
  * marching kernel's W/E exchange (LDS row / direct cached loads / wave shuffle), prefetch depth,
  * load/store cache policy and strip width, 96 + R (R = 2 .. 8 rows, + 16 / + 32 cache-policy

@@ -268,3 +268,42 @@ def test_fused_shifted_laplace_shapes_bit_identical(n, kind, rpb, slabs):
     for xs, hist in out[1:]:
         np.testing.assert_array_equal(hist, out[0][1])
         np.testing.assert_array_equal(xs, out[0][0])
+
+
+@pytest.mark.parametrize("n,kind,rpb,slabs", [(97, "c2", 0, 1), (700, "c1", 13, 1), (700, "c1", 100, 1),
+                                              (1100, "const", 0, 1), (2100, "c1", 0, 1),
+                                              (301, "c1", 0, 3), (63, "c1", 0, 1),
+                                              (125, "c2", 5, 2)])
+def test_fused_shifted_laplace9_shapes_bit_identical(n, kind, rpb, slabs):
+    """9-point operator (row F4): the round-1 two-barrier fused M A (kSl2Variant + 0 / + 4, NT v)
+    and the default shape (sl2_tile9_v2: LDS row tables, Mb / Db / 1/|Db|^2 handed from the first
+    sweep to the second, mask-free interior tiles; + 3 / + 7, and + 11 / + 15 held to 3 waves per
+    SIMD) against the two-launch path, bit for bit: ragged n, odd and over-tall band heights,
+    virtual slabs; GMRES histories too."""
+    b, C, wn = 12, 81.0, 10.0
+    om, h, eta = O.problem_params(n, b, wn, 2.0)
+    cm = medium(kind, n)
+    c = H.Context(device=0, virtual_slabs=slabs)
+    A = H.build_A_matrix(b, C, eta, om, h, n, cm, context=c, stencil=9)
+    M = H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7)
+    x = rand_complex(n * n, 23)
+    A.sl_fusion(False)
+    M.configure()
+    ref = A._apply_host(x, H._ffi.HH_APPLY_PREC_A)
+    A.sl_fusion(True)
+    for v in (-1, 160, 164, 163, 167, 171, 175):
+        A.tune(v, rpb, 0)
+        M.configure()
+        np.testing.assert_array_equal(A._apply_host(x, H._ffi.HH_APPLY_PREC_A), ref, err_msg=str(v))
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    out = []
+    for v in (-1, 160, 167):
+        A.tune(v, rpb, 0)
+        xs, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=12, M=M,
+                                 callback=lambda r: None, callback_type="legacy",
+                                 return_history=True)
+        out.append((xs, hist))
+    A.tune(-1, 0, 0)
+    for xs, hist in out[1:]:
+        np.testing.assert_array_equal(hist, out[0][1])
+        np.testing.assert_array_equal(xs, out[0][0])

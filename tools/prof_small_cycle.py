@@ -40,6 +40,9 @@ for mode in ("on", "off", "on"):
     else:  # (maxiter then counts cycles: iters // 20 of them)
         H.gmres(A, f, rtol=1e-14, restart=20, maxiter=a.iters // 20, M=M)
     dt = time.perf_counter() - t0
+    tail = (ctypes.c_double * 7)()
+    if mode == "on":
+        _ffi.check(_ffi.lib.hh_op_small_cycle_tail_profile(A.handle, tail))
     _ffi.check(_ffi.lib.hh_op_small_cycle_profile(A.handle, 0, ph))
     per = [ph[q] / a.iters for q in (0, 5, 6, 1, 3, 2, 4)]
     span = sum(ph[q] for q in range(7))
@@ -49,3 +52,9 @@ for mode in ("on", "off", "on"):
              "  phases us/it: stencil %.2f dots %.2f publish %.2f allreduce %.2f coef+ghosts %.2f"
              " update %.2f givens-wait %.2f  (shader clock %.0f MHz)"
              % tuple(per + [mhz])), flush=True)
+    if mode == "on":
+        cyc = -(-a.iters // 20)
+        print("  per cycle (us, workgroup 0): head %.2f  last round + Givens solve %.2f  x update +"
+              " hand-off %.2f  residual + all-reduce %.2f\n  Givens workgroup per cycle: waits %.2f"
+              "  per-round work %.2f  last column + solve + publish %.2f" % tuple(v / cyc for v in tail),
+              flush=True)
