@@ -136,7 +136,7 @@ __device__ __forceinline__ bool ld_gran(const unsigned long long* p, unsigned ta
   }
 }
 __device__ bool allreduce_rows(const ArArgs& ar, int par, unsigned epoch, int cols, l1* out,
-                               l1* red) {
+                               l1* red, unsigned long long* t_reduced = nullptr) {
   const int G = ar.G, g = blockIdx.x;
   const int t = threadIdx.x;
   const unsigned tag = gran_tag(ar.seq, epoch);
@@ -187,6 +187,7 @@ __device__ bool allreduce_rows(const ArArgs& ar, int par, unsigned epoch, int co
       double s = 0.0;
       for (int q = 0; q < kRuns; ++q) s += red[kRedRuns + q];
       st_gran(ar.sums + (size_t)epoch * 2 * kPStride + 2 * c, tag, s);
+      if (t_reduced && c == 0) *t_reduced = wall_clock64();  // (profiling: column 0 summed)
     }
   }
   if (t < cols) {
@@ -328,12 +329,15 @@ __device__ bool givens_role(const Shared& sh, const SmallCycleArgs& a, int stop_
   const int lane = threadIdx.x;
   const bool l0 = lane == 0;
   // optional span timing (lane 0; slots 12 sum waits, 13 per-round work, 14 last column + solve)
+  // (accumulated in registers, written once at the end: a read-modify-write of the counters
+  // per span would itself wait on a global load)
   const bool prof = a.phase_ticks != nullptr && l0;
   unsigned long long tp = prof ? wall_clock64() : 0;
+  unsigned long long acc[3] = {0, 0, 0};
   auto span = [&](int slot) {
     if (prof) {
       const unsigned long long now = wall_clock64();
-      a.phase_ticks[slot] += now - tp;
+      acc[slot - 12] += now - tp;
       tp = now;
     }
   };
@@ -396,6 +400,8 @@ __device__ bool givens_role(const Shared& sh, const SmallCycleArgs& a, int stop_
   }
   if (l0) sh.ctl[1] = col;
   span(14);
+  if (prof)
+    for (int q = 0; q < 3; ++q) a.phase_ticks[12 + q] += acc[q];
   return true;
 }
 __device__ __forceinline__ void givens_tail_tick(const SmallCycleArgs& a, unsigned long long t0) {
@@ -562,8 +568,9 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
   // 2 basis update (coefficients and the next scale inline), 4 the closing barrier
   const bool prof = a.phase_ticks != nullptr && g == 0 && t == 0;
   unsigned long long tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_first_hop = 0;  // all-reduce: publish -> column 0 reduced here (slot 15)
   unsigned long long tprev = prof ? wall_clock64() : 0;
-  if (prof) a.phase_ticks[8] += tprev - t_launch;
+  unsigned long long tl[4] = {prof ? tprev - t_launch : 0, 0, 0, 0};  // head / tail spans
   const unsigned long long cyc0 = prof ? __builtin_amdgcn_s_memtime() : 0;
   auto tick = [&](int ph) {
     if (prof) {
@@ -694,7 +701,10 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
       vg[0] = __hip_atomic_load((gu64*)vp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       vg[1] = __hip_atomic_load((gu64*)(vp + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (!allreduce_rows(ar, par, epoch, cols, sh.sum, sh.red)) return;
+    unsigned long long t_red = 0;
+    const unsigned long long t_ar = tprev;
+    if (!allreduce_rows(ar, par, epoch, cols, sh.sum, sh.red, prof ? &t_red : nullptr)) return;
+    if (prof) t_first_hop += t_red - t_ar;
     tick(1);
     double2 zl = z2, zh = z2;
     bool zok = true;
@@ -811,16 +821,13 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
       break;
     }
   }
-  if (prof) {
-    for (int q = 0; q < 7; ++q) a.phase_ticks[q] += tk[q];
-    // shader-clock cycles over the loop (the effective clock: slot 7 / sum of slots)
-    a.phase_ticks[7] += __builtin_amdgcn_s_memtime() - cyc0;
-    tprev = wall_clock64();
-  }
-  auto tail_tick = [&](int slot) {  // head / tail spans (slots 8 .. 11)
+  // shader-clock cycles over the loop (the effective clock: slot 7 / sum of slots); every
+  // counter is written at the end of the launch (no global round trip inside the timed spans)
+  tk[7] = prof ? __builtin_amdgcn_s_memtime() - cyc0 : 0;
+  auto tail_tick = [&](int slot) {  // head / tail spans (slots 8 .. 11, written at the end)
     if (prof) {
       const unsigned long long now = wall_clock64();
-      a.phase_ticks[slot] += now - tprev;
+      tl[slot - 8] += now - tprev;
       tprev = now;
     }
   };
@@ -972,6 +979,11 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
   }
   if (!allreduce_rows(ar, par, epoch, 2, sh.sum, sh.red)) return;
   tail_tick(11);
+  if (prof) {
+    for (int q = 0; q < 8; ++q) a.phase_ticks[q] += tk[q];
+    for (int q = 0; q < 4; ++q) a.phase_ticks[8 + q] += tl[q];
+    a.phase_ticks[15] += t_first_hop;
+  }
   if (g == 0 && t == 0) {
     a.red[4] = sh.sum[0];  // (device: the next cycle's |r|^2, |M r|^2)
     a.red[5] = sh.sum[1];

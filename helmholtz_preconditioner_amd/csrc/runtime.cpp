@@ -1557,7 +1557,7 @@ HH_API int hh_op_small_cycle_tail_profile(hh_op* op, double* tail_us) {
   HIPC(hipMemcpy(t, op->small_ticks, sizeof(t), hipMemcpyDeviceToHost));
   int khz = 100000;
   (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, op->ctx->device);
-  for (int q = 0; q < 7; ++q) tail_us[q] = t[8 + q] * 1e3 / (khz > 0 ? khz : 100000);
+  for (int q = 0; q < 8; ++q) tail_us[q] = t[8 + q] * 1e3 / (khz > 0 ? khz : 100000);
   GUARD_END
 }
 

@@ -245,7 +245,9 @@ int hh_op_small_cycle_profile(hh_op* op, int enable, double* phase_us);
  * to the first iteration, [1] the last column's round + the Givens workgroup's solve (y received),
  * [2] the x update and the x rows' hand-off, [3] the next cycle's residual and its all-reduce;
  * the Givens workgroup's [4] waits for the rounds' sums, [5] per-round Hessenberg work, [6] last
- * column, triangular solve and publication of y (tail_us: 7 doubles). */
+ * column, triangular solve and publication of y; [7] the all-reduces' first hop as workgroup 0
+ * sees it: its publication to column 0 reduced on it, i.e. the rows' arrival skew + one hop
+ * (tail_us: 8 doubles). */
 int hh_op_small_cycle_tail_profile(hh_op* op, double* tail_us);
 /* Performance tuning of the stencil kernel used by HH_APPLY_A: variant in [0, 48) selects the
  * marching kernel's W/E exchange (LDS row / direct cached loads / wave shuffle), prefetch depth,

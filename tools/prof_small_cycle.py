@@ -40,7 +40,7 @@ for mode in ("on", "off", "on"):
     else:  # (maxiter then counts cycles: iters // 20 of them)
         H.gmres(A, f, rtol=1e-14, restart=20, maxiter=a.iters // 20, M=M)
     dt = time.perf_counter() - t0
-    tail = (ctypes.c_double * 7)()
+    tail = (ctypes.c_double * 8)()
     if mode == "on":
         _ffi.check(_ffi.lib.hh_op_small_cycle_tail_profile(A.handle, tail))
     _ffi.check(_ffi.lib.hh_op_small_cycle_profile(A.handle, 0, ph))
@@ -56,5 +56,19 @@ for mode in ("on", "off", "on"):
         cyc = -(-a.iters // 20)
         print("  per cycle (us, workgroup 0): head %.2f  last round + Givens solve %.2f  x update +"
               " hand-off %.2f  residual + all-reduce %.2f\n  Givens workgroup per cycle: waits %.2f"
-              "  per-round work %.2f  last column + solve + publish %.2f" % tuple(v / cyc for v in tail),
+              "  per-round work %.2f  last column + solve + publish %.2f" % tuple(v / cyc for v in tail[:7]),
               flush=True)
+        print("  all-reduce first hop (publish -> column 0 reduced on workgroup 0): %.2f us/it"
+              % (tail[7] / a.iters),
+              flush=True)
+
+for rep in range(2):  # the profiled runs instrument workgroup 0; then the same without it
+    A.small_cycle("on")
+    H.gmres(A, f, rtol=1e-14, restart=20, maxiter=20, M=M, callback=lambda r: None,
+            callback_type="legacy")
+    t0 = time.perf_counter()
+    H.gmres(A, f, rtol=1e-14, restart=20, maxiter=a.iters, M=M, callback=lambda r: None,
+            callback_type="legacy")
+    dt = time.perf_counter() - t0
+    print(f"n={n} small_cycle=on, not profiled: {a.iters / dt:9.1f} it/s"
+          f" ({dt / a.iters * 1e6:6.2f} us/it)", flush=True)
