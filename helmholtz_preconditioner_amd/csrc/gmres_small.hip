@@ -368,15 +368,16 @@ __device__ bool givens_role(const Shared& sh, const SmallCycleArgs& a, int stop_
     // expressions; `rest` summed in their k order)
     const double w2 = sh.sum[2 * K], u2 = sh.sum[2 * K + 1];
     const double vj = j >= 1 ? 1.0 / sqrt(u2) : sh.vs[0];
-    double tv = 0.0;
+    double tv = 0.0, tw = 0.0;
     if (lane <= j) {
       const double2 d = make_double2(sh.sum[2 * lane], sh.sum[2 * lane + 1]);
       const double vk = lane == j ? vj : sh.vs[lane];
       sh.H[(size_t)j * R1 + lane] = cscale(cscale(d, vk), vj / sh.ss[j]);
-      tv = cabs2(d) * vk * vk;
+      tv = cabs2(d) * vk;
+      tw = vk;
     }
     double rest = w2;
-    for (int k = 0; k <= j; ++k) rest -= rlane(tv, k);
+    for (int k = 0; k <= j; ++k) rest = fma(-rlane(tv, k), rlane(tw, k), rest);
     bool stop = false;
     if (j >= 1) {
       const int c = j - 1;
@@ -754,20 +755,21 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
         double2 w = lrow == 1 ? sh.zrow[lcol] : zl;
         for (int k0 = 0; k0 < K; k0 += kStep) {
           double2 cv[kStep], uv[kStep];
-          double tv[kStep];
+          double tv[kStep], tw[kStep];
 #pragma unroll
           for (int i = 0; i < kStep; ++i) {
             const int k = min(k0 + i, K - 1);
             const double vk = k == j ? vj : sh.vs[k];
             const double2 d = make_double2(sh.sum[2 * k], sh.sum[2 * k + 1]);
             cv[i] = cscale(cscale(d, vk), vk);
-            tv[i] = cabs2(d) * vk * vk;
+            tv[i] = cabs2(d) * vk;
+            tw[i] = vk;
             uv[i] = Urow(k, lrow)[lcol];
           }
 #pragma unroll
           for (int i = 0; i < kStep; ++i)
             if (k0 + i < K) {
-              rest -= tv[i];
+              rest = fma(-tv[i], tw[i], rest);  // (|d_k|^2 v_k^2, explicitly fused)
               w = csub(w, cmul(cv[i], uv[i]));
             }
         }
@@ -782,21 +784,22 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
       double2 w[3] = {zl, z, zh};
       for (int k0 = 0; k0 < K; k0 += kStep) {
         double2 cv[kStep], uv[3][kStep];
-        double tv[kStep];
+        double tv[kStep], tw[kStep];
 #pragma unroll
         for (int i = 0; i < kStep; ++i) {
           const int k = min(k0 + i, K - 1);
           const double vk = k == j ? vj : sh.vs[k];
           const double2 d = make_double2(sh.sum[2 * k], sh.sum[2 * k + 1]);
           cv[i] = cscale(cscale(d, vk), vk);
-          tv[i] = cabs2(d) * vk * vk;
+          tv[i] = cabs2(d) * vk;
+          tw[i] = vk;
 #pragma unroll
           for (int r = 0; r < 3; ++r) uv[r][i] = Urow(k, r)[t];
         }
 #pragma unroll
         for (int i = 0; i < kStep; ++i)
           if (k0 + i < K) {
-            rest -= tv[i];
+            rest = fma(-tv[i], tw[i], rest);
 #pragma unroll
             for (int r = 0; r < 3; ++r) w[r] = csub(w[r], cmul(cv[i], uv[r][i]));
           }

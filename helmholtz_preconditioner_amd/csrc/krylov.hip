@@ -62,6 +62,17 @@ __device__ __forceinline__ void block_reduce_vec(double (&v)[NV], double* partia
   }
 }
 
+// lane k's double, on every lane of the wave
+__device__ __forceinline__ double rlane(double v, int k) {
+  const long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffff), k);
+  const int hi = __builtin_amdgcn_readlane((int)(u >> 32), k);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double2 rlane2(double2 v, int k) {
+  return make_double2(rlane(v.x, k), rlane(v.y, k));
+}
+
 template <bool SC1 = false>
 __device__ double wave_reduce_like_block(const double* partials, int count, int width);
 __device__ void column_from_sums(const GivensState& g, int col, const double* rd, double rn0,
@@ -181,7 +192,7 @@ __global__ __launch_bounds__(kT) void update_kernel(const double2* __restrict__ 
     if (last_block(cf.counter)) {
       if (threadIdx.x < kWave) {
         const double rn0 = wave_reduce_like_block<true>(partials, gridDim.x, kMaxNorms);
-        if (threadIdx.x == 0) column_from_sums(cf.g, cf.col, cf.rd, rn0, cf.eps, cf.ptol, cf.stop_col);
+        column_from_sums(cf.g, cf.col, cf.rd, rlane(rn0, 0), cf.eps, cf.ptol, cf.stop_col);
       }
       if (threadIdx.x == 0) *cf.counter = 0u;
     }
@@ -312,75 +323,107 @@ __device__ double wave_reduce_like_block(const double* partials, int count, int 
   return x;
 }
 
-// Second half of a Hessenberg column (lane 0): subdiagonal h1 against h0 (scipy's breakdown
-// test), the previous Givens rotations, a new one (zlartg), the residual estimate and the inner
-// exit test (iterative.py:767-795).  h[0 .. col] are already in place.
-__device__ void gmres_finish_column(const GivensState& g, int col, double h0, double h1,
-                                    double inv_sigma_next, double eps, double ptol, int stop_col) {
+// Second half of a Hessenberg column, by ONE wave (every lane computes the same values, lane 0
+// stores them): subdiagonal h1 against h0 (scipy's breakdown test), the previous Givens
+// rotations, a new one (zlartg), the residual estimate and the inner exit test
+// (iterative.py:767-795).  hk = entry `lane` of the column (lanes 0 .. col).  Lane k loads
+// rotation k, so the chain of previous rotations takes its operands by readlane: one global
+// load latency per column instead of one per rotation (the one-lane form waited on a dependent
+// G load per step: 14 us per column at col ~ 19).  Same operations in the same order as the
+// one-lane form: bit-identical.  Returns the exit decision (uniform; also in g.ctrl[0]).
+// The finish's memory operands (lane k: rotation k; S[col] on every lane), loaded unconditionally
+// from clamped addresses so that a caller can issue them with its own loads: one memory latency
+// per launch (a load under a branch makes hipcc wait for every load at the join).
+struct ColIn {
+  double ck;
+  double2 sk, Sc;
+};
+__device__ __forceinline__ ColIn load_col_in(const GivensState& g, int col) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int kr = min(lane, max(col - 1, 0));
+  ColIn in;
+  in.ck = g.G[2 * kr].x;
+  in.sk = g.G[2 * kr + 1];
+  in.Sc = g.S[col];
+  return in;
+}
+__device__ bool gmres_finish_column(const GivensState& g, int col, double2 hk, const ColIn& in,
+                                    double h0, double h1, double inv_sigma_next, double eps,
+                                    double ptol, int stop_col) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const bool l0 = lane == 0;
   const int R1 = g.restart + 1;
   double2* h = g.H + (size_t)col * R1;
-  h[col + 1] = make_double2(h1, 0.0);
+  double2 hsub = make_double2(h1, 0.0);
   double brk = 0.0;
   if (h1 <= eps * h0) {
-    h[col + 1] = make_double2(0.0, 0.0);
+    hsub = make_double2(0.0, 0.0);
     brk = 1.0;
-  } else {
+  } else if (l0) {
     g.vscale[col + 1] = inv_sigma_next;
   }
+  const double ck = in.ck;
+  const double2 sk = in.sk;
+  double2 n0 = rlane2(hk, 0);
   for (int k = 0; k < col; ++k) {
-    const double c = g.G[2 * k].x;
-    const double2 s = g.G[2 * k + 1];
-    const double2 n0 = h[k], n1 = h[k + 1];
-    h[k] = cadd(cscale(n0, c), cmul(s, n1));
-    h[k + 1] = cadd(cmul(make_double2(-s.x, s.y), n0), cscale(n1, c));  // -conj(s)*n0 + c*n1
+    const double c = rlane(ck, k);
+    const double2 s = rlane2(sk, k), n1 = rlane2(hk, k + 1);
+    const double2 hn = cadd(cscale(n0, c), cmul(s, n1));
+    if (l0) h[k] = hn;
+    n0 = cadd(cmul(make_double2(-s.x, s.y), n0), cscale(n1, c));  // -conj(s)*n0 + c*n1
   }
   double c;
   double2 s, r;
-  zlartg(h[col], h[col + 1], &c, &s, &r);
-  g.G[2 * col] = make_double2(c, 0.0);
-  g.G[2 * col + 1] = s;
-  h[col] = r;
-  h[col + 1] = make_double2(0.0, 0.0);
-  const double2 Sc = g.S[col];
+  zlartg(n0, hsub, &c, &s, &r);
+  const double2 Sc = in.Sc;
   const double2 tmp = cmul(make_double2(-s.x, s.y), Sc);  // -conj(s) * S[col]
-  g.S[col] = cscale(Sc, c);
-  g.S[col + 1] = tmp;
   const double presid = hypot(tmp.x, tmp.y);
-  g.status[0] = presid;
-  g.status[1] = brk;
-  g.status[2] = h0;
-  g.status[3] = h1;
-  double* st = g.status_it + 4 * col;
-  st[0] = presid;
-  st[1] = brk;
-  st[2] = h0;
-  st[3] = h1;
-  g.ctrl[1] = col;
-  if (presid <= ptol || brk != 0.0 || col >= stop_col) g.ctrl[0] = 1;
+  const bool stop = presid <= ptol || brk != 0.0 || col >= stop_col;
+  if (l0) {
+    g.G[2 * col] = make_double2(c, 0.0);
+    g.G[2 * col + 1] = s;
+    h[col] = r;
+    h[col + 1] = make_double2(0.0, 0.0);
+    g.S[col] = cscale(Sc, c);
+    g.S[col + 1] = tmp;
+    g.status[0] = presid;
+    g.status[1] = brk;
+    g.status[2] = h0;
+    g.status[3] = h1;
+    double* st = g.status_it + 4 * col;
+    st[0] = presid;
+    st[1] = brk;
+    st[2] = h0;
+    st[3] = h1;
+    g.ctrl[1] = col;
+    if (stop) g.ctrl[0] = 1;
+  }
+  return stop;
 }
 
-// column `col` from the reduced dots rd and |w_new|^2 = rn0 (lane 0)
+// column `col` from the reduced dots rd and |w_new|^2 = rn0 (one wave: entry k on lane k); rd,
+// the scales and the finish's operands are loaded together
 __device__ void column_from_sums(const GivensState& g, int col, const double* rd, double rn0,
                                  double eps, double ptol, int stop_col) {
-  const int R1 = g.restart + 1;
-  double2* h = g.H + (size_t)col * R1;
-  for (int k = 0; k <= col; ++k) h[k] = cscale(make_double2(rd[2 * k], rd[2 * k + 1]), g.vscale[k]);
-  const double h0 = sqrt(rd[2 * (col + 1)]);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int kc = min(lane, col);
+  const double2 dk = make_double2(rd[2 * kc], rd[2 * kc + 1]);
+  const double vk = g.vscale[kc];
+  const double h0sq = rd[2 * (col + 1)];
+  const ColIn in = load_col_in(g, col);
+  const double2 hk = lane <= col ? cscale(dk, vk) : make_double2(0.0, 0.0);
+  const double h0 = sqrt(h0sq);
   const double h1 = sqrt(rn0);
-  gmres_finish_column(g, col, h0, h1, 1.0 / h1, eps, ptol, stop_col);
+  gmres_finish_column(g, col, hk, in, h0, h1, 1.0 / h1, eps, ptol, stop_col);
 }
 
 __global__ void gmres_column_kernel(GivensState g, int col, const double* rd, const double* rn,
                                     const double* npart, int ncount, double eps, double ptol,
                                     int stop_col) {
   if (g.ctrl[0]) return;
-  double rn0;
-  if (npart) {
-    rn0 = wave_reduce_like_block(npart, ncount, kMaxNorms);
-  }
-  if (threadIdx.x != 0) return;
-  if (!npart) rn0 = rn[0];
-  column_from_sums(g, col, rd, rn0, eps, ptol, stop_col);
+  const double rn0 = npart ? wave_reduce_like_block(npart, ncount, kMaxNorms) : rn[0];
+  // (wave_reduce_like_block leaves the sum in lane 0: broadcast it)
+  column_from_sums(g, col, rd, npart ? rlane(rn0, 0) : rn0, eps, ptol, stop_col);
 }
 
 // One-allreduce iteration j (lagged normalisation, world > 1; see runtime.cpp hh_gmres).  The
@@ -398,34 +441,55 @@ __global__ void gmres_column_kernel(GivensState g, int col, const double* rd, co
 //       reach the solve.
 // The update (w -= sum_k d_k vscale[k]^2 u_k) follows with the exact vscale.  `final` (after the
 // cycle's last iteration): rd is unused and sig2 holds |u_j|^2 -- steps (a), (b) only.
+// One wave: entry k of a column on lane k (the sum of (d) in k order by readlane).
 __global__ void gmres_lag_kernel(GivensState g, int j, const double* rd, const double* sig2,
                                  int final_step, double eps, double ptol, int stop_col) {
-  if (g.ctrl[0] || threadIdx.x != 0) return;
+  const int lane = threadIdx.x & (kWave - 1);
   const int R1 = g.restart + 1;
-  double vj = g.vscale[0];
+  // every operand loaded up front, from clamped addresses (the finish of column j-1 and the start
+  // of column j read disjoint words: the finish writes only vscale[j], which the start takes
+  // from vj): one memory latency per launch
+  const int col = max(j - 1, 0);
+  const int stopped = g.ctrl[0];
+  const double sig = *sig2;
+  const double vs0 = g.vscale[0], vcol = g.vscale[col], scol = g.sscale[col], sj_ = g.sscale[j];
+  const double h0c = g.status_it[4 * col + 2];  // stored when the column was started
+  const double2 hk0 = g.H[(size_t)col * R1 + min(lane, col)];  // (previous launch)
+  const ColIn in = load_col_in(g, col);
+  const int kj = min(lane, j);
+  const double vkj = g.vscale[kj];
+  const double* rdp = rd ? rd : sig2;  // (final step: rd unused, any valid words of red)
+  const double2 d = make_double2(rdp[2 * kj], rdp[2 * kj + 1]);
+  const double w2 = rdp[2 * (j + 1)];
+  if (stopped) return;
+  double vj = vs0;
   if (j >= 1) {
-    const double sj = sqrt(*sig2);
+    const double sj = sqrt(sig);
     vj = 1.0 / sj;
-    const int col = j - 1;
-    const double f = g.vscale[col] / g.sscale[col];
-    const double h0 = g.status_it[4 * col + 2];  // stored when the column was started
+    const double f = vcol / scol;
     const double h1 = sj * f;
-    gmres_finish_column(g, col, h0, h1, vj, eps, ptol, stop_col);
-    if (g.ctrl[0] || final_step) return;
+    const double2 hk = lane <= col ? hk0 : make_double2(0.0, 0.0);
+    const bool stop = gmres_finish_column(g, col, hk, in, h0c, h1, vj, eps, ptol, stop_col);
+    if (stop || final_step) return;
   }
-  const double f = vj / g.sscale[j];
+  const double f = vj / sj_;
   double2* h = g.H + (size_t)j * R1;
-  const double w2 = rd[2 * (j + 1)];
-  double rest = w2;
-  for (int k = 0; k <= j; ++k) {
-    const double vk = k == j ? vj : g.vscale[k];
-    const double2 d = make_double2(rd[2 * k], rd[2 * k + 1]);
-    h[k] = cscale(cscale(d, vk), f);
-    rest -= cabs2(d) * vk * vk;
+  double tv = 0.0, tw = 0.0;
+  if (lane <= j) {
+    const double vk = lane == j ? vj : vkj;
+    h[lane] = cscale(cscale(d, vk), f);
+    tv = cabs2(d) * vk;
+    tw = vk;
   }
-  g.status_it[4 * j + 2] = sqrt(w2) * f;
-  const double floor2 = fmax(w2 * 1e-28, 1e-300);
-  g.sscale[j + 1] = 1.0 / sqrt(fmax(rest, floor2));
+  // rest -= |d_k|^2 v_k^2 in k order, the last multiply fused as the one-lane loop's compiled
+  // form fused it (fp-contract), explicitly here
+  double rest = w2;
+  for (int k = 0; k <= j; ++k) rest = fma(-rlane(tv, k), rlane(tw, k), rest);
+  if (lane == 0) {
+    g.status_it[4 * j + 2] = sqrt(w2) * f;
+    const double floor2 = fmax(w2 * 1e-28, 1e-300);
+    g.sscale[j + 1] = 1.0 / sqrt(fmax(rest, floor2));
+  }
 }
 
 __global__ void gmres_start_kernel(GivensState g, const double* red, int idx_r, int idx_m) {
