@@ -29,6 +29,7 @@
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
 #include "hh_error.hpp"
+#include "hh_wave.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -88,9 +89,10 @@ struct Shared {  // LDS layout (carved from dynamic shared memory; see small_cyc
 // sees the half that came with it; nothing needs ordering or draining).  The tag is the launch's
 // sequence number and the round (epoch), so granules of an earlier round or launch never match.
 //  1. every workgroup has stored its row of partial sums as granules, part[par][g][.];
-//  2. column c is reduced by workgroup c mod G: thread q polls row q's two granules of the
-//     column until both carry the round's tag, then the rows are summed in row order (32 runs
-//     of consecutive rows, the run sums in run order) and the sum is stored as two granules;
+//  2. column c is reduced by workgroup c mod G, on its first wave: lane l polls the two
+//     granules of rows l, l + 64, ... until all carry the round's tag, sums them in that order,
+//     and the 64 lane sums are added by DPP lane moves in a fixed order (no barrier, no LDS);
+//     the sum is stored as two granules;
 //  3. every workgroup polls the `cols` sums' granules until tagged.
 // Two hops (partials -> reducer -> everyone) and no serialised atomics.  The arithmetic order is
 // fixed: identical sums on every workgroup and every run.  Rows and sums are double-buffered by
@@ -98,7 +100,7 @@ struct Shared {  // LDS layout (carved from dynamic shared memory; see small_cyc
 // before every workgroup has read them.  Returns false on timeout (every workgroup then leaves).
 constexpr int kRuns = 32;
 constexpr int kBatch = 8;  // LDS loads a thread keeps in flight in its reduction loops
-constexpr int kRunMax = (kSmallThreads + kRuns - 1) / kRuns;  // rows per run, at most
+constexpr int kRowsPerLane = (kSmallThreads + kWave - 1) / kWave;  // reducer rows per lane
 // sh.red: [0, kRedRuns) the partial-sum segments of the caller, [kRedRuns, + kRuns) run sums
 constexpr int kRedRuns = 2 * (kSmallThreads + kWave);
 struct ArArgs {
@@ -140,36 +142,34 @@ __device__ bool allreduce_rows(const ArArgs& ar, int par, unsigned epoch, int co
   const int G = ar.G, g = blockIdx.x;
   const int t = threadIdx.x;
   const unsigned tag = gran_tag(ar.seq, epoch);
-  const int run = (G + kRuns - 1) / kRuns;  // rows per summing thread (<= 16)
   bool ok = true;
+  (void)red;
   for (int c = g; c < cols; c += G) {
-    if (t < kRuns) {
-      // this thread's run of rows, all granules in flight together, polled until tagged;
-      // then summed in row order
-      const int q0 = t * run, q1 = min(G, q0 + run);
+    if (t < kWave) {
+      // wave 0: lane l polls rows l, l + 64, ... (all granules in flight together) until
+      // tagged, sums them in row order, then the 64 lane sums by DPP (fixed order, no barrier,
+      // no LDS); lane 63 publishes the column's sum
       double s = 0.0;
       unsigned spins = 0;
       for (;;) {
-        unsigned long long v[2 * kRunMax];
+        unsigned long long v[2 * kRowsPerLane];
 #pragma unroll
-        for (int i = 0; i < kRunMax; ++i) {
-          const unsigned long long* p =
-              ar.part + ((size_t)par * G + min(q0 + i, q1 - 1)) * 2 * kPStride + 2 * c;
-          v[2 * i] = i < q1 - q0 ? __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-          v[2 * i + 1] = i < q1 - q0 ? __hip_atomic_load((gu64*)(p + 1), __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        for (int i = 0; i < kRowsPerLane; ++i) {
+          const int q = min(t + kWave * i, G - 1);
+          const unsigned long long* p = ar.part + ((size_t)par * G + q) * 2 * kPStride + 2 * c;
+          v[2 * i] = __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v[2 * i + 1] =
+              __hip_atomic_load((gu64*)(p + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         bool all = true;
 #pragma unroll
-        for (int i = 0; i < kRunMax; ++i)
-          if (i < q1 - q0)
-            all = all && (unsigned)(v[2 * i] >> 32) == tag &&
-                  (unsigned)(v[2 * i + 1] >> 32) == tag;
+        for (int i = 0; i < kRowsPerLane; ++i)
+          if (t + kWave * i < G)
+            all = all && (unsigned)(v[2 * i] >> 32) == tag && (unsigned)(v[2 * i + 1] >> 32) == tag;
         if (all) {
 #pragma unroll
-          for (int i = 0; i < kRunMax; ++i)
-            if (i < q1 - q0)
+          for (int i = 0; i < kRowsPerLane; ++i)
+            if (t + kWave * i < G)
               s += __longlong_as_double(
                   (long long)((v[2 * i] << 32) | (v[2 * i + 1] & 0xffffffffull)));
           break;
@@ -180,13 +180,8 @@ __device__ bool allreduce_rows(const ArArgs& ar, int par, unsigned epoch, int co
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      red[kRedRuns + t] = s;
-    }
-    __syncthreads();
-    if (t == 0) {
-      double s = 0.0;
-      for (int q = 0; q < kRuns; ++q) s += red[kRedRuns + q];
-      st_gran(ar.sums + (size_t)epoch * 2 * kPStride + 2 * c, tag, s);
+      s = wave_sum_to_63(s);
+      if (t == kWave - 1) st_gran(ar.sums + (size_t)epoch * 2 * kPStride + 2 * c, tag, s);
       if (t_reduced && c == 0) *t_reduced = wall_clock64();  // (profiling: column 0 summed)
     }
   }
@@ -203,12 +198,6 @@ __device__ bool allreduce_rows(const ArArgs& ar, int par, unsigned epoch, int co
   return true;
 }
 
-// fixed-order wave sum (xor butterfly; addition commutes, so every lane gets the same bits)
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = kWave / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
 
 // LAPACK zlartg main branch (krylov.hip), by value: each branch yields all three results (no
 // output pointers -- a branch-selected store target would become a scratch slot)
@@ -242,16 +231,6 @@ __device__ __forceinline__ Rot zlartg_s(double2 f, double2 g) {
   return o;
 }
 
-// lane k's double, on every lane
-__device__ __forceinline__ double rlane(double v, int k) {
-  const long long u = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffff), k);
-  const int hi = __builtin_amdgcn_readlane((int)(u >> 32), k);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double2 rlane2(double2 v, int k) {
-  return make_double2(rlane(v.x, k), rlane(v.y, k));
-}
 
 // The Givens workgroup's wave: complete column `col` with its subdiagonal h1 (krylov.hip
 // gmres_finish_column) -- every lane computes the same values, lane 0 stores them.  Lane k
@@ -843,8 +822,8 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
       const l2* ul = Urow(last, 1);
       double s = 0.0;
       for (int p = t; p < n; p += kWave) s = fma(ul[p].x, ul[p].x, fma(ul[p].y, ul[p].y, s));
-      s = wave_sum(s);
-      if (t == 0)
+      s = wave_sum_to_63(s);
+      if (t == kWave - 1)
         st_gran(ar.part + ((size_t)par * G + g) * 2 * kPStride, gran_tag(a.seq, epoch + 1), s);
     }
     epoch++;
@@ -964,10 +943,10 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
     r2 = cabs2(rr);
     m2 = cabs2(mr);
   }
-  // row sums: per wave by butterfly, then the waves in order
+  // row sums: per wave by DPP lane moves, then the waves in order
   {
-    const double r2w = wave_sum(r2), m2w = wave_sum(m2);
-    if ((t & (kWave - 1)) == 0) {
+    const double r2w = wave_sum_to_63(r2), m2w = wave_sum_to_63(m2);
+    if ((t & (kWave - 1)) == kWave - 1) {
       sh.red[2 * (t / kWave)] = r2w;
       sh.red[2 * (t / kWave) + 1] = m2w;
     }

@@ -14,6 +14,7 @@
 
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
+#include "hh_wave.hpp"
 
 namespace hh {
 namespace {
@@ -62,16 +63,6 @@ __device__ __forceinline__ void block_reduce_vec(double (&v)[NV], double* partia
   }
 }
 
-// lane k's double, on every lane of the wave
-__device__ __forceinline__ double rlane(double v, int k) {
-  const long long u = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffff), k);
-  const int hi = __builtin_amdgcn_readlane((int)(u >> 32), k);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double2 rlane2(double2 v, int k) {
-  return make_double2(rlane(v.x, k), rlane(v.y, k));
-}
 
 template <bool SC1 = false>
 __device__ double wave_reduce_like_block(const double* partials, int count, int width);

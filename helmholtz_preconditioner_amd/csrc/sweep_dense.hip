@@ -28,6 +28,7 @@
 // with S_m = BS_m R1_i, N_m = BN_m R1_i (c3 / c4 of code.py:130-154).  w is the result.
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
+#include "hh_wave.hpp"
 #include "sweep.hpp"
 #include "hh_error.hpp"
 
@@ -45,26 +46,6 @@ __device__ __forceinline__ void ufor(F&& f) {
   }
 }
 
-// Sum over the 64 lanes of a wave by DPP lane moves (no LDS round trips, unlike a shuffle
-// butterfly: 12 dependent ds_bpermute per double), fixed order; the total lands in lane 63.
-// Pairs, quads, 8 (half-row mirror), 16 (row mirror), then row 0 -> 1 and row 2 -> 3
-// (row_bcast:15), rows 0-1 -> 2-3 (row_bcast:31).  Lanes a move does not write read 0.
-template <int CTRL, int ROWS>
-__device__ __forceinline__ double dpp_mov(double x) {
-  const long long u = __double_as_longlong(x);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(u & 0xffffffff), CTRL, ROWS, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, ROWS, 0xf, false);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double wave_sum_to_63(double v) {
-  v += dpp_mov<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
-  v += dpp_mov<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
-  v += dpp_mov<0x141, 0xf>(v);  // row_half_mirror
-  v += dpp_mov<0x140, 0xf>(v);  // row_mirror
-  v += dpp_mov<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
-  v += dpp_mov<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
-  return v;
-}
 
 constexpr int kSetupThreads = 256;  // RHS columns per setup block
 
