@@ -45,10 +45,10 @@ __device__ __forceinline__ double2 csel(bool c, double2 a, double2 b) {
 }
 
 constexpr int kSmallThreads = 256;    // grid rows at most (n <= 256)
-// Block size: P = min(4, 512 / npad) copies of the row's npad threads.  The stencil, x update
-// and residual need one thread per column; with P >= 3 the basis update gives each of the three
-// rows (ghost, own, ghost) a thread group of its own and the partial sums get more segments,
-// so all four SIMDs of the CU work instead of one or two waves (npad = 128: 2 waves).
+// Block size: P copies of the row's npad threads (P = 2 by default, up to 4 = 512 / 128).  The
+// stencil, x update and residual need one thread per column; the partial sums get P times the
+// segments, and with P >= 3 the basis update gives each of the three rows (ghost, own, ghost) a
+// thread group of its own (measured slower at 128^2: the block barriers of 8 waves).
 constexpr int kSmallBlock = 512;
 constexpr int kPStride = kSmallCols;  // partial-sum columns (global layout)
 constexpr unsigned kSpinLimit = 1u << 22;  // ~1 s of polling: a barrier wait is microseconds
@@ -1042,9 +1042,11 @@ void launch_one(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds, hipS
 
 void launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi, hipStream_t s) {
   const int npad = (a.n + kWave - 1) / kWave * kWave;
-  // (HH_SMALL_WIDE=0: one copy, the round-2 r02qc shape, for A/B timing)
-  static const bool wide = !(getenv("HH_SMALL_WIDE") && atoi(getenv("HH_SMALL_WIDE")) == 0);
-  const int threads = npad * (wide ? std::max(1, std::min(4, kSmallBlock / npad)) : 1);
+  // at most 2 copies of the row's threads by default: 9.76-9.80 us/it at 128^2 against
+  // 9.80-9.91 for 1 and 9.96-10.14 for 4 (the row-split update; block barriers of 8 waves)
+  // (profiles/r02z_*); HH_SMALL_WIDE=c selects up to c copies, for A/B timing
+  static const int wide = getenv("HH_SMALL_WIDE") ? std::max(1, atoi(getenv("HH_SMALL_WIDE"))) : 2;
+  const int threads = npad * std::max(1, std::min(wide, kSmallBlock / npad));
   const size_t lds = small_cycle_lds_bytes(a.n, a.restart);
   const dim3 grid(a.n + 1), block(threads);  // + the Givens workgroup
   if (const_c) {

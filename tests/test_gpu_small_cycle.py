@@ -7,6 +7,8 @@ cycles), Jacobi, a converging run (adaptive ptol, several cycles, info 0), nonze
 maxiter ending inside a cycle, restart 1 and 7, ragged n (block sizes not a multiple of the
 wave, one-row grids), both media kinds.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -149,3 +151,38 @@ def test_small_cycle_queued_cycles(ctx, case):
         for u, v in zip(c1, c2):
             assert np.linalg.norm(u - v) <= 1e-6 * np.linalg.norm(v)
     assert np.linalg.norm(x1 - x2) <= 1e-6 * np.linalg.norm(x2)
+
+
+@pytest.mark.parametrize("wide", ["1", "4"])
+def test_small_cycle_block_widths(wide):
+    """The whole-cycle kernel with 1 and 4 copies of the row's threads (HH_SMALL_WIDE; 4 takes
+    the row-split basis update) against the regular cycle, in a child process (the width is read
+    once per process)."""
+    import subprocess
+    import sys
+    code = r'''
+import numpy as np, sys
+sys.path.insert(0, ".")
+import helmholtz_preconditioner_amd as H
+from oracle import helmholtz_oracle as O
+for n, pre in ((128, None), (37, "jacobi"), (65, None)):
+    om, h, eta = O.problem_params(n, 6, 3.0, 2.0)
+    A = H.build_A_matrix(6, 61.0, eta, om, h, n, H.init_c1_mat(.5, .5, n))
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    out = []
+    for mode in ("on", "off"):
+        A.small_cycle(mode)
+        out.append(H.gmres(A, f, rtol=1e-3, restart=20, maxiter=45, M=pre,
+                           callback=lambda r: None, callback_type="legacy", return_history=True))
+    (x1, i1, h1), (x2, i2, h2) = out
+    assert i1 == i2 and len(h1) == len(h2), (n, i1, i2)
+    # (three restart cycles in two summation orders: the 1e-6 contract of DESIGN 6)
+    assert np.all(np.abs(h1 - h2) <= 1e-6 * np.abs(h2) + 1e-15), n
+    assert np.linalg.norm(x1 - x2) <= 1e-6 * np.linalg.norm(x2), n
+print("ok")
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HH_SMALL_WIDE=wide)
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
