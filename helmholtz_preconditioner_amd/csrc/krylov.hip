@@ -207,22 +207,38 @@ __global__ __launch_bounds__(kT) void xupdate_kernel(const double2* __restrict__
   }
 }
 
-// One block per output column: out[k] = sum_b partials[b*width + k] in fixed order.
+// One block per output column: out[k] = sum_b partials[b*width + k] in fixed order: each thread
+// its b = t, t + 256, ... in ascending order (the loads of 8 of them issued together), then the
+// pairwise tree sh[t] += sh[t + off], off = 128 .. 1 -- its last six levels by wave shuffles in the
+// same operand order (two block barriers instead of eight; wave_reduce_like_block emulates it).
 __global__ __launch_bounds__(kT) void reduce_kernel(const double* __restrict__ partials, int count,
                                                     int width, double* __restrict__ out,
                                                     const int* stop) {
   if (stop && *stop) return;
   __shared__ double sh[kT];
   const int k = blockIdx.x;
+  const int t = threadIdx.x;
+  constexpr int kChunk = 8;
   double s = 0.0;
-  for (int b = threadIdx.x; b < count; b += kT) s += partials[(size_t)b * width + k];
-  sh[threadIdx.x] = s;
-  __syncthreads();
-  for (int off = kT / 2; off > 0; off >>= 1) {
-    if (threadIdx.x < off) sh[threadIdx.x] += sh[threadIdx.x + off];
-    __syncthreads();
+  for (int b0 = t; b0 < count; b0 += kChunk * kT) {
+    double v[kChunk];
+#pragma unroll
+    for (int i = 0; i < kChunk; ++i)
+      v[i] = partials[(size_t)min(b0 + i * kT, count - 1) * width + k];
+#pragma unroll
+    for (int i = 0; i < kChunk; ++i)
+      if (b0 + i * kT < count) s += v[i];
   }
-  if (threadIdx.x == 0) out[k] = sh[0];
+  sh[t] = s;
+  __syncthreads();
+  if (t < kT / 2) sh[t] += sh[t + kT / 2];
+  __syncthreads();
+  if (t < kWave) {
+    double x = sh[t] + sh[t + kWave];  // (off = 64)
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) x += __shfl_down(x, off);
+    if (t == 0) out[k] = x;
+  }
 }
 
 __global__ void add_small_kernel(const double* in, double* out, int count, const int* stop) {
@@ -293,17 +309,28 @@ template <bool SC1>
 __device__ double wave_reduce_like_block(const double* partials, int count, int width) {
   static_assert(kT == 4 * kWave, "four strided sums per lane emulate a 256-thread block");
   const int l = threadIdx.x & (kWave - 1);
-  double s[4];
+  // the four strided sums, each in ascending b; the loads of a chunk of 8 x 256 blocks issued
+  // together from clamped addresses (one memory latency per chunk: count <= 2048 is one chunk;
+  // a load per iteration would wait a round trip each -- 11 us for 1024 partials)
+  constexpr int kChunk = 8;
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int b0 = l; b0 < count; b0 += kChunk * kT) {
+    double v[4][kChunk];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    double acc = 0.0;
-    for (int b = l + q * kWave; b < count; b += kT) {
-      const double* p = partials + (size_t)b * width;
-      acc += SC1 ? __longlong_as_double((long long)__hip_atomic_load(
-                       (gu64k*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                 : *p;
-    }
-    s[q] = acc;
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < kChunk; ++i) {
+        const int b = min(b0 + q * kWave + i * kT, count - 1);
+        const double* p = partials + (size_t)b * width;
+        v[q][i] = SC1 ? __longlong_as_double((long long)__hip_atomic_load(
+                            (gu64k*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                      : *p;
+      }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < kChunk; ++i)
+        if (b0 + q * kWave + i * kT < count) s[q] += v[q][i];
   }
   s[0] += s[2];  // off = 128: threads l and l + 64
   s[1] += s[3];
@@ -394,27 +421,45 @@ __device__ bool gmres_finish_column(const GivensState& g, int col, double2 hk, c
 
 // column `col` from the reduced dots rd and |w_new|^2 = rn0 (one wave: entry k on lane k); rd,
 // the scales and the finish's operands are loaded together
-__device__ void column_from_sums(const GivensState& g, int col, const double* rd, double rn0,
-                                 double eps, double ptol, int stop_col) {
+struct SumsIn {  // a column's reduced dots (entry `lane`), scale and |w|^2, loaded together
+  double2 dk;
+  double vk, h0sq;
+  ColIn in;
+};
+__device__ __forceinline__ SumsIn load_sums_in(const GivensState& g, int col, const double* rd) {
   const int lane = threadIdx.x & (kWave - 1);
   const int kc = min(lane, col);
-  const double2 dk = make_double2(rd[2 * kc], rd[2 * kc + 1]);
-  const double vk = g.vscale[kc];
-  const double h0sq = rd[2 * (col + 1)];
-  const ColIn in = load_col_in(g, col);
-  const double2 hk = lane <= col ? cscale(dk, vk) : make_double2(0.0, 0.0);
-  const double h0 = sqrt(h0sq);
+  SumsIn s;
+  s.dk = make_double2(rd[2 * kc], rd[2 * kc + 1]);
+  s.vk = g.vscale[kc];
+  s.h0sq = rd[2 * (col + 1)];
+  s.in = load_col_in(g, col);
+  return s;
+}
+__device__ void column_from_sums(const GivensState& g, int col, const SumsIn& s, double rn0,
+                                 double eps, double ptol, int stop_col) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const double2 hk = lane <= col ? cscale(s.dk, s.vk) : make_double2(0.0, 0.0);
+  const double h0 = sqrt(s.h0sq);
   const double h1 = sqrt(rn0);
-  gmres_finish_column(g, col, hk, in, h0, h1, 1.0 / h1, eps, ptol, stop_col);
+  gmres_finish_column(g, col, hk, s.in, h0, h1, 1.0 / h1, eps, ptol, stop_col);
+}
+__device__ void column_from_sums(const GivensState& g, int col, const double* rd, double rn0,
+                                 double eps, double ptol, int stop_col) {
+  column_from_sums(g, col, load_sums_in(g, col, rd), rn0, eps, ptol, stop_col);
 }
 
 __global__ void gmres_column_kernel(GivensState g, int col, const double* rd, const double* rn,
                                     const double* npart, int ncount, double eps, double ptol,
                                     int stop_col) {
-  if (g.ctrl[0]) return;
+  // the column's operands and the stop flag requested before the norm's partials are summed
+  // (one memory latency for all of them)
+  const SumsIn s = load_sums_in(g, col, rd);
+  const int stopped = g.ctrl[0];
   const double rn0 = npart ? wave_reduce_like_block(npart, ncount, kMaxNorms) : rn[0];
+  if (stopped) return;
   // (wave_reduce_like_block leaves the sum in lane 0: broadcast it)
-  column_from_sums(g, col, rd, npart ? rlane(rn0, 0) : rn0, eps, ptol, stop_col);
+  column_from_sums(g, col, s, npart ? rlane(rn0, 0) : rn0, eps, ptol, stop_col);
 }
 
 // One-allreduce iteration j (lagged normalisation, world > 1; see runtime.cpp hh_gmres).  The
