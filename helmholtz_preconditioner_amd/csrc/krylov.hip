@@ -42,12 +42,12 @@ __device__ __forceinline__ void block_reduce_vec(double (&v)[NV], double* partia
   __shared__ double red[NV][kT / kWave];
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
+  // wave sums by DPP lane moves (VALU only; the xor butterfly took 12 dependent ds_bpermute per
+  // value: ~500 LDS permutes per wave for the 41 values of a 20-vector multidot)
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    double x = v[k];
-#pragma unroll
-    for (int off = kWave / 2; off > 0; off >>= 1) x += __shfl_xor(x, off);
-    if (lane == 0) red[k][wave] = x;
+    const double x = wave_sum_to_63(v[k]);
+    if (lane == kWave - 1) red[k][wave] = x;
   }
   __syncthreads();
   for (int k = threadIdx.x; k < NV; k += kT) {
