@@ -91,7 +91,7 @@ constexpr int kRedReport = 389;
 constexpr int kRedOuter = 400;  // [400, 408): the small cycle's restart-loop state (device only)
 // whole-cycle launches queued behind each other (one host sync per batch); each reports into its
 // own slot of the host mirror, status_h + (1 + i) kRedDoubles
-constexpr int kSmallBatch = 8;
+constexpr int kSmallBatch = 16;
 static_assert(kRedOuter >= kRedReport && kRedOuter + kOuterDoubles <= kRedDoubles, "red layout");
 }  // namespace
 

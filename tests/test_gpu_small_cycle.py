@@ -116,7 +116,7 @@ def test_small_cycle_queued_cycles(ctx, case):
     om, h, eta = O.problem_params(n, b, wn, 2.0)
     A = H.build_A_matrix(b, C, eta, om, h, n, medium("c2", n), context=ctx)
     f = O.init_f1_mat(.5, .125, om, n).ravel()
-    kw = {"cycles": dict(rtol=1e-12, restart=5, maxiter=9),
+    kw = {"cycles": dict(rtol=1e-12, restart=5, maxiter=19),  # (16 + 3: two batches)
           "converge": dict(rtol=1e-4, restart=10, maxiter=400, M="jacobi"),
           "xcb": dict(rtol=1e-4, restart=10, maxiter=400, M="jacobi")}[case]
     out = []
@@ -139,7 +139,7 @@ def test_small_cycle_queued_cycles(ctx, case):
     (x1, i1, h1, c1), (x2, i2, h2, c2) = out
     assert i1 == i2
     if case == "cycles":
-        assert i1 == 9 and len(h1) == len(h2) == 45
+        assert i1 == 19 and len(h1) == len(h2) == 95, (i1, len(h1), len(h2))
     if case == "converge":
         assert i1 == 0 and len(h1) == len(h2) and len(h1) > 10
     if h1 is not None:
