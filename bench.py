@@ -321,6 +321,50 @@ def gmres_bytes(args, its, bpp, N):
     return sum((bpp + pre) * N + 16 * (j + 2) * N + 16 * (j + 3) * N for j in js), fused
 
 
+def span_breakdown(H, A, ctx, args, its, f_host, R, applies=20):
+    """Where an N-rank apply / GMRES iteration spends its time, per rank (diagnostic, after
+    the timed legs, so the timed numbers carry no event overhead): HIP events around the halo
+    exchange, boundary and interior kernels, allreduces and Krylov kernels on the streams they
+    run on (hh_op_read_timing), as microseconds per apply and per inner iteration, max over
+    ranks (the slowest rank sets the pace of every collective)."""
+    import numpy as np
+    from helmholtz_preconditioner_amd import _ffi
+    names = _ffi.SPAN_NAMES
+    x, y = [A.vector() for _ in range(R)], [A.vector() for _ in range(R)]
+    for k, v in enumerate(x):
+        v.fill_hash(7 + k)
+    A.set_timing(True)
+    A.time_apply(x, y, applies)
+    ap = A.read_timing()
+    for v in x + y:
+        v.close()
+    out = {"source": "HIP events per span on each rank's own streams (hh_op_read_timing), one "
+                     "extra untimed run after the timed legs; max over ranks",
+           "unit": "us"}
+    vec = [1e3 * ap[k][0] / applies for k in names]
+    gm = None
+    if not args.no_gmres and its > 0:
+        f = A.vector(f_host)
+        M = make_precond(H, A, args.precond, args.sl_sweeps)
+        A.read_timing()
+        _, _, hist = H.gmres(A, f, rtol=1e-14, restart=args.restart, maxiter=its, M=M,
+                             callback=lambda r: None, callback_type="legacy",
+                             return_history=True)
+        gm = A.read_timing()
+        f.close()
+        k = max(1, len(hist))
+        vec += [1e3 * gm[n][0] / k for n in names] + [gm["allreduce"][1] / k]
+    A.set_timing(False)
+    mx = ctx.allreduce_max(np.asarray(vec, dtype=np.float64))
+    out["spmv_per_apply"] = {k: round(float(mx[i]), 3) for i, k in enumerate(names)
+                             if k in ("halo", "boundary", "interior", "halo_wait")}
+    if gm is not None:
+        m = len(names)
+        out["gmres_per_iteration"] = {k: round(float(mx[m + i]), 3) for i, k in enumerate(names)}
+        out["gmres_per_iteration"]["allreduces"] = round(float(mx[2 * m]), 3)
+    return out
+
+
 def same_n_leg(H, dist, args, ctx, rank, world, wd):
     """Strong scaling at the fixed BASELINE grid in the same job: the grid on all `world`
     ranks, then on rank 0 alone with a world-1 context on its own GPU (the other ranks wait at
@@ -345,6 +389,9 @@ def same_n_leg(H, dist, args, ctx, rank, world, wd):
         if not args.no_gmres and its > 0:
             k, tg, _ = timed_gmres(H, A, c, local_f1(omega, n, j0, j1), args, its)
             out["gmres_iters_per_s"] = k / tg
+        if w > 1:
+            wd.phase(f"same-N leg: span breakdown on {w} ranks", 300)
+            out["breakdown"] = span_breakdown(H, A, c, args, its, local_f1(omega, n, j0, j1), R)
         A.close()
         return out
 
@@ -371,6 +418,8 @@ def same_n_leg(H, dist, args, ctx, rank, world, wd):
                  "single_gpu_ms_per_step": round(single["spmv_ms_per_step"], 5),
                  "speedup_same_n": round(single["spmv_ms_per_step"] / multi["spmv_ms_per_step"], 3)},
     }
+    if "breakdown" in multi:
+        block["breakdown"] = multi["breakdown"]
     if "gmres_iters_per_s" in multi:
         block["gmres"] = {"iterations": its, "precond": args.precond,
                           "iters_per_s": round(multi["gmres_iters_per_s"], 3),

@@ -37,6 +37,8 @@ GMRES_CYCLE_CALLBACK = ctypes.CFUNCTYPE(c_int, c_void_p, c_long)
 GMRES_HISTORY_CALLBACK = ctypes.CFUNCTYPE(c_int, c_void_p, c_long, c_int,
                                           ctypes.POINTER(ctypes.c_double))
 HH_ERR_ABORTED = -6
+SPAN_NAMES = ("halo", "boundary", "interior", "halo_wait", "allreduce", "column", "multidot",
+              "update")  # HH_SPAN_* order (include/helmholtz_amd.h)
 ABI_VERSION = 2
 
 
@@ -85,6 +87,9 @@ SIGNATURES = [
     ("hh_op_sl_fusion", c_int, [c_void_p, c_int]),
     ("hh_op_set_krylov_mode", c_int, [c_void_p, c_int]),
     ("hh_op_set_small_cycle", c_int, [c_void_p, c_int]),
+    ("hh_op_last_solve_path", c_int, [c_void_p, c_ip]),
+    ("hh_op_set_timing", c_int, [c_void_p, c_int]),
+    ("hh_op_read_timing", c_int, [c_void_p, c_dp, c_lp]),
     ("hh_op_small_cycle_profile", c_int, [c_void_p, c_int, c_dp]),
     ("hh_op_small_cycle_tail_profile", c_int, [c_void_p, c_dp]),
     ("hh_op_tune", c_int, [c_void_p, c_int, c_int, c_int]),

@@ -1021,7 +1021,7 @@ bool small_cycle_eligible(int n, int restart, int device_cus) {
 }
 
 template <bool C, bool J>
-void launch_one(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s) {
+hipError_t launch_one(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s) {
   // dynamic LDS above 64 KB (gfx950 has 160 KB per CU, the kernel's static LDS included) must
   // be allowed per kernel, once
   static const hipError_t attr = [] {
@@ -1037,10 +1037,25 @@ void launch_one(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds, hipS
     fail(HH_ERR_HIP, "small-grid GMRES cycle: cannot enable %zu B of dynamic LDS (%s)", lds,
          hipGetErrorString(attr));
   }
-  hipLaunchKernelGGL((gmres_small_cycle_kernel<C, J>), grid, block, lds, s, a);
+  // Cooperative: the workgroups wait on each other (tagged granules), so all n + 1 must be
+  // resident at once; the runtime refuses a grid that cannot be (instead of the waits spinning
+  // to their bound) and the caller then takes the regular cycle.  HH_SMALL_COOP_REFUSE=1 makes
+  // this launch report the refusal without launching (tests the caller's fallback).
+  static const bool refuse = [] {
+    const char* e = std::getenv("HH_SMALL_COOP_REFUSE");
+    return e && e[0] == '1';
+  }();
+  if (refuse) return hipErrorCooperativeLaunchTooLarge;
+  SmallCycleArgs arg = a;
+  void* params[] = {&arg};
+  const hipError_t e = hipLaunchCooperativeKernel(
+      reinterpret_cast<const void*>(&gmres_small_cycle_kernel<C, J>), grid, block, params,
+      (unsigned)lds, s);
+  if (e != hipSuccess) (void)hipGetLastError();  // (reported by the caller, not a later check)
+  return e;
 }
 
-void launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi, hipStream_t s) {
+hipError_t launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi, hipStream_t s) {
   const int npad = (a.n + kWave - 1) / kWave * kWave;
   // at most 2 copies of the row's threads by default: 9.76-9.80 us/it at 128^2 against
   // 9.80-9.91 for 1 and 9.96-10.14 for 4 (the row-split update; block barriers of 8 waves)
@@ -1049,13 +1064,10 @@ void launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi, hipS
   const int threads = npad * std::max(1, std::min(wide, kSmallBlock / npad));
   const size_t lds = small_cycle_lds_bytes(a.n, a.restart);
   const dim3 grid(a.n + 1), block(threads);  // + the Givens workgroup
-  if (const_c) {
-    if (jacobi) launch_one<true, true>(a, grid, block, lds, s);
-    else launch_one<true, false>(a, grid, block, lds, s);
-  } else {
-    if (jacobi) launch_one<false, true>(a, grid, block, lds, s);
-    else launch_one<false, false>(a, grid, block, lds, s);
-  }
+  if (const_c) return jacobi ? launch_one<true, true>(a, grid, block, lds, s)
+                             : launch_one<true, false>(a, grid, block, lds, s);
+  return jacobi ? launch_one<false, true>(a, grid, block, lds, s)
+                : launch_one<false, false>(a, grid, block, lds, s);
 }
 
 }  // namespace hh

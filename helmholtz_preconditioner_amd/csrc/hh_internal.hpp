@@ -267,7 +267,9 @@ constexpr int kSmallRounds = kMaxProj + 8;  // all-reduce rounds per launch (<= 
 bool small_cycle_eligible(int n, int restart, int device_cus);
 size_t small_cycle_lds_bytes(int n, int restart);
 size_t small_cycle_scratch_doubles(int n);
-void launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi, hipStream_t s);
+// cooperative launch; returns the runtime's refusal (e.g. a grid that cannot be co-resident)
+// instead of throwing, so the caller can take the regular cycle before any state changed
+hipError_t launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi, hipStream_t s);
 // End of a cycle: triangular solve for y, ycoef_k = y_k * vscale_k.
 void launch_gmres_solve(const GivensState& g, int col, hipStream_t stream);
 

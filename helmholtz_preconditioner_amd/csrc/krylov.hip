@@ -73,12 +73,16 @@ __device__ void column_from_sums(const GivensState& g, int col, const double* rd
 // it releases them (device-scope fence) and takes a ticket; the block holding the last ticket
 // acquires and does what the next, one-block kernel would have done -- one launch boundary
 // and one kernel start fewer per GMRES iteration.  The ticket counter is re-armed by that block.
+// The ticket is an agent-scope acq_rel RMW behind a workgroup barrier: the release publishes
+// every wave's partial stores (the barrier orders them before thread 0's release), the acquire
+// makes the last block see all of them -- a guarantee of the memory model, not an assumption
+// about the multi-XCD hardware (HH_KRYLOV_FUSE only; no default path uses these kernels).
 __device__ __forceinline__ bool last_block(unsigned* counter) {
   __shared__ int last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 partial stores landed
   __syncthreads();
   if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add((gu32k*)counter, 1u, __ATOMIC_RELAXED,
+    last = __hip_atomic_fetch_add((gu32k*)counter, 1u, __ATOMIC_ACQ_REL,
                                   __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   return last;

@@ -114,6 +114,44 @@ struct Slab {
 };
 }  // namespace
 
+namespace {
+// Diagnostic span timing (hh_op_set_timing / hh_op_read_timing): HIP events recorded around the
+// pieces of an apply / GMRES iteration on the streams they run on, summed per category when
+// read.  Off by default (no event is recorded then); the N > 1 bench turns it on for one extra,
+// untimed solve to say where a rank's time goes.
+struct SpanTimer {
+  bool on = false;
+  std::vector<hipEvent_t> pool;  // created lazily, reused after each read
+  size_t used = 0;
+  struct Span {
+    int cat;
+    hipEvent_t a, b;
+    bool clamp;  // a wait: max(0, b - a) (b may complete before a)
+  };
+  std::vector<Span> spans;
+  hipEvent_t mark(hipStream_t s) {
+    if (used == pool.size()) {
+      hipEvent_t e = nullptr;
+      HIPC(hipEventCreate(&e));
+      pool.push_back(e);
+    }
+    hipEvent_t e = pool[used++];
+    HIPC(hipEventRecord(e, s));
+    return e;
+  }
+  void span(int cat, hipEvent_t a, hipEvent_t b, bool clamp = false) {
+    if (a && b) spans.push_back({cat, a, b, clamp});
+  }
+  void reset() {
+    spans.clear();
+    used = 0;
+  }
+  ~SpanTimer() {
+    for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+  }
+};
+}  // namespace
+
 struct hh_op {
   int refs = 1;  // the caller's handle + one per live vector (freed at zero)
   hh_ctx* ctx = nullptr;
@@ -207,6 +245,9 @@ struct hh_op {
   void* hist_user = nullptr;
   int grid_override = 0;
   hh_stats stats{};
+  SpanTimer timer;
+  int last_path = 0;  // the last hh_gmres: 0 regular cycle, 1 small-grid cycle kernel, 2 small
+                      // cycle refused at launch -> regular cycle (hh_op_last_solve_path)
 };
 
 struct hh_vec {
@@ -221,9 +262,19 @@ void ensure_scratch(hh_op* op) {
   if (!op->scrZ) op->scrZ = dalloc<double2>(op->nloc);
 }
 
+// timing marks (no-ops unless hh_op_set_timing enabled them)
+hipEvent_t tmark(hh_op* op, hipStream_t s) { return op->timer.on ? op->timer.mark(s) : nullptr; }
+void tspan(hh_op* op, int cat, hipEvent_t a, hipEvent_t b, bool clamp = false) {
+  if (op->timer.on) op->timer.span(cat, a, b, clamp);
+}
+
 void allreduce_sum_dev(hh_op* op, double* d, int count) {
   hh_ctx* c = op->ctx;
-  if (c->world > 1) c->comm->allreduce(d, count, false, c->stream);
+  if (c->world > 1) {
+    hipEvent_t a = tmark(op, c->stream);
+    c->comm->allreduce(d, count, false, c->stream);
+    tspan(op, HH_SPAN_ALLREDUCE, a, tmark(op, c->stream));
+  }
 }
 
 // Halo exchange for rank-local vector `in` and stencil launch of `epi` over all slabs.
@@ -235,13 +286,17 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
   const int S = (int)op->slabs.size();
   const bool lo_x = c->world > 1 && c->rank > 0;             // cross-rank halo below
   const bool hi_x = c->world > 1 && c->rank < c->world - 1;  // cross-rank halo above
+  hipEvent_t t_ready = nullptr, t_halo = nullptr, t_int1 = nullptr;
   if (lo_x || hi_x) {
     const Slab& s0 = op->slabs[0];
     const Slab& sl = op->slabs[S - 1];
+    t_ready = tmark(op, c->stream);  // (the input is complete: the exchange may start)
     c->comm->halo(lo_x ? in + s0.off : nullptr, lo_x ? s0.halo_lo_buf : nullptr,
                   hi_x ? in + sl.off + (size_t)(sl.nl - 1) * n : nullptr,
                   hi_x ? sl.halo_hi_buf : nullptr, 2 * sizeof(double) * (size_t)n, c->stream,
                   c->cstream, c->ev_in);
+    t_halo = tmark(op, c->cstream);
+    tspan(op, HH_SPAN_HALO, t_ready, t_halo);
   }
 
   auto make_args = [&](int si) {
@@ -294,6 +349,7 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
 
   // interior (independent of cross-rank halos) first, then the dependent boundary rows
   bool first = true;
+  hipEvent_t t_int0 = tmark(op, c->stream);
   for (int si = 0; si < S; ++si) {
     const Slab& s = op->slabs[si];
     const int r0 = (si == 0 && lo_x) ? 1 : 0;
@@ -303,6 +359,8 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
     if (first && op->tk1) HIPC(hipEventRecord(op->tk1, c->stream));
     first = false;
   }
+  t_int1 = tmark(op, c->stream);
+  tspan(op, HH_SPAN_INTERIOR, t_int0, t_int1);
   if (lo_x || hi_x) {
     // The boundary rows run on the halo stream, right behind the exchange (which it ordered
     // after everything the compute stream had queued), concurrently with the interior launch;
@@ -319,6 +377,9 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
       if (lo_x) launch_rows(0, 0, 1, 1, 0, hs);
       if (hi_x) launch_rows(S - 1, sl.nl - 1, sl.nl, 1, 0, hs);
     }
+    hipEvent_t t_bnd = tmark(op, hs);
+    tspan(op, HH_SPAN_BOUNDARY, t_halo, t_bnd);
+    tspan(op, HH_SPAN_HALO_WAIT, t_int1, t_bnd, true);  // compute stream idle behind the halo
     HIPC(hipEventRecord(c->ev_halo, hs));
     HIPC(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
   }
@@ -341,13 +402,17 @@ void run_sl2(hh_op* op, const double2* v, const double* vs, double2* out) {
   const int S = (int)op->slabs.size();
   const bool lo_x = c->world > 1 && c->rank > 0;
   const bool hi_x = c->world > 1 && c->rank < c->world - 1;
+  hipEvent_t t_halo = nullptr;
   if (lo_x || hi_x) {
     const Slab& s0 = op->slabs[0];
     const Slab& sl = op->slabs[S - 1];
+    hipEvent_t t_ready = tmark(op, c->stream);
     c->comm->halo(lo_x ? v + s0.off : nullptr, lo_x ? s0.halo2_lo : nullptr,
                   hi_x ? v + sl.off + (size_t)(sl.nl - 2) * n : nullptr,
                   hi_x ? sl.halo2_hi : nullptr, 2 * 2 * sizeof(double) * (size_t)n, c->stream,
                   c->cstream, c->ev_in);
+    t_halo = tmark(op, c->cstream);
+    tspan(op, HH_SPAN_HALO, t_ready, t_halo);
   }
   auto launch_rows = [&](int si, int r0, int r1, int rpb, int step, hipStream_t st) {
     if (r1 <= r0) return;
@@ -379,6 +444,7 @@ void run_sl2(hh_op* op, const double2* v, const double* vs, double2* out) {
     launch_sl2(op->const_c, a, st, op->variant);
   };
   // interior rows (no cross-rank halo needed: a band reads two rows beyond itself) first
+  hipEvent_t t_int0 = tmark(op, c->stream);
   for (int si = 0; si < S; ++si) {
     const Slab& s = op->slabs[si];
     const int r0 = (si == 0 && lo_x) ? 2 : 0;
@@ -387,6 +453,8 @@ void run_sl2(hh_op* op, const double2* v, const double* vs, double2* out) {
     launch_rows(si, r0, r1, s.rpb, 0, c->stream);
     if (si == 0 && op->tk1) HIPC(hipEventRecord(op->tk1, c->stream));
   }
+  hipEvent_t t_int1 = tmark(op, c->stream);
+  tspan(op, HH_SPAN_INTERIOR, t_int0, t_int1);
   if (lo_x || hi_x) {
     // the two rows next to each cross-rank boundary, on the halo stream behind the exchange
     hipStream_t hs = c->cstream;
@@ -399,6 +467,9 @@ void run_sl2(hh_op* op, const double2* v, const double* vs, double2* out) {
       if (lo_x) launch_rows(0, 0, std::min(2, s0.nl), 2, 0, hs);
       if (hi_x) launch_rows(S - 1, std::max(0, sl.nl - 2), sl.nl, 2, 0, hs);
     }
+    hipEvent_t t_bnd = tmark(op, hs);
+    tspan(op, HH_SPAN_BOUNDARY, t_halo, t_bnd);
+    tspan(op, HH_SPAN_HALO_WAIT, t_int1, t_bnd, true);
     HIPC(hipEventRecord(c->ev_halo, hs));
     HIPC(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
   }
@@ -668,6 +739,24 @@ void read_dev(hh_op* op, const double* dsrc, double* hdst, int count) {
                       op->ctx->stream));
   HIPC(hipStreamSynchronize(op->ctx->stream));
   std::memcpy(hdst, op->status_h, count * sizeof(double));
+}
+
+// The persistent sweep chain (sweep_dense.hip) bounds its grid-wide waits and reports a
+// timeout in red[kRedTimeout] instead of hanging; its output is then garbage.  Every path that
+// ran a chained sweep apply checks the word here (one synchronising read; nothing for the other
+// preconditioners) and clears it only after the check, so no timeout is lost or reported twice.
+void check_sweep_chain(hh_op* op) {
+  if (!op->sw_chain || !is_sweep(op->pkind)) return;
+  double w = 0.0;
+  read_dev(op, op->red + kRedTimeout, &w, 1);
+  unsigned tmo = 0;
+  std::memcpy(&tmo, &w, sizeof(unsigned));
+  if (tmo != 0) {
+    HIPC(hipMemset(op->red + kRedTimeout, 0, sizeof(double)));
+    fail(HH_ERR_STATE, "sweeping preconditioner: the persistent apply chain timed out "
+                       "(workgroups not co-resident?); HH_SWEEP_CHAIN=0 selects one launch "
+                       "per GEMV");
+  }
 }
 
 void ensure_gmres(hh_op* op, int restart) {
@@ -1228,6 +1317,7 @@ HH_API int hh_op_apply(hh_op* op, const double* x, double* y, int mode) {
   apply_mode(op, op->hx, dst, mode);
   HIPC(hipMemcpyAsync(y, dst, op->nloc * sizeof(double2), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
+  if (mode == HH_APPLY_PREC || mode == HH_APPLY_PREC_A) check_sweep_chain(op);
   GUARD_END
 }
 
@@ -1386,6 +1476,7 @@ HH_API int hh_op_apply_dev(hh_op* op, const hh_vec* x, hh_vec* y, int mode) {
   HIPC(hipSetDevice(op->ctx->device));
   apply_mode(op, x->d, y->d, mode);
   HIPC(hipStreamSynchronize(op->ctx->stream));
+  if (mode == HH_APPLY_PREC || mode == HH_APPLY_PREC_A) check_sweep_chain(op);
   GUARD_END
 }
 
@@ -1447,6 +1538,7 @@ HH_API int hh_op_time_apply_set(hh_op* op, const hh_vec* const* xs, hh_vec* cons
   op->tk0 = op->tk1 = nullptr;
   HIPC(hipEventRecord(t1, s));
   HIPC(hipEventSynchronize(t1));
+  if (mode == HH_APPLY_PREC || mode == HH_APPLY_PREC_A) check_sweep_chain(op);
   float ms = 0.f;
   HIPC(hipEventElapsedTime(&ms, t0, t1));
   *total_ms = ms;
@@ -1639,6 +1731,43 @@ HH_API int hh_op_probe_stream_set(hh_op* op, int kind, int blocks, const hh_vec*
   GUARD_END
 }
 
+HH_API int hh_op_set_timing(hh_op* op, int enable) {
+  GUARD_BEGIN
+  REQUIRE(op, "null op");
+  HIPC(hipSetDevice(op->ctx->device));
+  HIPC(hipStreamSynchronize(op->ctx->stream));
+  op->timer.reset();
+  op->timer.on = enable != 0;
+  GUARD_END
+}
+
+HH_API int hh_op_read_timing(hh_op* op, double* ms, long* counts) {
+  GUARD_BEGIN
+  REQUIRE(op && ms && counts, "null argument");
+  HIPC(hipSetDevice(op->ctx->device));
+  HIPC(hipDeviceSynchronize());  // (the halo stream's events too)
+  for (int k = 0; k < HH_SPAN_COUNT; ++k) {
+    ms[k] = 0.0;
+    counts[k] = 0;
+  }
+  for (const auto& sp : op->timer.spans) {
+    float t = 0.f;
+    HIPC(hipEventElapsedTime(&t, sp.a, sp.b));
+    if (sp.clamp && t < 0.f) t = 0.f;
+    ms[sp.cat] += t;
+    counts[sp.cat] += 1;
+  }
+  op->timer.reset();  // (timing stays enabled; the next read covers what follows)
+  GUARD_END
+}
+
+HH_API int hh_op_last_solve_path(hh_op* op, int* path) {
+  GUARD_BEGIN
+  REQUIRE(op && path, "null argument");
+  *path = op->last_path;
+  GUARD_END
+}
+
 HH_API int hh_op_last_stats(hh_op* op, hh_stats* st) {
   GUARD_BEGIN
   REQUIRE(op && st, "null argument");
@@ -1753,6 +1882,8 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
                      (op->pkind == HH_PREC_NONE || op->pkind == HH_PREC_JACOBI) &&
                      (op->krylov_mode != 1) && small_cycle_eligible(op->n, restart, device_cus(c)) &&
                      (op->small_cycle == 1 || (size_t)op->n * op->n <= ((size_t)1 << 18));
+  // every sweep apply above (M b, the as-is constant) is checked before the word is re-armed
+  check_sweep_chain(op);
   unsigned* small_timeout = reinterpret_cast<unsigned*>(op->red + kRedTimeout);
   HIPC(hipMemsetAsync(small_timeout, 0, sizeof(double), s));  // (the device wait-bound word)
   if (small) {
@@ -1796,6 +1927,8 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       }
     }
   };
+  bool small_refused = false;
+  op->last_path = small ? 1 : 0;
   if (small) {
     // Small grids: whole-cycle launches (gmres_small.hip), up to kSmallBatch queued behind each
     // other -- scipy's restart-loop decisions are taken on the device from the state below
@@ -1860,9 +1993,20 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         sa.timeout_word = small_timeout;
         sa.phase_ticks = op->small_ticks;
         sa.outer = outer;
-        launch_small_cycle(sa, op->const_c, op->pkind == HH_PREC_JACOBI, s);
-        HIPC(hipGetLastError());
+        const hipError_t le = launch_small_cycle(sa, op->const_c, op->pkind == HH_PREC_JACOBI, s);
+        if (le != hipSuccess) {
+          // refused before anything of the cycle ran (cooperative launch: e.g. the grid cannot
+          // be co-resident): the first launch of the solve falls back to the regular cycle, which
+          // starts from the same state (V[0] = M r, red[4..5]); a later refusal cannot, as cycles
+          // already changed x
+          REQUIRE(iteration == 0 && i == 0,
+                  "small-grid GMRES: cooperative launch refused after %ld cycles (%s)", iteration,
+                  hipGetErrorString(le));
+          small_refused = true;
+          break;
+        }
       }
+      if (small_refused) break;
       HIPC(hipStreamSynchronize(s));
       for (int i = 0; i < P && !done; ++i) {
         const double* rep = op->status_h + (size_t)(1 + i) * kRedDoubles;
@@ -1899,8 +2043,11 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         done = rep[6] != 0.0;  // (rnorm <= atol, breakdown, or legacy maxiter)
       }
     }
-    finish(inner, rnorm <= atol ? 0 : (int)std::min<long>(maxiter, 0x7fffffff), rnorm);
-    return HH_OK;
+    if (!small_refused) {
+      finish(inner, rnorm <= atol ? 0 : (int)std::min<long>(maxiter, 0x7fffffff), rnorm);
+      return HH_OK;
+    }
+    op->last_path = 2;  // refused: the regular cycle below runs the whole solve
   }
 
   for (long iteration = 0; iteration < maxiter; ++iteration) {
@@ -1926,12 +2073,18 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       const int* stp = g.ctrl;
       apply_MA(op, vcol, g.sscale + c2, w);  // w = M A (s_c2 u_c2)
       const int K = c2 + 1;
+      hipEvent_t k0 = tmark(op, s);
       launch_multidot(V, ldv, K, w, L, op->partials, blocks, s, stp);
       launch_reduce(op->partials, blocks, 2 * K + 2, 2 * K + 1, op->red + 16, s, stp);
       if (c2 > 0) launch_reduce(op->npart, blocks, kMaxNorms, 1, op->red + 16 + 2 * K + 1, s, stp);
+      tspan(op, HH_SPAN_MULTIDOT, k0, tmark(op, s));
       allreduce_sum_dev(op, op->red + 16, 2 * K + (c2 > 0 ? 2 : 1));
+      hipEvent_t k1 = tmark(op, s);
       launch_gmres_lag(g, c2, op->red + 16, op->red + 16 + 2 * K + 1, false, eps, ptol, stop_col, s);
+      hipEvent_t k2 = tmark(op, s);
+      tspan(op, HH_SPAN_COLUMN, k1, k2);
       launch_update(V, ldv, K, op->red + 16, g.vscale, w, w, L, op->npart, blocks, s, stp);
+      tspan(op, HH_SPAN_UPDATE, k2, tmark(op, s));
       HIPC(hipGetLastError());
       if (c2 == stop_col) {  // the cycle's last column needs the norm of the last update
         launch_reduce(op->npart, blocks, kMaxNorms, 1, op->red + 8, s, stp);
@@ -1969,13 +2122,17 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         HIPC(hipGetLastError());
         continue;
       }
+      hipEvent_t k0 = tmark(op, s);
       launch_multidot(V, ldv, K, w, L, op->partials, blocks, s, stp);
       launch_reduce(op->partials, blocks, 2 * K + 2, 2 * K + 1, op->red + 16, s, stp);
+      tspan(op, HH_SPAN_MULTIDOT, k0, tmark(op, s));
       allreduce_sum_dev(op, op->red + 16, 2 * K + 1);
       // single rank: the column kernel sums the update's norm partials itself (one launch
       // fewer per iteration); across ranks they are reduced and allreduced first
       const bool fold = c->world == 1;
+      hipEvent_t k1 = tmark(op, s);
       launch_update(V, ldv, K, op->red + 16, g.vscale, w, w, L, op->partials, blocks, s, stp);
+      tspan(op, HH_SPAN_UPDATE, k1, tmark(op, s));
       if (!fold) {  // (with reorth this norm is superseded by the second pass's)
         launch_reduce(op->partials, blocks, kMaxNorms, 1, op->red + 8, s, stp);
         allreduce_sum_dev(op, op->red + 8, 1);
@@ -1993,8 +2150,10 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         }
         launch_add_small(op->red + 96, op->red + 16, 2 * K, s, stp);
       }
+      hipEvent_t k2 = tmark(op, s);
       launch_gmres_column(g, c2, op->red + 16, op->red + 8, fold ? op->partials : nullptr, blocks,
                           eps, ptol, stop_col, s);
+      tspan(op, HH_SPAN_COLUMN, k2, tmark(op, s));
       HIPC(hipGetLastError());
     }
     op->stop_flag = nullptr;  // (the SolveScope also clears it if anything above throws)
@@ -2025,6 +2184,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     launch_xupdate(V, ldv, col + 1, g.ycoef, x, L, blocks, s);
     residual(op, b, x, V, 4);  // r = b - A x; V[0] = M r for the next cycle
     read_dev(op, op->red + 4, st, 1);
+    check_sweep_chain(op);  // (the M r of the last cycle is never read by a cycle report)
     rnorm = std::sqrt(st[0]);
     if (legacy && inner == maxiter) {
       finish(inner, rnorm <= atol ? 0 : (int)std::min<long>(maxiter, 0x7fffffff), rnorm);

@@ -287,6 +287,27 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
             raise ValueError(f"mode must be one of {sorted(modes)}")
         check(lib.hh_op_set_small_cycle(self.handle, modes[mode]))
 
+    def set_timing(self, enable: bool = True):
+        """Diagnostic span timing (hh_op_set_timing): HIP events around the halo exchange,
+        boundary / interior kernels, allreduces and Krylov kernels of the following applies
+        and solves.  Adds queue work: for diagnostic runs only."""
+        check(lib.hh_op_set_timing(self.handle, int(bool(enable))))
+
+    def read_timing(self):
+        """{span: (total ms, count)} since the last read (hh_op_read_timing)."""
+        ms = np.zeros(len(_ffi.SPAN_NAMES))
+        cnt = (ctypes.c_long * len(_ffi.SPAN_NAMES))()
+        check(lib.hh_op_read_timing(self.handle, _ffi.dptr(ms), cnt))
+        return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(_ffi.SPAN_NAMES)}
+
+    SOLVE_PATHS = {0: "regular", 1: "small-cycle", 2: "small-cycle refused -> regular"}
+
+    def last_solve_path(self) -> str:
+        """Cycle form the last ``gmres`` on this operator ran (hh_op_last_solve_path)."""
+        p = ctypes.c_int(-1)
+        check(lib.hh_op_last_solve_path(self.handle, ctypes.byref(p)))
+        return self.SOLVE_PATHS[p.value]
+
     def stats(self):
         s = _ffi.HHStats()
         check(lib.hh_op_last_stats(self.handle, ctypes.byref(s)))

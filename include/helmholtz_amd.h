@@ -190,6 +190,10 @@ int hh_op_time_apply_set(hh_op* op, const hh_vec* const* xs, hh_vec* const* ys, 
  *   cb:   optional per-iteration callback(user, iteration, presid/||b||); returns 0 to
  *         continue, non-zero to stop the solve at once (hh_gmres then returns
  *         HH_ERR_ABORTED; scipy propagates a callback's exception the same way).
+ *         After HH_ERR_ABORTED the contents of x are unspecified: the small-grid cycle kernel
+ *         (hh_op_set_small_cycle) queues up to 16 restart cycles per host synchronisation, so
+ *         x may be up to 15 cycles past the iteration the callback stopped at (scipy's callers
+ *         never see x in that case either: the exception propagates).
  * On every exit path -- success, error or abort -- the operator is left ready for plain
  * applies (no stale in-solve state). */
 typedef int (*hh_gmres_callback)(void* user, long iteration, double rel_presid);
@@ -222,18 +226,23 @@ int hh_op_set_history_callback(hh_op* op, hh_gmres_history_callback cb, void* us
  * the previous iteration's update wrote travels with the projections (lagged normalisation: the
  * Hessenberg subdiagonal of column j is completed in iteration j+1, the SpMV input is scaled by a
  * Pythagorean estimate meanwhile; H, the residual history and x agree to rounding, one extra
- * collective per restart cycle).  mode 0 (default): 2 across ranks, 1 on a single rank.  CGS2
- * (reorth) always uses mode 1. */
+ * collective per restart cycle).  mode 0 (default): one reduction (mode 2) across ranks, two
+ * (mode 1) on a single rank.  CGS2 (reorth) always uses mode 1. */
 int hh_op_set_krylov_mode(hh_op* op, int mode);
 /* Whole-cycle GMRES kernel for small grids (no reference counterpart): a restart cycle of
  * hh_gmres as ONE launch whose workgroups keep the Krylov basis on chip and meet once per inner
  * iteration (lagged normalisation as krylov mode 2), instead of five launches per iteration.
  * Applies on a single rank and slab, 5-point operator, M = none or Jacobi, without reorth, when
- * n <= 255 (n + 1 workgroups, one per CU) and the basis fits the LDS (3 n (restart + 1) x 16 B
- * <= ~150 KB).  mode -1 (default):
+ * n <= 255 (n + 1 workgroups, one per CU, launched cooperatively) and the basis fits the LDS
+ * (3 n (restart + 1) x 16 B <= ~150 KB).  mode -1 (default):
  * used when it applies and n^2 <= 2^18; 1: whenever it applies; 0: never.  Results agree with the
  * regular cycle to rounding. */
 int hh_op_set_small_cycle(hh_op* op, int mode);
+/* Which cycle form the last hh_gmres on `op` ran: 0 the regular per-launch cycle, 1 the
+ * small-grid whole-cycle kernel, 2 the small-grid kernel refused at its first (cooperative)
+ * launch -- its n + 1 workgroups could not be co-resident -- so the regular cycle ran the whole
+ * solve instead (same results to rounding; no partial state). */
+int hh_op_last_solve_path(hh_op* op, int* path);
 /* Diagnostic: phase timing of the small-grid cycle kernel (workgroup 0's wall clock summed over
  * the following solves): phase_us (optional, 8 doubles) receives the totals so far in us
  * (0 stencil + z hand-off, 5 partial sums, 6 their publication, 1 all-reduce, 3 coefficients +
@@ -300,6 +309,33 @@ int hh_op_probe_stream(hh_op* op, int kind, int blocks, const hh_vec* x, hh_vec*
 int hh_op_probe_stream_set(hh_op* op, int kind, int blocks, const hh_vec* const* xs,
                            hh_vec* const* ys, int nvec, int iters, double* kernel_ms,
                            int* bytes_per_point);
+
+/* Diagnostic span timing (no reference counterpart): with timing enabled, the operator records
+ * HIP events around the pieces of every apply and GMRES inner iteration on the streams they run
+ * on; hh_op_read_timing synchronises the device, sums the spans per category (ms; counts = spans
+ * recorded) and restarts the sums.  Categories:
+ *   HALO       input complete (compute stream) -> the halo exchange done (halo stream)
+ *   BOUNDARY   the boundary-row kernel(s) behind the exchange (halo stream)
+ *   INTERIOR   the interior stencil / fused M A launch (compute stream)
+ *   HALO_WAIT  compute stream idle after the interior launch until the boundary rows are done
+ *              (0 when the exchange hid behind the interior)
+ *   ALLREDUCE  each in-solve device allreduce (RCCL / SHM; none on one rank)
+ *   COLUMN     the Givens / Hessenberg column kernel of an inner iteration
+ *   MULTIDOT   projections V^H w and their fixed-order block reduction
+ *   UPDATE     w -= V h (+ the norm partials)
+ * Events add ~1-2 us of queue work each: enable it for diagnostic runs, not timed ones.
+ * enable = 0 stops recording (and clears); the whole-cycle small-grid kernel is not split. */
+#define HH_SPAN_HALO 0
+#define HH_SPAN_BOUNDARY 1
+#define HH_SPAN_INTERIOR 2
+#define HH_SPAN_HALO_WAIT 3
+#define HH_SPAN_ALLREDUCE 4
+#define HH_SPAN_COLUMN 5
+#define HH_SPAN_MULTIDOT 6
+#define HH_SPAN_UPDATE 7
+#define HH_SPAN_COUNT 8
+int hh_op_set_timing(hh_op* op, int enable);
+int hh_op_read_timing(hh_op* op, double* ms /* [HH_SPAN_COUNT] */, long* counts /* [HH_SPAN_COUNT] */);
 
 /* Optional per-call counters of the last hh_gmres / hh_op_time_apply. */
 typedef struct {

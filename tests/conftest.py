@@ -58,4 +58,13 @@ def _ensure_native_library():
                         os.path.join(ROOT, "helmholtz_preconditioner_amd", "csrc")], check=True)
 
 
+def _ensure_c_oracle():
+    """Build the C oracle (oracle/build/libhh_oracle.so, test infrastructure) if missing."""
+    so = os.path.join(ROOT, "oracle", "build", "libhh_oracle.so")
+    if not os.path.exists(so):
+        import subprocess
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+
+
 _ensure_native_library()
+_ensure_c_oracle()

@@ -1,5 +1,7 @@
-"""One rank of a BASELINE config-4 run (8192^2 constant medium, used by
-tests/test_gpu_configs.py): every rank sits on device 0 with the shared-memory transport.
+"""One rank of a BASELINE config-4 / config-5 run (8192^2 / 16384^2 constant medium, used by
+tests/test_gpu_configs.py): every rank sits on device 0, over the shared-memory transport or
+the production RCCL one (--transport; RCCL then needs one NCCL host id per rank, which the
+parent sets in the environment).
 
 The input is the hash fill (hh_vec_fill_hash: a pure function of the global index, identical
 for any slab decomposition), so nothing of size N crosses the process boundary on the way in;
@@ -27,21 +29,35 @@ def main():
     p.add_argument("--wave-num", type=float)
     p.add_argument("--iters", type=int)
     p.add_argument("--ref-dir")
+    p.add_argument("--transport", default="shm", choices=["shm", "rccl"])
+    p.add_argument("--no-apply", action="store_true", help="skip the apply comparison")
     a = p.parse_args()
-    ctx = H.Context(device=0, rank=a.rank, world=a.world, nccl_id=bytes.fromhex(a.id),
-                    transport="shm")
+    if a.transport == "rccl":  # rank 0's ncclGetUniqueId, shipped through a node-local file
+        from helmholtz_preconditioner_amd import dist
+        uid = dist.exchange_unique_id(a.rank, a.world, key=a.id[:32], timeout=120.0)
+    else:
+        uid = bytes.fromhex(a.id)
+    ctx = H.Context(device=0, rank=a.rank, world=a.world, nccl_id=uid, transport=a.transport)
+    if a.transport == "rccl":
+        ctx.barrier()
+        if a.rank == 0:
+            dist.cleanup_rendezvous(a.id[:32])
     n = a.n
     om, h, eta = H.problem_params(n, 12, a.wave_num, 2.0)
     A = H.build_A_matrix(12, 81.0, eta, om, h, n, np.broadcast_to(1.0, (n + 2, n + 2)),
                          context=ctx)
     j0, j1 = A.row_begin, A.row_end
-    x, y = A.vector(), A.vector()
-    x.fill_hash(7)
-    A.apply_device(x, y)
-    yl = y.download()
-    yref = np.load(os.path.join(a.ref_dir, "y.npy"), mmap_mode="r")[j0 * n:j1 * n]
-    out = dict(j0=j0, j1=j1, y_mismatch=int(np.count_nonzero(yl != yref)))
-    del yl, yref
+    out = dict(j0=j0, j1=j1, transport=a.transport, y_mismatch=-1)
+    if not a.no_apply:
+        x, y = A.vector(), A.vector()
+        x.fill_hash(7)
+        A.apply_device(x, y)
+        yl = y.download()
+        x.close()
+        y.close()
+        yref = np.load(os.path.join(a.ref_dir, "y.npy"), mmap_mode="r")[j0 * n:j1 * n]
+        out["y_mismatch"] = int(np.count_nonzero(yl != yref))
+        del yl, yref
     f = H.init_f1_mat(.5, .125, om, n)[j0:j1].ravel()
     xs, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=a.iters, M="jacobi",
                              callback=lambda r: None, callback_type="legacy",

@@ -180,6 +180,15 @@ def test_bench_two_ranks_rehearsal(tmp_path, transport):
     assert sn["n"] == 1024 and sn["spmv"]["speedup_same_n"] > 0
     assert sn["spmv"]["single_gpu_value"] > 0 and 0 < sn["spmv"]["per_gpu_frac"] < 1
     assert sn["gmres"]["speedup_same_n"] > 0
+    # where the time goes on N ranks: per-span HIP-event times, max over ranks, all >= 0
+    bd = sn["breakdown"]
+    sp, gi = bd["spmv_per_apply"], bd["gmres_per_iteration"]
+    assert set(sp) == {"halo", "boundary", "interior", "halo_wait"}
+    assert all(v >= 0 for v in sp.values()) and all(v >= 0 for v in gi.values())
+    assert sp["interior"] > 0 and sp["halo"] > 0 and sp["boundary"] > 0
+    for k in ("allreduce", "column", "multidot", "update", "interior", "halo"):
+        assert gi[k] > 0, (k, gi)
+    assert 1 <= gi["allreduces"] <= 3  # one per inner iteration (+ per-cycle extras)
 
 
 def test_bench_stalled_rank_exits_with_the_phase_named(tmp_path):

@@ -186,3 +186,59 @@ print("ok")
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
                        text=True, timeout=240)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_small_cycle_path_reported(ctx):
+    """The whole-cycle kernel is launched cooperatively and the operator reports which cycle
+    form ran (hh_op_last_solve_path)."""
+    n = 64
+    om, h, eta = O.problem_params(n, 6, 3.0, 2.0)
+    A = H.build_A_matrix(6, 61.0, eta, om, h, n, medium("c1", n), context=ctx)
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    for mode, path in (("on", "small-cycle"), ("off", "regular"), ("auto", "small-cycle")):
+        A.small_cycle(mode)
+        H.gmres(A, f, rtol=1e-3, restart=20, maxiter=25, callback=lambda r: None,
+                callback_type="legacy")
+        assert A.last_solve_path() == path, (mode, A.last_solve_path())
+    n = 240  # ineligible: 3 n (restart + 1) x 16 B of basis exceed the LDS -> regular cycle
+    om, h, eta = O.problem_params(n, 6, 3.0, 2.0)
+    A = H.build_A_matrix(6, 61.0, eta, om, h, n, medium("c1", n), context=ctx)
+    A.small_cycle("on")
+    H.gmres(A, O.init_f1_mat(.5, .125, om, n).ravel(), rtol=1e-3, restart=20, maxiter=25,
+            callback=lambda r: None, callback_type="legacy")
+    assert A.last_solve_path() == "regular"
+
+
+def test_small_cycle_refused_launch_falls_back():
+    """A cooperative launch the runtime refuses (simulated: HH_SMALL_COOP_REFUSE=1 makes the
+    launch report hipErrorCooperativeLaunchTooLarge without launching) runs the whole solve on
+    the regular cycle -- no spin to a timeout, no partial state -- with the reference's history
+    (golden, 1e-6).  Child process: the knob is read once per process."""
+    import subprocess
+    import sys
+    code = r'''
+import numpy as np, sys
+sys.path.insert(0, ".")
+sys.path.insert(0, "tests")
+import helmholtz_preconditioner_amd as H
+from conftest import load_golden, medium
+from oracle import helmholtz_oracle as O
+z = load_golden("gmres_n128_none.npz")
+n = int(z["n"]); om = complex(z["omega"])
+A = H.build_A_matrix(int(z["b"]), float(z["C"]), float(z["eta"]), om, float(z["h"]), n,
+                     medium(str(z["medium"]), n))
+f = O.init_f1_mat(.5, .125, om, n).ravel()
+A.small_cycle("on")
+x, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=int(z["K"]),
+                        callback=lambda r: None, callback_type="legacy", return_history=True)
+assert A.last_solve_path() == "small-cycle refused -> regular", A.last_solve_path()
+assert info == int(z["info"]) and len(hist) == int(z["niter"])
+assert np.max(np.abs(hist - z["history"]) / z["history"]) < 1e-6
+assert np.linalg.norm(x - z["x"]) < 1e-6 * np.linalg.norm(z["x"])
+print("ok")
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HH_SMALL_COOP_REFUSE="1")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr

@@ -121,3 +121,60 @@ def test_marmousi_like_medium_is_deterministic_and_scaled():
     assert not part[:, :40].any() and not part[:, 77:].any()
     # velocity increases with depth on average (depth grows toward small y = small row)
     assert c[:20].mean() > c[-20:].mean()
+
+
+# ------------------------------------------------ the matrix-free C oracle (configs 4 and 5)
+def _so():
+    from oracle import stencil_oracle as SO
+    return SO
+
+
+@pytest.mark.parametrize("name", ["spmv_n128_const.npz", "spmv_n257_c1.npz"])
+def test_c_oracle_spmv_matches_reference(name):
+    """oracle/stencil_oracle.c (build_A_matrix's rows without the matrix) against the
+    reference's own SpMV outputs."""
+    z = load_golden(name)
+    n = int(z["n"])
+    A = _so().MatrixFreeOperator(int(z["b"]), float(z["C"]), float(z["eta"]),
+                                 complex(z["omega"]), float(z["h"]), n, medium(str(z["medium"]), n))
+    y = A @ rand_complex(n * n, 0)
+    assert np.linalg.norm(y - z["y"]) / np.linalg.norm(z["y"]) < 1e-14
+
+
+@pytest.mark.parametrize("n,kind", [(1, "const"), (2, "c1"), (33, "c2"), (64, "c1"), (150, "marm"),
+                                    (301, "const")])
+def test_c_oracle_equals_csr_oracle(n, kind):
+    """Row for row the CSR of oracle.build_A_matrix (pinned above by the golden CSRs): apply,
+    diagonal and a constant medium given as a scalar, to rounding; and scipy gmres on either
+    operator gives the same history (the C oracle stands in for the CSR at 8192^2 and 16384^2)."""
+    SO = _so()
+    b = min(12, max(1, n // 3))
+    om, h, eta = O.problem_params(n, b, 5.0, 2.0)
+    cm = media.marmousi_like_c_mat(n) if kind == "marm" else medium(kind, n)
+    R = O.build_A_matrix(b, 81.0, eta, om, h, n, cm)
+    for A in (SO.MatrixFreeOperator(b, 81.0, eta, om, h, n, cm),) + (
+            (SO.MatrixFreeOperator(b, 81.0, eta, om, h, n, 1.0),) if kind == "const" else ()):
+        x = rand_complex(n * n, 4)
+        y, yr = A @ x, R @ x
+        assert np.max(np.abs(y - yr)) <= 1e-15 * np.max(np.abs(yr)) * 4
+        d, dr = A.diagonal(), R.diagonal()
+        assert np.max(np.abs(d - dr)) <= 1e-15 * np.max(np.abs(dr)) * 4
+        assert (A @ x.reshape(-1, 1)).shape == (n * n, 1)
+    if n >= 33:
+        f = O.init_f1_mat(.5, .125, om, n).ravel()
+        _, i1, h1, _ = O.gmres_reference(R, f, M=O.jacobi_preconditioner(R), maxiter=6)
+        _, i2, h2, _ = O.gmres_reference(A, f, M=SO.jacobi_preconditioner(A), maxiter=6)
+        assert i1 == i2 and np.max(np.abs(h1 - h2) / h1) < 1e-12
+
+
+def test_c_oracle_shifted_mass_scale():
+    """mass_scale 1 + i beta is build_A_matrix(c_mat / sqrt(1 + i beta)) (golden shifted CSR)."""
+    z = load_golden("shift_n64.npz")
+    n = int(z["n"])
+    A = _so().MatrixFreeOperator(int(z["b"]), float(z["C"]), float(z["eta"]),
+                                 complex(z["omega"]), float(z["h"]), n, O.init_c1_mat(.5, .5, n),
+                                 mass_scale=1 + 1j * float(z["beta"]))
+    import scipy.sparse
+    R = scipy.sparse.csr_matrix((z["data"], z["indices"], z["indptr"]), shape=(n * n, n * n))
+    x = rand_complex(n * n, 6)
+    assert np.linalg.norm(A @ x - R @ x) / np.linalg.norm(R @ x) < 1e-14

@@ -9,6 +9,9 @@ parity horizons of the GPU tests.
 usage:
   python tools/gmres_sensitivity.py [n] [wave_num]                 # c1 medium, all M, K 6/12/30
   python tools/gmres_sensitivity.py --config 2 --iters 10,20,40,100  # a BASELINE config exactly
+  python tools/gmres_sensitivity.py --config 4 --iters 20 --matrix-free  # 8192^2: the C oracle
+  python tools/gmres_sensitivity.py --config 2 --iters 100 --compare-operators
+      # scipy gmres on the CSR vs on the matrix-free C oracle (oracle/stencil_oracle.py)
 """
 import argparse
 import os
@@ -20,10 +23,12 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from oracle import helmholtz_oracle as O  # noqa: E402
+from oracle import stencil_oracle as SO  # noqa: E402
 
 # BASELINE.json configs: n, medium, wave_num, preconditioner
 CONFIGS = {1: (128, "const", 8.0, "none"), 2: (1024, "const", 64.0, "jacobi"),
-           3: (4096, "marmousi", 100.0, "sl"), 4: (8192, "const", 256.0, "jacobi")}
+           3: (4096, "marmousi", 100.0, "sl"), 4: (8192, "const", 256.0, "jacobi"),
+           5: (16384, "const", 800.0, "jacobi")}
 
 
 def medium(kind, n):
@@ -44,6 +49,10 @@ def main():
     p.add_argument("--precond", default="all")
     p.add_argument("--iters", default="6,12,30")
     p.add_argument("--x0", action="store_true", help="also x0 = 1e-6 f")
+    p.add_argument("--matrix-free", action="store_true",
+                   help="the C oracle operator instead of the CSR (grids too large for a CSR)")
+    p.add_argument("--compare-operators", action="store_true",
+                   help="drift between scipy gmres on the CSR and on the C oracle operator")
     a = p.parse_args()
     n, med, wn, pcs = a.n, a.medium, a.wave_num, a.precond
     if a.config:
@@ -52,16 +61,24 @@ def main():
     cm = medium(med, n)
     om, h, eta = O.problem_params(n, b, wn, al)
     t0 = time.perf_counter()
-    A = O.build_A_matrix(b, C, eta, om, h, n, cm)
+    mf = a.matrix_free or a.compare_operators
+    A = (SO.MatrixFreeOperator(b, C, eta, om, h, n, 1.0 if med == "const" else cm)
+         if a.matrix_free else O.build_A_matrix(b, C, eta, om, h, n, cm))
     f = O.init_f1_mat(.5, .125, om, n).ravel()
     fp = f * (1 + 1e-15 * np.random.default_rng(1).standard_normal(f.size))
-    precs = {"none": lambda: None, "jacobi": lambda: O.jacobi_preconditioner(A),
+    if a.compare_operators:  # the second run: same f, the other operator
+        A2 = SO.MatrixFreeOperator(b, C, eta, om, h, n, 1.0 if med == "const" else cm)
+        fp = f
+    jac = SO.jacobi_preconditioner if mf else O.jacobi_preconditioner
+    precs = {"none": lambda: None, "jacobi": lambda: jac(A),
              "sl": lambda: O.shifted_laplace_jacobi(b, C, eta, om, h, n, cm, beta=0.5, sweeps=2,
                                                     damping=0.7)[0]}
     names = list(precs) if pcs == "all" else pcs.split(",")
-    print(f"n={n} medium={med} wave_num={wn} (setup {time.perf_counter() - t0:.1f} s): drift "
-          f"between scipy gmres on f and on f(1 + 1e-15 N(0,1)), rtol=1e-3, restart=20",
-          flush=True)
+    what = ("scipy gmres on the CSR and on the matrix-free C oracle (same f)"
+            if a.compare_operators else "scipy gmres on f and on f(1 + 1e-15 N(0,1))")
+    print(f"n={n} medium={med} wave_num={wn} operator={'C oracle' if a.matrix_free else 'CSR'} "
+          f"(setup {time.perf_counter() - t0:.1f} s): drift between {what}, rtol=1e-3, "
+          f"restart=20", flush=True)
     for name in names:
         M = precs[name]()
         for x0s in ((None, 1e-6) if a.x0 else (None,)):
@@ -70,8 +87,15 @@ def main():
                 t0 = time.perf_counter()
                 x1, i1, h1, r1 = O.gmres_reference(A, f, M=M, rtol=1e-3, restart=20, maxiter=K,
                                                    x0=None if x0 is None else x0.copy())
-                x2, _, h2, r2 = O.gmres_reference(A, fp, M=M, rtol=1e-3, restart=20, maxiter=K,
-                                                  x0=None if x0 is None else x0.copy())
+                if a.compare_operators:
+                    M2 = SO.jacobi_preconditioner(A2) if name == "jacobi" else M
+                    x2, _, h2, r2 = O.gmres_reference(A2, f, M=M2, rtol=1e-3, restart=20,
+                                                      maxiter=K,
+                                                      x0=None if x0 is None else x0.copy())
+                else:
+                    x2, _, h2, r2 = O.gmres_reference(A, fp, M=M, rtol=1e-3, restart=20,
+                                                      maxiter=K,
+                                                      x0=None if x0 is None else x0.copy())
                 m = min(len(h1), len(h2))
                 print(f"M={name:6s} x0={'0' if x0s is None else '1e-6 f':7s} iters={K:3d} "
                       f"(ran {len(h1)}/{len(h2)}, info {i1}): presid "
