@@ -161,21 +161,26 @@ def local_f1(omega, n, j0, j1, r1=.5, r2=.125):
     return np.exp(-(4 * omega / np.pi) ** 2 * ((x[None, :] - r1) ** 2 + (yy - r2) ** 2)).ravel()
 
 
+TRAFFIC_DB = "profiles/r03_pmc_traffic.json"
+
+
 def measured_traffic(n, medium, world, stencil=5):
-    """HBM bytes per stencil launch from the rocprofv3 PMC passes committed under profiles/
-    (FETCH_SIZE x2 + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md, calibrated
-    on the probe kernels in the same run).  PMC counters cannot be read inside the timed
-    run, so this is the committed measurement of the same kernel and workload (None
-    otherwise)."""
-    name = "r01_pmc_traffic.json" if stencil == 5 else "r01_pmc_traffic_s9.json"
-    path = os.path.join(ROOT, "profiles", name)
-    if not (n == 4096 and medium == "marmousi" and world == 1 and os.path.exists(path)):
-        return None, None
-    rec = json.load(open(path)).get("tile_kernel<0" if stencil == 5 else "stencil_kernel<0")
+    """HBM bytes per apply-kernel launch from the rocprofv3 PMC passes committed under profiles/
+    (FETCH_SIZE x2 + WRITE_SIZE in separate passes, the gfx950 correction of
+    MI355X_MICROARCH.md; tools/gpu_session.sh step `pmcset` -> tools/pmc_traffic.py) for this
+    grid, medium and stencil.  PMC counters cannot be read inside the timed run, so this is the
+    committed measurement of the same kernel and workload: (bytes, ratio to the algorithmic
+    bytes, source), or Nones for a workload without a record (e.g. a rank's slab at N > 1)."""
+    path = os.path.join(ROOT, TRAFFIC_DB)
+    if world != 1 or not os.path.exists(path):
+        return None, None, None
+    kind = "const" if medium == "const" else medium
+    rec = json.load(open(path)).get(f"n{n}_{kind}_s{stencil}")
     if not rec:
-        return None, None
-    return int(rec["fetch_x2"] + rec["write"]), (f"profiles/{name}: FETCH_SIZE x2 "
-                                                 "+ WRITE_SIZE per launch, same kernel/workload")
+        return None, None, None
+    return (int(rec["traffic"]), round(rec["ratio"], 4),
+            f"{TRAFFIC_DB}: FETCH_SIZE x2 + WRITE_SIZE per launch of {rec['kernel'][:60]}..., "
+            f"same grid / medium / stencil")
 
 
 def make_medium(kind, n, cols):
@@ -504,6 +509,8 @@ def main():
             "ms_per_step": round(tc * 1e3 / args.const_steps, 5),
             "bytes_per_unknown": Ac.bytes_per_point,
             "pct_hbm_peak": round(100.0 * vc / (HBM_PEAK_GBPS * world), 2)}
+        ct, cr, _ = measured_traffic(n, "const", world, args.stencil)
+        const_block.update(traffic=ct, traffic_vs_algorithmic=cr)
         Ac.close()
         del Ac
 
@@ -564,7 +571,7 @@ def main():
         "device_ms_per_step": round(dev_ms / args.steps, 5),
         "init_s": round(t_init, 3),
     }
-    traffic, traffic_src = measured_traffic(n, args.medium, world, args.stencil)
+    traffic, traffic_ratio, traffic_src = measured_traffic(n, args.medium, world, args.stencil)
     result["roofline"] = {
         "bound": "hbm",
         "achieved": round(achieved_min, 1),
@@ -572,6 +579,7 @@ def main():
         "unit": "GB/s",
         "frac": round(achieved_min / HBM_PEAK_GBPS, 4),
         "traffic": traffic,
+        "traffic_vs_algorithmic": traffic_ratio,
         "traffic_source": traffic_src,
         "kernel": (f"tile_kernel<EPI_AX,{'true' if A.constant_medium else 'false'},4 rows> "
                    "(interior rows)") if (args.stencil == 5 and n >= 2048 and args.variant < 0) else

@@ -101,7 +101,12 @@ SIGNATURES = [
     ("hh_op_last_stats", c_int, [c_void_p, ctypes.POINTER(HHStats)]),
 ]
 
+# HH_LIB_AB=1 (diagnostic A/B timing against an older build given by HH_LIB_PATH): entry points
+# the older library lacks are left unbound instead of failing the import
+_AB = os.environ.get("HH_LIB_AB") == "1"
 for _name, _res, _args in SIGNATURES:
+    if _AB and not hasattr(lib, _name):
+        continue
     _fn = getattr(lib, _name)
     _fn.restype = _res
     _fn.argtypes = _args

@@ -1046,6 +1046,15 @@ hipError_t launch_one(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds
     return e && e[0] == '1';
   }();
   if (refuse) return hipErrorCooperativeLaunchTooLarge;
+  // HH_SMALL_COOP=0: the plain launch of round 2 (co-residency then NOT guaranteed; A/B timing)
+  static const bool coop = [] {
+    const char* e = std::getenv("HH_SMALL_COOP");
+    return !(e && e[0] == '0');
+  }();
+  if (!coop) {
+    hipLaunchKernelGGL((gmres_small_cycle_kernel<C, J>), grid, block, lds, s, a);
+    return hipGetLastError();
+  }
   SmallCycleArgs arg = a;
   void* params[] = {&arg};
   const hipError_t e = hipLaunchCooperativeKernel(

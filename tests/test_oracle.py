@@ -178,3 +178,18 @@ def test_c_oracle_shifted_mass_scale():
     R = scipy.sparse.csr_matrix((z["data"], z["indices"], z["indptr"]), shape=(n * n, n * n))
     x = rand_complex(n * n, 6)
     assert np.linalg.norm(A @ x - R @ x) / np.linalg.norm(R @ x) < 1e-14
+
+
+@pytest.mark.parametrize("K", [5, 7, 20])
+def test_gmres_restart_k_is_restart_20(K):
+    """scipy gmres (code.py:516, restart 20) stopped by legacy maxiter = K <= 20 inside its first
+    cycle is bitwise the restart = K run: the configs-4/5 oracle uses restart K to avoid scipy's
+    (restart + 1) x N basis allocation at 16384^2."""
+    n = 96
+    om, h, eta = O.problem_params(n, 12, 6.0, 2.0)
+    A = O.build_A_matrix(12, 81.0, eta, om, h, n, O.init_c1_mat(.5, .5, n))
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    M = O.jacobi_preconditioner(A)
+    a = O.gmres_reference(A, f, M=M, rtol=1e-3, restart=20, maxiter=K)
+    b = O.gmres_reference(A, f, M=M, rtol=1e-3, restart=K, maxiter=K)
+    assert a[1] == b[1] and np.array_equal(a[0], b[0]) and np.array_equal(a[2], b[2])

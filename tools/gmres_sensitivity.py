@@ -85,15 +85,16 @@ def main():
             for K in [int(k) for k in a.iters.split(",")]:
                 x0 = None if x0s is None else x0s * f
                 t0 = time.perf_counter()
-                x1, i1, h1, r1 = O.gmres_reference(A, f, M=M, rtol=1e-3, restart=20, maxiter=K,
+                rs = min(20, K)  # (bitwise restart 20 for K <= 20: tests/test_oracle.py)
+                x1, i1, h1, r1 = O.gmres_reference(A, f, M=M, rtol=1e-3, restart=rs, maxiter=K,
                                                    x0=None if x0 is None else x0.copy())
                 if a.compare_operators:
                     M2 = SO.jacobi_preconditioner(A2) if name == "jacobi" else M
-                    x2, _, h2, r2 = O.gmres_reference(A2, f, M=M2, rtol=1e-3, restart=20,
+                    x2, _, h2, r2 = O.gmres_reference(A2, f, M=M2, rtol=1e-3, restart=rs,
                                                       maxiter=K,
                                                       x0=None if x0 is None else x0.copy())
                 else:
-                    x2, _, h2, r2 = O.gmres_reference(A, fp, M=M, rtol=1e-3, restart=20,
+                    x2, _, h2, r2 = O.gmres_reference(A, fp, M=M, rtol=1e-3, restart=rs,
                                                       maxiter=K,
                                                       x0=None if x0 is None else x0.copy())
                 m = min(len(h1), len(h2))

@@ -14,6 +14,7 @@
 #                        the tile kernel's average over the timed launches
 #   pmc[:ARGS]           FETCH_SIZE and WRITE_SIZE, one rocprofv3 --pmc pass each, of
 #                        tools/prof_stencil.py ARGS (default --iters 20)
+#   pmcset               the same at every BASELINE config's grid, summarised into pmc_traffic.json
 #   py:SCRIPT[,ARGS]     python tools/SCRIPT ARGS (diagnostics, tuning sweeps)
 #   rocpy:SCRIPT[,ARGS]  the same under rocprofv3 --kernel-trace --stats
 # example: tools/gpu_session.sh r03a tests smoke bench driver rocprof pmc
@@ -58,6 +59,22 @@ for st in "$@"; do
                --output-format csv -- python3 tools/prof_stencil.py "${A[@]}"
              run "${name}_write" 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/${name}_write" -o run \
                --output-format csv -- python3 tools/prof_stencil.py "${A[@]}" ;;
+    pmcset)  # FETCH / WRITE passes of the apply at every BASELINE config's grid (+ 9-point),
+             # merged into $OUT/pmc_traffic.json (bench.py reads profiles/r03_pmc_traffic.json)
+             for cfg in 128:const:5 1024:const:5 4096:marmousi:5 4096:const:5 4096:marmousi:9 \
+                        8192:const:5 16384:const:5; do
+               IFS=':' read -r pn pm ps <<< "$cfg"
+               it=20; [ "$pn" -le 1024 ] && it=200
+               nm="pmcset_${pn}_${pm}_s${ps}"
+               for ctr in FETCH_SIZE WRITE_SIZE; do
+                 run "${nm}_$ctr" 240 rocprofv3 --pmc $ctr -d "$OUT/${nm}_$ctr" -o run \
+                   --output-format csv -- python3 tools/prof_stencil.py --n "$pn" --medium "$pm" \
+                   --stencil "$ps" --iters $it
+               done
+               python3 tools/pmc_traffic.py "$OUT/${nm}_FETCH_SIZE/run_counter_collection.csv" \
+                 "$OUT/${nm}_WRITE_SIZE/run_counter_collection.csv" --n "$pn" --medium "$pm" \
+                 --stencil "$ps" --merge "$OUT/pmc_traffic.json" || true
+             done ;;
     py)      run "py_$(slug "$arg")" 420 python "tools/${A[0]}" "${A[@]:1}" ;;
     rocpy)   name="rocpy_$(slug "$arg")"
              run "$name" 420 rocprofv3 --kernel-trace --stats -d "$OUT/$name" -o run \

@@ -1,39 +1,59 @@
-"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes (separate runs, KB units) per kernel,
-with the gfx950 correction from MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes of a
-16-B/lane coalesced read stream) and the algorithmic bytes of each kernel for comparison.
-usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV [OUT_JSON]
+"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes (separate runs, KB units) of the operator
+apply kernels, with the gfx950 correction from MI355X_MICROARCH.md (FETCH_SIZE counts half the
+bytes of a 16-B/lane coalesced read stream: doubled) next to each kernel's algorithmic bytes
+(read u 16 + 1/c^2 8, write y 16 per unknown; 16 + 16 for a constant medium).
+
+usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV --n N --medium M [--stencil S]
+                                   [--merge OUT_JSON]
+--merge adds the record under key "n{N}_{M}_s{S}" to OUT_JSON (bench.py's measured_traffic
+reads profiles/r03_pmc_traffic.json).
 """
+import argparse
 import csv
 import json
-import sys
+import os
 from collections import defaultdict
 
-N = 4096 * 4096
-ALGO = {  # kernel-name fragment -> (read bytes, write bytes) per launch at 4096^2
-    "p0(": (24 * N, 16 * N), "p1(": (24 * N, 16 * N), "p3(": (16 * N, 16 * N),
-    "p4(": (24 * N, 0), "stencil_kernel<0": (24 * N, 16 * N), "tile_kernel<0": (24 * N, 16 * N),
-}
+KERNELS = ("tile_kernel<0", "tile9_kernel<0", "stencil_kernel<0")  # the EPI_AX apply kernels
 
 
 def load(path):
     acc = defaultdict(list)
     for r in csv.DictReader(open(path)):
         acc[r["Kernel_Name"]].append(float(r["Counter_Value"]) * 1024.0)
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+    return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
 
-fetch, write = load(sys.argv[1]), load(sys.argv[2])
-out = {}
-for name in fetch:
-    key = next((k for k in ALGO if k in name), None)
-    if key is None:
-        continue
-    rd, wr = ALGO[key]
-    f, w = fetch[name], write.get(name, float("nan"))
-    out[key] = dict(kernel=name[:90], fetch_raw=f, write=w, fetch_x2=2 * f,
-                    algo_read=rd, algo_write=wr,
-                    read_ratio_x2=(2 * f / rd) if rd else None, write_ratio=(w / wr) if wr else None)
-    print(f"{key:18s} FETCH raw {f/1e6:8.1f} MB (x2 {2*f/1e6:8.1f}) vs algo read {rd/1e6:7.1f} MB"
-          f" | WRITE {w/1e6:7.1f} MB vs algo {wr/1e6:7.1f} MB")
-if len(sys.argv) > 3:
-    json.dump(out, open(sys.argv[3], "w"), indent=1)
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("fetch")
+    p.add_argument("write")
+    p.add_argument("--n", type=int, required=True)
+    p.add_argument("--medium", default="marmousi")
+    p.add_argument("--stencil", type=int, default=5)
+    p.add_argument("--merge")
+    a = p.parse_args()
+    N = a.n * a.n
+    rd = (16 if a.medium == "const" else 24) * N
+    wr = 16 * N
+    fetch, write = load(a.fetch), load(a.write)
+    rec = None
+    for name, (f, cnt) in sorted(fetch.items(), key=lambda kv: -kv[1][1]):
+        if not any(k in name for k in KERNELS):
+            continue
+        w = write.get(name, (float("nan"), 0))[0]
+        rec = dict(kernel=name[:110], launches=cnt, fetch_raw=f, fetch_x2=2 * f, write=w,
+                   algo_read=rd, algo_write=wr, traffic=2 * f + w,
+                   ratio=(2 * f + w) / (rd + wr), read_ratio_x2=2 * f / rd, write_ratio=w / wr)
+        print(f"n={a.n} {a.medium} s{a.stencil} {name[:70]}: FETCH x2 {2 * f / 1e6:9.1f} MB vs "
+              f"algo read {rd / 1e6:9.1f} | WRITE {w / 1e6:9.1f} vs {wr / 1e6:9.1f} | total "
+              f"{rec['ratio']:.3f}x algorithmic ({cnt} launches)")
+        break  # the apply kernel with the most launches (the timed ones)
+    if rec and a.merge:
+        db = json.load(open(a.merge)) if os.path.exists(a.merge) else {}
+        db[f"n{a.n}_{a.medium}_s{a.stencil}"] = rec
+        json.dump(db, open(a.merge, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
