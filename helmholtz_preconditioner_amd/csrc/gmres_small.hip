@@ -78,6 +78,8 @@ struct Shared {  // LDS layout (carved from dynamic shared memory; see small_cyc
   li* ctl;   // [4]: 0 stop, 1 last column, 2 abort
   l1* gv;    // [2]: presid and breakdown of the last finished column (Givens workgroup; then
              // workgroup 0, for the restart loop's decisions)
+  HH_LDS unsigned long long* tk;  // [16] phase timing of workgroup 0's thread 0 (optional): kept
+                                  // in LDS, not registers, so it costs the row path nothing
   l1* st;    // [R][4]: the columns' statuses (Givens workgroup), copied to the host-mapped
              // status_it only after y is published: a store to host memory holds the storing
              // wave's next vmcnt wait for a PCIe round trip (~3 us per column on the books)
@@ -232,6 +234,16 @@ __device__ __forceinline__ Rot zlartg_s(double2 f, double2 g) {
 }
 
 
+// What changes from one restart cycle to the next inside a multi-cycle launch: the tags' sequence
+// number, the cycle's slot of the host-mapped report (statuses, control words) and |M r|^2.
+struct CycleView {
+  unsigned seq;
+  double* report;     // [kRedDoubles]: [4..7] norms / decisions, statuses at kRedStatusOff
+  double* status_it;  // report + kRedStatusOff
+  int* ctrl;          // (int*)(report + kRedCtrlOff)
+  double mn2;         // |M r|^2 of the cycle's start
+};
+
 // The Givens workgroup's wave: complete column `col` with its subdiagonal h1 (krylov.hip
 // gmres_finish_column) -- every lane computes the same values, lane 0 stores them.  Lane k
 // holds rotation k and entry k of the column, so the chain of previous rotations reads its
@@ -303,7 +315,8 @@ __device__ bool finish_column(const Shared& sh, const SmallCycleArgs& a, int col
 // and y_k / sigma_k.  A round's 2K + 2 sums are fetched by one lane each (one load latency per
 // round, not one per column: the books then keep up with the rows, and the cycle's tail waits
 // on one round trip); lane 0 does the arithmetic.  Returns false on timeout (wave-uniform).
-__device__ bool givens_role(const Shared& sh, const SmallCycleArgs& a, int stop_col, double ptol) {
+__device__ bool givens_role(const Shared& sh, const SmallCycleArgs& a, const CycleView& cv,
+                            int stop_col, double ptol) {
   const int R1 = a.restart + 1;
   const int lane = threadIdx.x;
   const bool l0 = lane == 0;
@@ -325,7 +338,7 @@ __device__ bool givens_role(const Shared& sh, const SmallCycleArgs& a, int stop_
     bool ok = true;
     if (lane < cols) {
       double v = 0.0;
-      ok = ld_gran(a.sums + (size_t)epoch * 2 * kPStride + 2 * lane, gran_tag(a.seq, epoch), &v);
+      ok = ld_gran(a.sums + (size_t)epoch * 2 * kPStride + 2 * lane, gran_tag(cv.seq, epoch), &v);
       sh.sum[lane] = v;
     }
     const bool all = __ballot(!ok) == 0;
@@ -333,7 +346,7 @@ __device__ bool givens_role(const Shared& sh, const SmallCycleArgs& a, int stop_
     return all;
   };
   if (l0) {
-    const double mn = sqrt(*a.mnorm2);
+    const double mn = sqrt(cv.mn2);
     sh.vs[0] = 1.0 / mn;
     sh.ss[0] = 1.0 / mn;
     for (int k = 0; k < R1; ++k) sh.S[k] = make_double2(k == 0 ? mn : 0.0, 0.0);
@@ -361,7 +374,7 @@ __device__ bool givens_role(const Shared& sh, const SmallCycleArgs& a, int stop_
     if (j >= 1) {
       const int c = j - 1;
       stop = finish_column(sh, a, c, (1.0 / vj) * sh.vs[c] / sh.ss[c], vj, ptol, stop_col);
-      if (l0) st_gran(a.verdict + 2 * c, gran_tag(a.seq, c + 1), stop ? 1.0 : 0.0);
+      if (l0) st_gran(a.verdict + 2 * c, gran_tag(cv.seq, c + 1), stop ? 1.0 : 0.0);
       if (stop) col = c;
     }
     if (l0) {
@@ -394,7 +407,7 @@ __device__ __forceinline__ void givens_tail_tick(const SmallCycleArgs& a, unsign
 // subtract y_k H_km in parallel (the next step's H entries loaded a step ahead) -- the
 // sequential solve's order, one column step per iteration instead of one entry.
 // y_k / sigma_k published for the x update.
-__device__ void solve_and_publish(const Shared& sh, const SmallCycleArgs& a) {
+__device__ void solve_and_publish(const Shared& sh, const SmallCycleArgs& a, const CycleView& cv) {
   const int R1 = a.restart + 1;
   const int lane = threadIdx.x;
   const int col = sh.ctl[1];
@@ -416,7 +429,7 @@ __device__ void solve_and_publish(const Shared& sh, const SmallCycleArgs& a) {
     }
     hk = hn;
   }
-  const unsigned ytag = gran_tag(a.seq, 0xff);
+  const unsigned ytag = gran_tag(cv.seq, 0xff);
   if (lane <= col) {
     const double2 c = cscale(y, sh.vs[lane]);
     st_gran(a.ycoef + 4 * lane, ytag, c.x);
@@ -429,9 +442,124 @@ __device__ void solve_and_publish(const Shared& sh, const SmallCycleArgs& a) {
   }
   // the columns' statuses to the host-mapped report, off the critical path now
   if (lane <= col) {
-    double* st = a.g.status_it + 4 * lane;
+    double* st = cv.status_it + 4 * lane;
     for (int q = 0; q < 4; ++q) st[q] = sh.st[4 * lane + q];
   }
+}
+
+// Co-residency gate, instead of a cooperative launch (whose launch cost measured ~55 us: 3 % of a
+// ten-cycle batch at 128^2, profiles/r03*_ab_c1.log).  The workgroups wait on each other, so all
+// of them must be resident at once.  Every workgroup stores its arrival (a word tagged with the
+// launch's sequence number); workgroup 0 polls all arrivals and decides GO; a workgroup whose
+// co-residents did not come within its bound decides ABORT.  The decision is ONE word, set by
+// compare-and-swap from any value not tagged with this launch: the first decision wins, so either
+// every workgroup proceeds, or every workgroup leaves before touching any state (workgroup 0,
+// which always runs eventually, then marks report slot 0 with ctrl = 3 and the host takes the
+// regular cycle).  Returns true to proceed (block-uniform).
+constexpr unsigned kGateSpins = 4000;  // ~ms: a resident grid arrives within microseconds
+__device__ unsigned gate_decide(unsigned long long* decide, unsigned seq, unsigned state) {
+  unsigned long long old =
+      __hip_atomic_load((gu64*)decide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    if ((unsigned)(old >> 2) == seq) return (unsigned)(old & 3u);  // decided already
+    const unsigned long long want = ((unsigned long long)seq << 2) | state;
+    if (__hip_atomic_compare_exchange_strong((gu64*)decide, &old, want, __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      return state;
+  }
+}
+__device__ bool coresidency_gate(const SmallCycleArgs& a, int nwg, HH_LDS int* flag) {
+  const int g = blockIdx.x, t = threadIdx.x;
+  if (t < kWave) {
+    if (t == 0)
+      __hip_atomic_store((gu32*)(a.gate_arrive + g), a.seq, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    unsigned st = 0;
+    if (g == 0) {  // wave 0 polls every arrival word, one lane per word
+      bool all = false;
+      for (unsigned spins = 0; !all && spins < kGateSpins && !a.gate_force_abort; ++spins) {
+        bool mine = true;
+        for (int q = t; q < nwg; q += kWave)
+          mine = mine && __hip_atomic_load((gu32*)(a.gate_arrive + q), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT) == a.seq;
+        all = __all(mine);
+        if (!all) __builtin_amdgcn_s_sleep(2);
+      }
+      if (t == 0) st = gate_decide(a.gate_decide, a.seq, all ? 1u : 2u);
+    } else if (t == 0) {
+      for (unsigned spins = 0;; ++spins) {
+        const unsigned long long v =
+            __hip_atomic_load((gu64*)a.gate_decide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned)(v >> 2) == a.seq) {
+          st = (unsigned)(v & 3u);
+          break;
+        }
+        if (spins > 2 * kGateSpins) {
+          st = gate_decide(a.gate_decide, a.seq, 2u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    if (t == 0) *flag = (int)st;
+  }
+  __syncthreads();
+  const bool go = *flag == 1;
+  if (!go && g == 0 && t == 0)  // (the refusal, for the host)
+    reinterpret_cast<int*>(a.report + kRedCtrl)[0] = 3;
+  return go;
+}
+
+__device__ __forceinline__ CycleView cycle_view(const SmallCycleArgs& a, int cyc) {
+  CycleView cv;
+  cv.seq = a.seq + (unsigned)cyc;
+  cv.report = a.report + (size_t)cyc * kRedDoubles;
+  cv.status_it = cv.report + kRedStatus;
+  cv.ctrl = reinterpret_cast<int*>(cv.report + kRedCtrl);
+  cv.mn2 = 0.0;
+  return cv;
+}
+
+// The head of cycle `cyc`: its stop column and inner tolerance, as given, or from the restart
+// loop's state that the previous cycle left -- in global memory for the launch's first cycle
+// (written before the launch), afterwards from workgroup 0's granules {ptol, inner iterations,
+// done, |M r|^2} (polled by every thread: the same four granules, cache hits after the first).
+// quit: the solve already finished (or a wait timed out): nothing to do.  bad: a wait timed out
+// here (WAVE: the Givens workgroup's single wave votes; otherwise the whole block).
+struct CycleHead {
+  int stop_col;
+  double ptol, mn2;
+  bool quit, bad;
+};
+template <bool WAVE>
+__device__ __forceinline__ CycleHead cycle_head(const SmallCycleArgs& a, const CycleView& cv,
+                                                int cyc) {
+  CycleHead h{a.stop_col, a.ptol, 0.0, false, false};
+  double inner = 0.0;
+  if (cyc == 0) {
+    h.mn2 = *a.mnorm2;
+    if (!a.outer) return h;
+    const double* o = a.outer;
+    h.quit = o[6] != 0.0 || *a.timeout_word != 0u;
+    h.ptol = o[0];
+    inner = o[3];
+  } else {
+    const unsigned otag = gran_tag(cv.seq - 1, 0xfd);
+    double ov[4];
+    bool ok = true;
+    for (int q = 0; q < 4; ++q) ok = ld_gran(a.obuf + 2 * q, otag, &ov[q]) && ok;
+    h.bad = WAVE ? __any(!ok) : __syncthreads_or(!ok);
+    h.ptol = ov[0];
+    inner = ov[1];
+    h.quit = ov[2] != 0.0 || *a.timeout_word != 0u;
+    h.mn2 = ov[3];
+  }
+  const double* o = a.outer;
+  if (o[5] != 0.0) {  // legacy: maxiter caps the inner iterations
+    const double left = o[4] - inner;
+    h.stop_col = left >= (double)a.restart ? a.restart - 1 : (int)left - 1;
+  }
+  return h;
 }
 
 template <bool CONSTC, bool JAC>
@@ -448,7 +576,8 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
   const int lrow = t / npad, lcol = min(t - lrow * npad, n - 1);
   const bool ract = split && lrow < 3 && t - lrow * npad < n;
   const int G = n;  // row workgroups; workgroup n keeps the Givens books
-  const unsigned long long t_launch = a.phase_ticks != nullptr ? wall_clock64() : 0;
+  const bool prof = a.phase_ticks != nullptr && blockIdx.x == 0 && threadIdx.x == 0;
+  const unsigned long long t_launch = prof ? wall_clock64() : 0;
   Shared sh;
   {
     using lc = HH_LDS char;
@@ -472,36 +601,9 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
     sh.ctl = (li*)take(sizeof(int) * 4);
     sh.gv = (l1*)take(sizeof(double) * 2);
     sh.st = (l1*)take(sizeof(double) * 4 * (size_t)a.restart);
+    sh.tk = (HH_LDS unsigned long long*)take(sizeof(unsigned long long) * 16);
   }
-  // this cycle's stop column and inner tolerance: as given, or from the restart loop's state
-  // that the previous queued cycle left (a finished solve or a timeout: nothing to do)
-  int stop_col = a.stop_col;
-  double ptol = a.ptol;
-  if (a.outer) {
-    const double* o = a.outer;
-    if (o[6] != 0.0 || *a.timeout_word != 0u) {
-      if (g == 0 && t == 0) a.g.ctrl[0] = 2;
-      return;
-    }
-    ptol = o[0];
-    if (o[5] != 0.0) {  // legacy: maxiter caps the inner iterations
-      const double left = o[4] - o[3];
-      stop_col = left >= (double)a.restart ? a.restart - 1 : (int)left - 1;
-    }
-  }
-  if (g == G) {
-    if (t >= kWave) return;
-    const bool ok = givens_role(sh, a, stop_col, ptol);  // (wave-uniform)
-    if (!ok) {
-      if (t == 0)
-        __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-    const unsigned long long ts = a.phase_ticks != nullptr ? wall_clock64() : 0;
-    solve_and_publish(sh, a);
-    givens_tail_tick(a, ts);
-    return;
-  }
+  if (!coresidency_gate(a, G + 1, sh.ctl + 3)) return;
   auto Urow = [&](int k, int r) -> l2* { return sh.U + ((size_t)k * 3 + r) * n; };
   const double2 z2 = make_double2(0.0, 0.0);
   ArArgs ar;
@@ -510,12 +612,78 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
   ar.timeout = a.timeout_word;
   ar.seq = a.seq;
   ar.G = G;
+  auto raise_timeout = [&] {
+    if (t == 0)
+      __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+
+  // Up to a.cycles restart cycles in this launch (one cooperative launch per host batch): cycle
+  // `cyc` tags its granules with seq + cyc and reports into its own slot of the host mapping.
+  // Between cycles, what the next launch would have read from global memory after the kernel
+  // boundary travels as tagged granules instead: the restart-loop state (workgroup 0's decisions,
+  // `obuf`) and the neighbours' rows of the new V[0] = M r (`mbuf`); the own row, x and |M r|^2
+  // is kept.  Per-point state (coefficients, x, b, the own row of V[0]) is reloaded every cycle
+  // (this thread wrote x and V[0] itself): nothing but |M r|^2 stays live across cycles.
+  if (g == G) {  // the Givens workgroup: its first wave keeps the books of every cycle
+    if (t >= kWave) return;
+    for (int cyc = 0; cyc < a.cycles; ++cyc) {
+      CycleView cv = cycle_view(a, cyc);
+      const CycleHead hd = cycle_head<true>(a, cv, cyc);
+      if (hd.bad) {
+        raise_timeout();
+        return;
+      }
+      if (hd.quit) return;  // (row workgroup 0 marks the skipped slots)
+      cv.mn2 = hd.mn2;
+      if (!givens_role(sh, a, cv, hd.stop_col, hd.ptol)) {  // (wave-uniform)
+        raise_timeout();
+        return;
+      }
+      const unsigned long long ts = a.phase_ticks != nullptr ? wall_clock64() : 0;
+      solve_and_publish(sh, a, cv);
+      givens_tail_tick(a, ts);
+    }
+    return;
+  }
+  double mn2 = 0.0;
+  // scipy's restart-loop state (iterative.py's outer loop): ptol, ptol_max_factor, inner
+  // iterations so far, done -- from `outer` at launch, then advanced by every row thread
+  double rs_ptol = a.ptol, rs_pmf = 1.0, rs_inner = 0.0;
+  bool rs_done = false;
+  if (a.outer) {
+    rs_ptol = a.outer[0];
+    rs_pmf = a.outer[1];
+    rs_inner = a.outer[3];
+    rs_done = a.outer[6] != 0.0;
+  }
+  for (int cyc = 0; cyc < a.cycles; ++cyc) {
+  const CycleView cv = cycle_view(a, cyc);
+  ar.seq = cv.seq;
+  // this cycle's stop column from the restart loop's state, which every row thread carries
+  // itself (ptol only matters to the Givens workgroup, which polls it) (the same decisions from the same reduced numbers in the same order
+  // everywhere: no hand-off on the critical path between cycles)
+  if (cyc == 0) mn2 = *a.mnorm2;
+  if (rs_done || *a.timeout_word != 0u) {  // the solve finished earlier: slots skipped
+    if (g == 0 && t == 0)
+      for (int q = cyc; q < a.cycles; ++q)
+        reinterpret_cast<int*>(a.report + (size_t)q * kRedDoubles + kRedCtrl)[0] = 2;
+    return;
+  }
+  int stop_col = a.stop_col;
+  if (a.outer && a.outer[5] != 0.0) {  // legacy: maxiter caps the inner iterations
+    const double left = a.outer[4] - rs_inner;
+    stop_col = left >= (double)a.restart ? a.restart - 1 : (int)left - 1;
+  }
 
   // operator coefficients of this thread's point (stencil.hip's formulas; row g, column t)
-  const double2 AW = a.tab_i[tc], AE = a.tab_i[n + tc], R1c = a.tab_i[2 * n + tc];
-  const double2 R2 = a.tab_j[4 * g], BS = a.tab_j[4 * g + 1], BN = a.tab_j[4 * g + 2];
-  const double2 OM = a.tab_j[4 * g + 3];
-  const double ic = CONSTC ? a.invc2_const : a.invc2[(size_t)g * n + tc];
+  const double2* tab_i = a.tab_i;
+  const double2* tab_j = a.tab_j;
+  const double* invc2 = a.invc2;
+  const double2* bvec = a.b;
+  const double2 AW = tab_i[tc], AE = tab_i[n + tc], R1c = tab_i[2 * n + tc];
+  const double2 R2 = tab_j[4 * g], BS = tab_j[4 * g + 1], BN = tab_j[4 * g + 2];
+  const double2 OM = tab_j[4 * g + 3];
+  const double ic = CONSTC ? a.invc2_const : invc2[(size_t)g * n + tc];
   const double2 W = cmul(AW, R2);
   const double2 E = cmul(AE, R2);
   const double2 S = cmul(BS, R1c);
@@ -526,37 +694,61 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
   // this point's x and b, for the cycle's tail (x += V y, r = b - A x): loaded now, off the tail's
   // critical path (only this thread writes x[g][t])
   const double2 x_old = a.x[(size_t)g * n + tc];
-  const double2 b_pt = a.b[(size_t)g * n + tc];
+  const double2 b_pt = bvec[(size_t)g * n + tc];
 
-  // u_0 = the (unnormalised) V[0] = M r of the regular cycle, own and ghost rows
+  // u_0 = the (unnormalised) V[0] = M r of the regular cycle, own and ghost rows: from global
+  // memory in the launch's first cycle, afterwards the neighbours' rows from their tagged
+  // granules (the own row: this thread's own store of the previous cycle)
   for (int r = 0; r < 3; ++r) {
     const int gr = g - 1 + r;
+    if (cyc > 0 && r != 1) continue;
     const double2 u0 = a.v0[(size_t)min(max(gr, 0), n - 1) * n + tc];
     if (act) Urow(0, r)[t] = csel(gr >= 0 && gr < n, u0, z2);
   }
+  bool mok = true;
+  if (cyc > 0 && act) {
+    const unsigned mtag = gran_tag(cv.seq - 1, 0xfe);
+    double lo_x = 0.0, lo_y = 0.0, hi_x = 0.0, hi_y = 0.0;
+    if (g > 0) {
+      const unsigned long long* p = a.mbuf + (size_t)(g - 1) * 4 * n + 4 * t;
+      mok = ld_gran(p, mtag, &lo_x) && ld_gran(p + 2, mtag, &lo_y);
+    }
+    if (g < n - 1 && mok) {
+      const unsigned long long* p = a.mbuf + (size_t)(g + 1) * 4 * n + 4 * t;
+      mok = ld_gran(p, mtag, &hi_x) && ld_gran(p + 2, mtag, &hi_y);
+    }
+    Urow(0, 0)[t] = make_double2(lo_x, lo_y);
+    Urow(0, 2)[t] = make_double2(hi_x, hi_y);
+  }
   // gmres_start_kernel's scaling of V[0], on every workgroup
-  const double vs0 = 1.0 / sqrt(*a.mnorm2);
+  const double vs0 = 1.0 / sqrt(mn2);
   if (t == 0) {
     sh.vs[0] = vs0;
     sh.ctl[0] = 0;
   }
-  __syncthreads();
+  if (__syncthreads_or(!mok)) {
+    raise_timeout();
+    return;
+  }
 
   unsigned epoch = 0;
   // optional phase timing (workgroup 0, thread 0; s_memrealtime ticks): 0 stencil + z hand-off,
   // 5 partial sums, 6 their publication, 1 all-reduce, 3 the neighbours' z (+ the verdict),
   // 2 basis update (coefficients and the next scale inline), 4 the closing barrier
-  const bool prof = a.phase_ticks != nullptr && g == 0 && t == 0;
-  unsigned long long tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long t_first_hop = 0;  // all-reduce: publish -> column 0 reduced here (slot 15)
-  unsigned long long tprev = prof ? wall_clock64() : 0;
-  unsigned long long tl[4] = {prof ? tprev - t_launch : 0, 0, 0, 0};  // head / tail spans
-  const unsigned long long cyc0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  // sh.tk: [0, 8) loop phases, [8, 12) head / tail spans, [12] the previous tick, [13] the
+  // all-reduce's first hop (publish -> column 0 reduced here), [14] shader clock at loop start
+  if (prof) {
+    const unsigned long long now = wall_clock64();
+    for (int q = 0; q < 16; ++q) sh.tk[q] = 0;
+    sh.tk[8] = cyc == 0 ? now - t_launch : 0;
+    sh.tk[12] = now;
+    sh.tk[14] = __builtin_amdgcn_s_memtime();
+  }
   auto tick = [&](int ph) {
     if (prof) {
       const unsigned long long now = wall_clock64();
-      tk[ph] += now - tprev;
-      tprev = now;
+      sh.tk[ph] += now - sh.tk[12];
+      sh.tk[12] = now;
     }
   };
   bool stopped = false;
@@ -581,7 +773,7 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
     // hand the z row to the neighbours (tagged granules: no drain, they poll them); keep it in
     // LDS for the partial sums
     const int par = epoch & 1;
-    const unsigned rtag = gran_tag(a.seq, epoch + 1);
+    const unsigned rtag = gran_tag(cv.seq, epoch + 1);
     unsigned long long* zout = a.zbuf + ((size_t)par * n + g) * 4 * n;
     if (act) {
       st_gran(zout + 4 * t, rtag, z.x);
@@ -682,9 +874,9 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
       vg[1] = __hip_atomic_load((gu64*)(vp + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     unsigned long long t_red = 0;
-    const unsigned long long t_ar = tprev;
+    const unsigned long long t_ar = prof ? sh.tk[12] : 0;
     if (!allreduce_rows(ar, par, epoch, cols, sh.sum, sh.red, prof ? &t_red : nullptr)) return;
-    if (prof) t_first_hop += t_red - t_ar;
+    if (prof) sh.tk[13] += t_red - t_ar;
     tick(1);
     double2 zl = z2, zh = z2;
     bool zok = true;
@@ -711,7 +903,7 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
     // the Givens workgroup's verdict on column j-2 (published two iterations ago, as a rule;
     // every workgroup polls the same granule, so all stop at the same iteration)
     if (t == 0 && j >= 2) {
-      const unsigned vtag = gran_tag(a.seq, j - 1);
+      const unsigned vtag = gran_tag(cv.seq, j - 1);
       double v = 0.0;
       if ((unsigned)(vg[0] >> 32) == vtag && (unsigned)(vg[1] >> 32) == vtag)
         v = __longlong_as_double((long long)((vg[0] << 32) | (vg[1] & 0xffffffffull)));
@@ -793,8 +985,7 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
     sj = 1.0 / sqrt(fmax(rest, fmax(w2 * 1e-28, 1e-300)));
     tick(2);
     if (__syncthreads_or(!zok)) {  // (a neighbour's z or the verdict never arrived)
-      if (t == 0)
-        __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      raise_timeout();
       return;
     }
     tick(4);
@@ -805,12 +996,12 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
   }
   // shader-clock cycles over the loop (the effective clock: slot 7 / sum of slots); every
   // counter is written at the end of the launch (no global round trip inside the timed spans)
-  tk[7] = prof ? __builtin_amdgcn_s_memtime() - cyc0 : 0;
+  if (prof) sh.tk[7] = __builtin_amdgcn_s_memtime() - sh.tk[14];
   auto tail_tick = [&](int slot) {  // head / tail spans (slots 8 .. 11, written at the end)
     if (prof) {
       const unsigned long long now = wall_clock64();
-      tl[slot - 8] += now - tprev;
-      tprev = now;
+      sh.tk[slot] += now - sh.tk[12];
+      sh.tk[12] = now;
     }
   };
   if (!stopped) {
@@ -824,27 +1015,26 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
       for (int p = t; p < n; p += kWave) s = fma(ul[p].x, ul[p].x, fma(ul[p].y, ul[p].y, s));
       s = wave_sum_to_63(s);
       if (t == kWave - 1)
-        st_gran(ar.part + ((size_t)par * G + g) * 2 * kPStride, gran_tag(a.seq, epoch + 1), s);
+        st_gran(ar.part + ((size_t)par * G + g) * 2 * kPStride, gran_tag(cv.seq, epoch + 1), s);
     }
     epoch++;
     if (!allreduce_rows(ar, par, epoch, 1, sh.sum, sh.red)) return;
   }
   // the column the cycle solved for and y_k / sigma_k, from the Givens workgroup
   {
-    const unsigned ytag = gran_tag(a.seq, 0xff);
+    const unsigned ytag = gran_tag(cv.seq, 0xff);
     bool ok = true;
     if (t == 0) {
       double c = 0.0, pr = 0.0;
       ok = ld_gran(a.ycoef + 4 * kMaxProj, ytag, &c);
-      if (ok && g == 0) ok = ld_gran(a.ycoef + 4 * kMaxProj + 2, ytag, &pr);
+      if (ok) ok = ld_gran(a.ycoef + 4 * kMaxProj + 2, ytag, &pr);
       const int cb = (int)c;
       sh.ctl[1] = cb & 63;
       sh.gv[0] = pr;
       sh.gv[1] = cb >= 64 ? 1.0 : 0.0;
     }
     if (__syncthreads_or(!ok)) {
-      if (t == 0)
-        __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      raise_timeout();
       return;
     }
     const int col = sh.ctl[1];
@@ -854,8 +1044,7 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
       sh.coef[t] = make_double2(cx, cy);
     }
     if (__syncthreads_or(!ok)) {
-      if (t == 0)
-        __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      raise_timeout();
       return;
     }
   }
@@ -882,7 +1071,7 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
   // The next cycle's start (runtime.cpp residual): r = b - A x, V[0] = M r, |r|^2 and |M r|^2,
   // in two more rounds -- the x rows to the neighbours (tagged granules), then a two-column
   // all-reduce -- instead of two launches and a copy after this one.
-  const unsigned xtag = gran_tag(a.seq, epoch + 1);
+  const unsigned xtag = gran_tag(cv.seq, epoch + 1);
   if (act) {
     unsigned long long* xo = a.xbuf + (size_t)g * 4 * n + 4 * t;
     st_gran(xo, xtag, xn.x);
@@ -920,8 +1109,7 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
     sh.zrow[t] = xn;
   }
   if (__syncthreads_or(!xok)) {
-    if (t == 0)
-      __hip_atomic_store((gu32*)a.timeout_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    raise_timeout();
     return;
   }
   tail_tick(10);
@@ -940,6 +1128,12 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
     const double2 rr = csub(b_pt, Ax);
     const double2 mr = JAC ? cdiv(rr, D) : rr;
     a.v0[(size_t)g * n + t] = mr;
+    if (cyc + 1 < a.cycles) {  // the next cycle's ghost rows of V[0]
+      unsigned long long* mo = a.mbuf + (size_t)g * 4 * n + 4 * t;
+      const unsigned mtag = gran_tag(cv.seq, 0xfe);
+      st_gran(mo, mtag, mr.x);
+      st_gran(mo + 2, mtag, mr.y);
+    }
     r2 = cabs2(rr);
     m2 = cabs2(mr);
   }
@@ -962,38 +1156,52 @@ __global__ __launch_bounds__(kSmallBlock) void gmres_small_cycle_kernel(SmallCyc
   if (!allreduce_rows(ar, par, epoch, 2, sh.sum, sh.red)) return;
   tail_tick(11);
   if (prof) {
-    for (int q = 0; q < 8; ++q) a.phase_ticks[q] += tk[q];
-    for (int q = 0; q < 4; ++q) a.phase_ticks[8 + q] += tl[q];
-    a.phase_ticks[15] += t_first_hop;
+    for (int q = 0; q < 12; ++q) a.phase_ticks[q] += sh.tk[q];
+    a.phase_ticks[15] += sh.tk[13];
+  }
+  mn2 = sh.sum[1];  // (|M r|^2; = |r|^2 bit for bit without a preconditioner)
+  // scipy's restart-loop decisions (the end of iterative.py's outer loop, exactly as runtime.cpp
+  // hh_gmres takes them) for the next cycle, on every thread
+  if (a.outer) {
+    const double* o = a.outer;  // ([2] atol, [4] maxiter, [5] legacy: constant during the solve)
+    const double presid = sh.gv[0];
+    const double rn = sqrt(sh.sum[0]);
+    rs_inner += (double)(col + 1);
+    rs_done = (o[5] != 0.0 && rs_inner >= o[4]) || rn <= o[2] || sh.gv[1] != 0.0;
+    if (!rs_done) {
+      rs_pmf = presid <= rs_ptol ? fmax(a.eps, 0.25 * rs_pmf) : fmin(1.0, 1.5 * rs_pmf);
+      rs_ptol = presid * fmin(rs_pmf, o[2] / rn);
+    }
+  } else {
+    rs_done = true;  // (a single cycle as given)
   }
   if (g == 0 && t == 0) {
     a.red[4] = sh.sum[0];  // (device: the next cycle's |r|^2, |M r|^2)
     a.red[5] = sh.sum[1];
-    a.report[4] = sh.sum[0];  // (host: this cycle's report)
-    a.report[5] = sh.sum[1];
-    if (a.outer) {
-      // scipy's restart-loop decisions (the end of iterative.py's outer loop, exactly as
-      // runtime.cpp hh_gmres takes them)
-      // for the cycle queued behind this one
+    cv.report[4] = sh.sum[0];  // (host: this cycle's report)
+    cv.report[5] = sh.sum[1];
+    if (a.outer) {  // for the launch queued behind this one, and the host
       double* o = a.outer;
-      const double presid = sh.gv[0];
-      const double rn = sqrt(sh.sum[0]);
-      const double inner = o[3] + (double)(col + 1);
-      const bool done = (o[5] != 0.0 && inner >= o[4]) || rn <= o[2] || sh.gv[1] != 0.0;
-      double pmf = o[1];
-      if (!done) {
-        pmf = presid <= o[0] ? fmax(a.eps, 0.25 * pmf) : fmin(1.0, 1.5 * pmf);
-        o[0] = presid * fmin(pmf, o[2] / rn);
-        o[1] = pmf;
+      o[0] = rs_ptol;
+      o[1] = rs_pmf;
+      o[3] = rs_inner;
+      o[6] = rs_done ? 1.0 : 0.0;
+      cv.report[6] = o[6];
+      cv.report[7] = o[0];
+      if (cyc + 1 < a.cycles) {  // to the Givens workgroup's next cycle
+        const unsigned otag = gran_tag(cv.seq, 0xfd);
+        st_gran(a.obuf, otag, rs_ptol);
+        st_gran(a.obuf + 2, otag, rs_inner);
+        st_gran(a.obuf + 4, otag, rs_done ? 1.0 : 0.0);
+        st_gran(a.obuf + 6, otag, sh.sum[1]);
       }
-      o[3] = inner;
-      o[6] = done ? 1.0 : 0.0;
-      a.report[6] = o[6];
-      a.report[7] = o[0];
     }
-    a.g.ctrl[1] = col;
-    a.g.ctrl[0] = 1;
+    cv.ctrl[1] = col;
+    cv.ctrl[0] = 1;
   }
+  // (no barrier before the next cycle: its head writes only this thread's own LDS columns and
+  // thread 0's sh.vs[0] / sh.ctl[0], which nothing in this tail reads after the last barrier)
+  }  // cycles
 }
 
 }  // namespace
@@ -1004,14 +1212,16 @@ size_t small_cycle_lds_bytes(int n, int restart) {
   return al(16 * R1 * 3 * n) + al(16 * (size_t)n) + al(16 * (size_t)restart * R1) +
          al(32 * (size_t)restart) + 2 * al(16 * R1) + 2 * al(8 * R1) + al(8 * (size_t)restart) +
          al(8 * (size_t)(kRedRuns + kRuns)) + al(8 * kPStride) + al(16) + al(16) +
-         al(32 * (size_t)restart);
+         al(32 * (size_t)restart) + al(8 * 16);
 }
 
 size_t small_cycle_scratch_doubles(int n) {
   // 8-byte granules: z rows [2][n][4n], x rows [n][4n], the all-reduce rows [2][n][2 kPStride],
-  // the sums of every round [kSmallRounds][2 kPStride], verdicts [kMaxProj][2], y [kMaxProj+1][4]
+  // the sums of every round [kSmallRounds][2 kPStride], verdicts [kMaxProj][2], y [kMaxProj+1][4],
+  // the next cycle's V[0] rows [n][4n] and restart-loop state [8]
   return 12 * (size_t)n * n + 4 * (size_t)kPStride * n + 2 * (size_t)kPStride * kSmallRounds +
-         2 * kMaxProj + 4 * (kMaxProj + 1);
+         2 * kMaxProj + 4 * (kMaxProj + 1) + 4 * (size_t)n * n + 8 +
+         (kSmallThreads + 2) / 2 + 2;  // + the gate: arrival words (u32) and the decision
 }
 
 bool small_cycle_eligible(int n, int restart, int device_cus) {
@@ -1037,19 +1247,12 @@ hipError_t launch_one(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds
     fail(HH_ERR_HIP, "small-grid GMRES cycle: cannot enable %zu B of dynamic LDS (%s)", lds,
          hipGetErrorString(attr));
   }
-  // Cooperative: the workgroups wait on each other (tagged granules), so all n + 1 must be
-  // resident at once; the runtime refuses a grid that cannot be (instead of the waits spinning
-  // to their bound) and the caller then takes the regular cycle.  HH_SMALL_COOP_REFUSE=1 makes
-  // this launch report the refusal without launching (tests the caller's fallback).
-  static const bool refuse = [] {
-    const char* e = std::getenv("HH_SMALL_COOP_REFUSE");
-    return e && e[0] == '1';
-  }();
-  if (refuse) return hipErrorCooperativeLaunchTooLarge;
-  // HH_SMALL_COOP=0: the plain launch of round 2 (co-residency then NOT guaranteed; A/B timing)
+  // Plain launch: co-residency is checked by the kernel's own gate (coresidency_gate), which
+  // refuses a grid that cannot be resident before any state changes.  HH_SMALL_COOP=1 launches
+  // cooperatively instead (the runtime's own residency check; ~55 us per launch), for A/B timing.
   static const bool coop = [] {
     const char* e = std::getenv("HH_SMALL_COOP");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   if (!coop) {
     hipLaunchKernelGGL((gmres_small_cycle_kernel<C, J>), grid, block, lds, s, a);

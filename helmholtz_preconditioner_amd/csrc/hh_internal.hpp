@@ -257,8 +257,21 @@ struct SmallCycleArgs {
   // stop_col / ptol from here and, after its residual, takes scipy's decisions for the next
   // cycle (report[6] = done, report[7] = the next ptol).  nullptr: stop_col / ptol as given.
   double* outer;
+  // cycles in this launch (>= 1; > 1 needs `outer`): cycle c tags with seq + c and reports into
+  // report + c kRedDoubles (statuses at + kRedStatus, control words at + kRedCtrl)
+  int cycles;
+  unsigned long long* obuf;  // [8] granules: the restart-loop state handed to the next cycle
+  unsigned long long* mbuf;  // [n][4n] granules: the next cycle's V[0] rows for the neighbours
+  unsigned* gate_arrive;     // [n + 1] co-residency gate: each workgroup's arrival (seq)
+  unsigned long long* gate_decide;  // the gate's decision word ((seq << 2) | 1 go / 2 abort)
+  int gate_force_abort;      // test hook: workgroup 0 decides ABORT (HH_SMALL_COOP_REFUSE=1)
 };
 constexpr int kOuterDoubles = 8;
+// layout of an operator's reduction buffer `red` and of each slot of its host mirror: [0, 256)
+// reductions, [256, 384) the cycle's per-iteration statuses, [384, 388) control words
+constexpr int kRedDoubles = 512;
+constexpr int kRedStatus = 256;
+constexpr int kRedCtrl = 384;
 constexpr int kSmallTicks = 16;  // phase_ticks: 7 loop phases, shader clock, 4 head / tail spans,
                                  // 3 Givens-workgroup spans
 // columns of the small cycle's all-reduce rows: 2 K dot halves, |z|^2, |u_j|^2 (K <= kMaxProj)
@@ -267,8 +280,9 @@ constexpr int kSmallRounds = kMaxProj + 8;  // all-reduce rounds per launch (<= 
 bool small_cycle_eligible(int n, int restart, int device_cus);
 size_t small_cycle_lds_bytes(int n, int restart);
 size_t small_cycle_scratch_doubles(int n);
-// cooperative launch; returns the runtime's refusal (e.g. a grid that cannot be co-resident)
-// instead of throwing, so the caller can take the regular cycle before any state changed
+// returns a launch error instead of throwing; a grid that cannot be co-resident is refused on the
+// device (report slot 0: ctrl = 3) before any state changed, so the caller can take the regular
+// cycle
 hipError_t launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi, hipStream_t s);
 // End of a cycle: triangular solve for y, ycoef_k = y_k * vscale_k.
 void launch_gmres_solve(const GivensState& g, int col, hipStream_t stream);

@@ -83,14 +83,12 @@ namespace {
 // [0, 256) reductions (norms at 0..15, dots from 16), [256, 384) the cycle's per-iteration
 // statuses (4 x restart), [384, 388) the cycle's control words (ints), [388] the small cycle's
 // timeout word; the end of a cycle copies [0, kRedReport) once
-constexpr int kRedDoubles = 512;
-constexpr int kRedStatus = 256;
-constexpr int kRedCtrl = 384;
 constexpr int kRedTimeout = 388;
 constexpr int kRedReport = 389;
 constexpr int kRedOuter = 400;  // [400, 408): the small cycle's restart-loop state (device only)
-// whole-cycle launches queued behind each other (one host sync per batch); each reports into its
-// own slot of the host mirror, status_h + (1 + i) kRedDoubles
+// restart cycles per whole-cycle launch (gmres_small.hip: one cooperative launch runs a batch,
+// one host sync per batch); cycle i reports into its own slot of the host mirror,
+// status_h + (1 + i) kRedDoubles
 constexpr int kSmallBatch = 16;
 static_assert(kRedOuter >= kRedReport && kRedOuter + kOuterDoubles <= kRedDoubles, "red layout");
 }  // namespace
@@ -1930,14 +1928,15 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
   bool small_refused = false;
   op->last_path = small ? 1 : 0;
   if (small) {
-    // Small grids: whole-cycle launches (gmres_small.hip), up to kSmallBatch queued behind each
-    // other -- scipy's restart-loop decisions are taken on the device from the state below
-    // (bitwise the host's expressions), so a cycle starts a kernel boundary after the previous
-    // one instead of a host round trip.  One sync per batch; the host then replays each cycle's
-    // report: callbacks in order, legacy maxiter, the x callback (which limits a batch to one
-    // cycle, x being observed after every cycle).  A launch queued behind a finished solve
-    // returns at once (ctrl = 2).  An exception raised by a callback ends the solve after the
-    // batch (x is then up to kSmallBatch - 1 cycles further; the Python shim returns no x then).
+    // Small grids: whole-cycle launches (gmres_small.hip), each running up to kSmallBatch restart
+    // cycles -- scipy's restart-loop decisions are taken on the device from the state below
+    // (bitwise the host's expressions), so a cycle starts right after the previous one inside
+    // the same launch instead of after a host round trip.  One cooperative launch and one sync
+    // per batch; the host then replays each cycle's report: callbacks in order, legacy maxiter,
+    // the x callback (which limits a batch to one cycle, x being observed after every cycle).
+    // The cycles after the one that finished the solve are skipped (ctrl = 2).  An exception
+    // raised by a callback ends the solve after the batch (x is then up to kSmallBatch - 1
+    // cycles further; the Python shim returns no x then).
     double* outer_h = op->status_h + kRedOuter;  // (pinned staging for the upload)
     outer_h[0] = ptol;
     outer_h[1] = ptol_max_factor;
@@ -1958,8 +1957,10 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       const long cycles_left =
           legacy ? (maxiter - inner + restart - 1) / restart : maxiter - iteration;
       const int P = (int)std::min<long>(cap, cycles_left);
-      for (int i = 0; i < P; ++i) {
-        double* rep = op->status_h + (size_t)(1 + i) * kRedDoubles;
+      {
+        // ONE cooperative launch runs the batch's P cycles (their restart-loop decisions taken
+        // on the device); cycle i reports into slot 1 + i of the pinned host mirror
+        double* rep = op->status_h + kRedDoubles;
         SmallCycleArgs sa{};
         sa.n = op->n;
         sa.restart = restart;
@@ -1973,13 +1974,10 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         sa.b = b;
         sa.x = x;
         sa.red = op->red;
-        // the cycle's report goes straight to its slot of the pinned host mirror (same layout
-        // as red): no copy after the launch; ctrl[0] = 1 marks it complete
         sa.report = rep;
         sa.g = g;
-        sa.g.status_it = rep + kRedStatus;
-        sa.g.ctrl = reinterpret_cast<int*>(rep + kRedCtrl);
-        sa.g.ctrl[0] = 0;
+        for (int i = 0; i < P; ++i)  // (ctrl[0] = 1 marks a slot's cycle complete)
+          reinterpret_cast<int*>(rep + (size_t)i * kRedDoubles + kRedCtrl)[0] = 0;
         sa.eps = eps;
         sa.ptol = ptol;  // (from `outer`)
         sa.zbuf = reinterpret_cast<unsigned long long*>(op->small_scr);
@@ -1988,8 +1986,20 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         sa.sums = sa.part + 2 * (size_t)op->n * 2 * kSmallCols;
         sa.verdict = sa.sums + (size_t)kSmallRounds * 2 * kSmallCols;
         sa.ycoef = sa.verdict + 2 * kMaxProj;
-        sa.seq = (++op->small_seq) & 0xffffffu;
-        if (sa.seq == 0) sa.seq = op->small_seq = 1;  // (tag 0 is the zeroed scratch)
+        sa.mbuf = sa.ycoef + 4 * (kMaxProj + 1);
+        sa.obuf = sa.mbuf + 4 * (size_t)op->n * op->n;
+        sa.gate_decide = sa.obuf + 8;
+        sa.gate_arrive = reinterpret_cast<unsigned*>(sa.gate_decide + 1);
+        static const bool force_abort = [] {  // test hook: the gate refuses the grid
+          const char* e = std::getenv("HH_SMALL_COOP_REFUSE");
+          return e && e[0] == '1';
+        }();
+        sa.gate_force_abort = force_abort ? 1 : 0;
+        // P consecutive sequence numbers, none 0 (tag 0 is the zeroed scratch)
+        if (((op->small_seq + (unsigned)P) & 0xffffffu) < (unsigned)P) op->small_seq = 0;
+        sa.seq = (op->small_seq + 1) & 0xffffffu;
+        op->small_seq += (unsigned)P;
+        sa.cycles = P;
         sa.timeout_word = small_timeout;
         sa.phase_ticks = op->small_ticks;
         sa.outer = outer;
@@ -1999,15 +2009,22 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
           // be co-resident): the first launch of the solve falls back to the regular cycle, which
           // starts from the same state (V[0] = M r, red[4..5]); a later refusal cannot, as cycles
           // already changed x
-          REQUIRE(iteration == 0 && i == 0,
+          REQUIRE(iteration == 0,
                   "small-grid GMRES: cooperative launch refused after %ld cycles (%s)", iteration,
                   hipGetErrorString(le));
           small_refused = true;
-          break;
         }
       }
       if (small_refused) break;
       HIPC(hipStreamSynchronize(s));
+      if (reinterpret_cast<const int*>(op->status_h + kRedDoubles + kRedCtrl)[0] == 3) {
+        // the kernel's co-residency gate refused the grid before any workgroup touched state
+        REQUIRE(iteration == 0,
+                "small-grid GMRES: workgroups not co-resident after %ld cycles (the GPU is "
+                "shared?); hh_op_set_small_cycle(op, 0) selects the regular cycle", iteration);
+        small_refused = true;
+        break;
+      }
       for (int i = 0; i < P && !done; ++i) {
         const double* rep = op->status_h + (size_t)(1 + i) * kRedDoubles;
         int ctl[2];

@@ -233,15 +233,16 @@ int hh_op_set_krylov_mode(hh_op* op, int mode);
  * hh_gmres as ONE launch whose workgroups keep the Krylov basis on chip and meet once per inner
  * iteration (lagged normalisation as krylov mode 2), instead of five launches per iteration.
  * Applies on a single rank and slab, 5-point operator, M = none or Jacobi, without reorth, when
- * n <= 255 (n + 1 workgroups, one per CU, launched cooperatively) and the basis fits the LDS
- * (3 n (restart + 1) x 16 B <= ~150 KB).  mode -1 (default):
+ * n <= 255 (n + 1 workgroups, one per CU, all resident at once: the kernel's own gate checks
+ * it and refuses the grid before touching any state otherwise) and the basis fits the LDS
+ * (3 n (restart + 1) x 16 B <= ~150 KB); up to 16 restart cycles run per launch.  mode -1 (default):
  * used when it applies and n^2 <= 2^18; 1: whenever it applies; 0: never.  Results agree with the
  * regular cycle to rounding. */
 int hh_op_set_small_cycle(hh_op* op, int mode);
 /* Which cycle form the last hh_gmres on `op` ran: 0 the regular per-launch cycle, 1 the
- * small-grid whole-cycle kernel, 2 the small-grid kernel refused at its first (cooperative)
- * launch -- its n + 1 workgroups could not be co-resident -- so the regular cycle ran the whole
- * solve instead (same results to rounding; no partial state). */
+ * small-grid whole-cycle kernel, 2 the small-grid kernel refused at its first launch -- its
+ * n + 1 workgroups could not be co-resident -- so the regular cycle ran the whole solve
+ * instead (same results to rounding; no partial state). */
 int hh_op_last_solve_path(hh_op* op, int* path);
 /* Diagnostic: phase timing of the small-grid cycle kernel (workgroup 0's wall clock summed over
  * the following solves): phase_us (optional, 8 doubles) receives the totals so far in us

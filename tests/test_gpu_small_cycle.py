@@ -189,8 +189,7 @@ print("ok")
 
 
 def test_small_cycle_path_reported(ctx):
-    """The whole-cycle kernel is launched cooperatively and the operator reports which cycle
-    form ran (hh_op_last_solve_path)."""
+    """The operator reports which cycle form ran (hh_op_last_solve_path)."""
     n = 64
     om, h, eta = O.problem_params(n, 6, 3.0, 2.0)
     A = H.build_A_matrix(6, 61.0, eta, om, h, n, medium("c1", n), context=ctx)
@@ -210,10 +209,11 @@ def test_small_cycle_path_reported(ctx):
 
 
 def test_small_cycle_refused_launch_falls_back():
-    """A cooperative launch the runtime refuses (simulated: HH_SMALL_COOP_REFUSE=1 makes the
-    launch report hipErrorCooperativeLaunchTooLarge without launching) runs the whole solve on
-    the regular cycle -- no spin to a timeout, no partial state -- with the reference's history
-    (golden, 1e-6).  Child process: the knob is read once per process."""
+    """A grid the kernel's co-residency gate refuses (simulated: HH_SMALL_COOP_REFUSE=1 makes
+    workgroup 0 decide ABORT, as when its co-residents never arrive) leaves before touching any
+    state, and the whole solve runs on the regular cycle -- no spin to a timeout, no partial
+    state -- with the reference's history (golden, 1e-6).  Child process: the knob is read once
+    per process."""
     import subprocess
     import sys
     code = r'''
