@@ -219,6 +219,8 @@ struct hh_op {
   double2* sw_uF = nullptr;
   double2* sw_const = nullptr;  // as-is (quirk Q1): M x = algo2_4(b) for every x
   double2* sw_T = nullptr;      // dense transfer matrices (sweep_dense.hip), or null
+  double2* sw_Pf = nullptr;     // chunk products of the partitioned solves, or null
+  double2* sw_Pb = nullptr;
   unsigned long long* sw_chain = nullptr;  // granules of the persistent apply chain, or null
   unsigned sw_seq = 0;                     // its launch sequence number
   double2* sw_u = nullptr;      // dense apply scratch (n^2)
@@ -230,8 +232,9 @@ struct hh_op {
     hipGraphExec_t exec;
   };
   std::vector<SweepGraph> sw_graphs;  // the 2 (n - b) + 1 GEMV launches, captured once
-  int sw_mode = -1;  // -1 auto, 0 block-Thomas solves, 1 dense transfer matrices, 2 dense with
-                     // one launch per GEMV (no persistent chain)
+  int sw_mode = -1;  // -1 auto, 0 block-Thomas solves (partitioned where the chunk products
+                     // fit), 1 dense transfer matrices, 2 dense with one launch per GEMV (no
+                     // persistent chain), 3 block-Thomas sequential solves
   // tuning (hh_op_tune): stencil variant for the plain apply, rows per block override
   int variant = -1;
   int rpb_override = 0;
@@ -1143,6 +1146,8 @@ static void op_release(hh_op* op) {
   dfree(op->small_ticks);
   dfree(op->kcount);
   dfree(op->sw_P);
+  dfree(op->sw_Pf);
+  dfree(op->sw_Pb);
   dfree(op->sw_y);
   dfree(op->sw_uF);
   dfree(op->sw_const);
@@ -1190,7 +1195,7 @@ static void sweep_chain_configure(hh_op* op) {
 // Dense-transfer form of the sweeping preconditioner (sweep_dense.hip): decide, allocate, form.
 static void sweep_dense_configure(hh_op* op) {
   const int n = op->n, b = op->b;
-  if (op->sw_mode == 0) {
+  if (op->sw_mode == 0 || op->sw_mode == 3) {
     sweep_dense_release(op);
     return;
   }
@@ -1236,6 +1241,44 @@ static void sweep_dense_configure(hh_op* op) {
   sweep_chain_configure(op);
 }
 
+// Partitioned block-Thomas solves (sweep.hip bt_solve_chunked) for the forward / backward
+// sweeps when the block-Thomas form is in use: the chunk products Psi_f / Psi_b (2 x the
+// factors' memory) formed once here.  Mode 3, the dense form, n < 2 columns per chunk or a lack
+// of memory keep the sequential solves.
+static void sweep_chunk_configure(hh_op* op) {
+  SweepArgs& a = op->sweep;
+  const int n = op->n, B = sweep_block(op->b);
+  const bool want = !op->sw_T && (op->sw_mode == -1 || op->sw_mode == 0) &&
+                    n >= 2 * kSweepChunks;
+  if (!want) {
+    dfree(op->sw_Pf);
+    dfree(op->sw_Pb);
+    op->sw_Pf = op->sw_Pb = nullptr;
+    a.chunks = 0;
+    a.Pf = a.Pb = nullptr;
+    return;
+  }
+  if (op->sw_Pf) return;
+  const size_t elems = (size_t)a.nsys * n * B * B;
+  size_t free_b = 0, total_b = 0;
+  HIPC(hipMemGetInfo(&free_b, &total_b));
+  if (2 * elems * sizeof(double2) > free_b / 10 * 8) return;  // sequential solves
+  op->sw_Pf = dalloc<double2>(elems);
+  try {
+    op->sw_Pb = dalloc<double2>(elems);
+  } catch (...) {
+    dfree(op->sw_Pf);
+    op->sw_Pf = nullptr;
+    throw;
+  }
+  a.chunks = kSweepChunks;
+  a.Pf = op->sw_Pf;
+  a.Pb = op->sw_Pb;
+  launch_sweep(a, 4, nullptr, nullptr, 0, op->ctx->stream);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(op->ctx->stream));
+}
+
 HH_API int hh_op_set_precond(hh_op* op, int kind, double beta, int sweeps, double damping) {
   GUARD_BEGIN
   REQUIRE(op, "null op");
@@ -1263,7 +1306,8 @@ HH_API int hh_op_set_precond(hh_op* op, int kind, double beta, int sweeps, doubl
       a.nsys = 1 + (n - b);
       op->sw_P = dalloc<double2>((size_t)a.nsys * n * B * B);
       a.ystride = sweep_scratch_per_wave(n);
-      op->sw_y = dalloc<double2>((size_t)std::max(1, a.nsys - 1) * a.ystride);
+      op->sw_y = dalloc<double2>(std::max((size_t)std::max(1, a.nsys - 1) * a.ystride,
+                                          sweep_chunk_scratch(n)));
       op->sw_uF = dalloc<double2>((size_t)b * n);
       a.P = op->sw_P;
       a.yscr = op->sw_y;
@@ -1273,12 +1317,15 @@ HH_API int hh_op_set_precond(hh_op* op, int kind, double beta, int sweeps, doubl
       a.invc2 = op->const_c ? nullptr : op->slabs[0].invc2;
       a.invc2_const = op->invc2_const;
       a.stop = nullptr;
+      a.chunks = 0;
+      a.Pf = a.Pb = nullptr;
       // algo2_3 (code.py:345-353): factor H_F and every H_m, all in parallel
       launch_sweep(a, 0, nullptr, nullptr, 0, op->ctx->stream);
       HIPC(hipGetLastError());
       HIPC(hipStreamSynchronize(op->ctx->stream));
     }
     sweep_dense_configure(op);
+    sweep_chunk_configure(op);
   }
   op->pkind = kind;
   op->beta = beta;
@@ -1674,11 +1721,15 @@ HH_API int hh_op_tune(hh_op* op, int variant, int rows_per_block, int grid_block
 HH_API int hh_op_sweep_mode(hh_op* op, int mode, int* active) {
   GUARD_BEGIN
   REQUIRE(op, "null op");
-  REQUIRE(mode >= -1 && mode <= 2, "mode must be -1, 0, 1 or 2");
+  REQUIRE(mode >= -1 && mode <= 3, "mode must be -1, 0, 1, 2 or 3");
   HIPC(hipSetDevice(op->ctx->device));
   op->sw_mode = mode;
-  if (op->sw_P) sweep_dense_configure(op);  // already factored: switch now
-  if (active) *active = op->sw_T ? 1 : 0;
+  if (op->sw_P) {  // already factored: switch now
+    if (mode == 1 || mode == 2) sweep_chunk_configure(op);  // release before the dense setup
+    sweep_dense_configure(op);
+    sweep_chunk_configure(op);
+  }
+  if (active) *active = op->sw_T ? 1 : (op->sweep.chunks > 0 ? 2 : 0);
   GUARD_END
 }
 

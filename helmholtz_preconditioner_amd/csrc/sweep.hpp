@@ -18,13 +18,26 @@ struct SweepArgs {
   double2* yscr;       // per-wave solve scratch, ystride double2 each (sweep_scratch_per_wave)
   size_t ystride;
   const int* stop;     // GMRES cycle stop flag (kernels return at once when set)
+  // chunked solves (partitioned Thomas): chunks = kSweepChunks splits the columns of every
+  // system into that many contiguous chunks (0: the sequential solves); per (system, column) the B x B
+  // products of the recurrence matrices inside its chunk -- forward Psi_f[i] = M_i .. M_a,
+  // M_i = -P_i L_i; backward Psi_b[i] = N_i .. N_{e-1}, N_i = -P_i U_i -- laid out as P
+  int chunks;
+  double2* Pf;
+  double2* Pb;
 };
 
 int sweep_block(int b);
 size_t sweep_scratch_per_wave(int n);  // padded block size B (4, 8, 12, 16) or 0 if b > 16
-// what: 0 factor (one wave per system), 1 forward sweep, 2 middle sweep, 3 backward sweep
+// what: 0 factor (one wave per system), 1 forward sweep, 2 middle sweep, 3 backward sweep,
+// 4 the chunk products Psi_f / Psi_b (after 0; needs a.chunks > 0, Pf, Pb).  With a.chunks > 0
+// the forward and backward sweeps run every solve partitioned over the chunks: one workgroup
+// of kSweepChunks / 2 waves, dependent depth ~2 (n / chunks + chunks) steps instead of 2 n.
 void launch_sweep(const SweepArgs& a, int what, double2* u, double2* uF, int asis,
                   hipStream_t st);
+constexpr int kSweepChunks = 16;  // chunks per partitioned solve (two per wave)
+// scratch (double2) of one partitioned solve: the n B-vectors + the chunk boundary vectors
+size_t sweep_chunk_scratch(int n);
 
 // Dense-transfer form (sweep_dense.hip): n matrices of n x n -- A_ll^-1 (l < b) of H_F, then
 // T_m (m = b+1 .. n) -- formed at setup from the block-Thomas factors; the apply is a GEMV chain.

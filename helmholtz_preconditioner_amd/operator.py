@@ -391,14 +391,17 @@ class Sweeping(DevicePreconditioner):
     sweep is sequential in the layer index).
     """
 
-    FORMS = {"auto": -1, "thomas": 0, "dense": 1, "dense-launches": 2}
+    FORMS = {"auto": -1, "thomas": 0, "dense": 1, "dense-launches": 2, "thomas-sequential": 3}
 
     def __init__(self, A: DeviceOperator, reference: bool = False, form: str = "auto"):
         """``form``: ``"dense"`` forms the n matrices T_m (n^3 x 16 B of HBM) at setup and
         applies M as a chain of GEMVs; ``"thomas"`` keeps O(n^2 b^2) block-Thomas factors
-        and solves; ``"auto"`` picks dense when n <= 2048 and it fits; ``"dense-launches"``
-        is the dense form with one launch per GEMV instead of the persistent chain (n <= 1024).
-        Same results to rounding (the two dense forms bit for bit)."""
+        and solves, each forward / backward-sweep solve partitioned over 16 column chunks
+        (3 x the factors' memory; sequential when that does not fit); ``"thomas-sequential"``
+        the unpartitioned solves (2n dependent steps each, least memory); ``"auto"`` picks
+        dense when n <= 2048 and it fits, else ``"thomas"``; ``"dense-launches"`` is the dense
+        form with one launch per GEMV instead of the persistent chain (n <= 1024).  Same
+        results to rounding (the two dense forms bit for bit)."""
         self.kind = _ffi.HH_PREC_SWEEP_REF if reference else _ffi.HH_PREC_SWEEP
         if form not in self.FORMS:
             raise ValueError(f"form must be one of {sorted(self.FORMS)}")
@@ -411,4 +414,5 @@ class Sweeping(DevicePreconditioner):
         check(lib.hh_op_sweep_mode(A.handle, self.FORMS[self.form], ctypes.byref(active)))
         super().configure()
         check(lib.hh_op_sweep_mode(A.handle, self.FORMS[self.form], ctypes.byref(active)))
-        self.dense = bool(active.value)
+        self.dense = active.value == 1
+        self.partitioned = active.value == 2  # chunked block-Thomas solves

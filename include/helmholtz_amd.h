@@ -288,13 +288,17 @@ int hh_op_set_stencil(hh_op* op, int points, double alpha, double c, double d);
 int hh_op_sl_fusion(hh_op* op, int enable);
 /* Sweeping preconditioner form (speed / memory only; results agree to rounding):
  *   mode -1 (default) dense transfer matrices when n <= 2048 and the n^3 x 16 B fit in HBM,
- *           else block-Thomas solves;  0 block-Thomas solves (O(n^2 b^2) memory, every solve
- *           2n dependent steps);  1 dense transfer matrices (error if they do not fit), their
+ *           else as mode 0;  0 block-Thomas solves, the forward / backward sweeps' solves
+ *           partitioned over 16 column chunks (chunk products: 2 x the factors' O(n^2 b^2)
+ *           memory; dependent depth ~2 (n/16 + 16) steps per solve) when n >= 32 and they fit,
+ *           else sequential;  1 dense transfer matrices (error if they do not fit), their
  *           GEMV chain as ONE persistent cooperative launch when n <= 1024 (else one launch per
  *           GEMV);  2 dense, one launch per GEMV always (HH_SWEEP_CHAIN=0 does the same for
- *           modes -1 and 1).  The dense forms give the same results bit for bit.
+ *           modes -1 and 1);  3 block-Thomas sequential solves (2n dependent steps each).  The
+ *           dense forms give the same results bit for bit, the others agree to rounding.
  * Applies at the next sweeping setup, or at once if the operator is already factored.
- * active (optional) receives 1 when the dense form is in use. */
+ * active (optional) receives 1 when the dense form is in use, 2 for partitioned solves,
+ * 0 for sequential ones. */
 int hh_op_sweep_mode(hh_op* op, int mode, int* active);
 /* Process-wide tuning of the Krylov streaming kernels (multidot / update): non-temporal
  * basis loads on (1) / off (0) / by vector length (-1, default: on above 2^21 rank-local

@@ -180,3 +180,70 @@ def test_sweep_persistent_chain_bit_identical_to_launches(ctx, n, b, kind):
                                callback_type="legacy", return_history=True))
         (x1, i1, h1), (x2, i2, h2) = out
         assert i1 == i2 and np.array_equal(h1, h2) and np.array_equal(x1, x2)
+
+
+# ------------------------------------------------------- partitioned block-Thomas solves
+@pytest.mark.parametrize("name", ["sweep_n48_c1.npz", "sweep_n37_c2.npz"])
+@pytest.mark.parametrize("form", ["thomas", "thomas-sequential"])
+def test_sweep_thomas_as_is_matches_reference_golden(ctx, name, form):
+    """the solve forms (n >= 32: "thomas" partitions every forward / backward-sweep solve over
+    16 column chunks) against the reference's own algo2_4 outputs"""
+    z = load_golden(name)
+    A, (b, C, eta, om, h, n, cm) = _case(z, ctx)
+    M = H.Sweeping(A, reference=True, form=form)
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    assert relerr(M @ f, z["u_f"]) < 1e-10
+    assert M.partitioned == (form == "thomas")
+    assert relerr(M @ rand_complex(n * n, 3), z["u_x"]) < 1e-10
+
+
+@pytest.mark.parametrize("n,b,kind", [(32, 5, "c1"), (33, 12, "c2"), (61, 5, "c1"),
+                                      (96, 12, "c1"), (130, 8, "const"), (200, 16, "c2"),
+                                      (257, 3, "c1")])
+def test_sweep_partitioned_vs_sequential_and_oracle(ctx, n, b, kind):
+    """ragged chunks (n not a multiple of 8), every block size B = 4, 8, 12, 16, both sweeps"""
+    om, h, eta = O.problem_params(n, b, 5.0, 2.0)
+    cm = medium(kind, n)
+    A = H.build_A_matrix(b, 81.0, eta, om, h, n, cm, context=ctx)
+    x = rand_complex(n * n, n + 3)
+    st = O.SweepState(b, 81.0, eta, om, h, n, cm) if n <= 200 else None
+    for reference in (False, True):
+        Mp = H.Sweeping(A, reference=reference, form="thomas")
+        yp = Mp @ x
+        assert Mp.partitioned and not Mp.dense
+        Ms = H.Sweeping(A, reference=reference, form="thomas-sequential")
+        ys = Ms @ x
+        assert not Ms.partitioned and not Ms.dense
+        assert relerr(yp, ys) < 1e-10
+        if st is not None:
+            assert relerr(yp, st.apply(x, corrected=not reference)) < 1e-10
+
+
+def test_gmres_partitioned_sweeping_vs_oracle(ctx):
+    z = load_golden("sweep_n48_c1.npz")
+    A, (b, C, eta, om, h, n, cm) = _case(z, ctx)
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    Aref = O.build_A_matrix(b, C, eta, om, h, n, cm)
+    Mref, _ = O.sweeping_preconditioner(b, C, eta, om, h, n, cm, corrected=True)
+    xr, infor, histr, _ = O.gmres_reference(Aref, f, M=Mref, rtol=1e-3, restart=20, maxiter=200)
+    x, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=200,
+                            M=H.Sweeping(A, form="thomas"), callback=lambda r: None,
+                            callback_type="legacy", return_history=True)
+    assert info == infor == 0 and len(hist) == len(histr)
+    assert np.max(np.abs(hist - histr) / histr) < 1e-6
+    assert relerr(x, xr) < 1e-6
+
+
+def test_sweep_partitioned_large_linearity(ctx):
+    """n = 4095 (beyond the dense form's n <= 2048): the partitioned corrected-sweep apply runs
+    and is linear to rounding, M (x + 2i y) = M x + 2i M y (no oracle at this size)"""
+    n, b = 4095, 12
+    om, h, eta = O.problem_params(n, b, 100.0, 2.0)
+    A = H.build_A_matrix(b, 81.0, eta, om, h, n, O.init_c1_mat(.5, .5, n), context=ctx)
+    M = H.Sweeping(A, form="auto")
+    M.configure()
+    assert M.partitioned
+    x, y = rand_complex(n * n, 1), rand_complex(n * n, 2)
+    mx, my, mxy = M @ x, M @ y, M @ (x + 2j * y)
+    assert np.all(np.isfinite(mxy))
+    assert relerr(mxy, mx + 2j * my) < 1e-10

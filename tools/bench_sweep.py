@@ -1,6 +1,8 @@
 """Sweeping preconditioner (row F1) timings on the device vs the reference's SuperLU path
 (oracle restatement of algo2_3 / algo2_4 on this host's CPU).
-usage: python tools/bench_sweep.py [--form dense|thomas|auto] [n ...]
+usage: python tools/bench_sweep.py [--form dense|thomas|thomas-sequential|auto] [--maxiter K]
+                                   [n ...]
+--maxiter 0 skips the GMRES solve (default 300; large n with the solve forms takes ~1 s/apply)
 
 Dense-form apply algorithmic bytes: every transfer matrix read once by the fused
 forward+middle pass and once by the backward pass: 2 (n - b) n^2 16 B + b n^2 16 B (F0)
@@ -17,9 +19,13 @@ import helmholtz_preconditioner_amd as H  # noqa: E402
 from helmholtz_preconditioner_amd import _ffi  # noqa: E402
 
 args = sys.argv[1:]
-form = "auto"
-if args and args[0] == "--form":
-    form, args = args[1], args[2:]
+form, maxiter = "auto", 300
+while args and args[0].startswith("--"):
+    if args[0] == "--form":
+        form = args[1]
+    elif args[0] == "--maxiter":
+        maxiter = int(args[1])
+    args = args[2:]
 ns = [int(v) for v in args] or [127, 255, 511, 1023]
 for n in ns:
     b, C, wn = 12, {127: 81.0, 255: 62.0, 511: 81.0, 1023: 100.0}.get(n, 81.0), n // 8 + 1
@@ -35,20 +41,24 @@ for n in ns:
     x, y = A.vector(f.ravel()), A.vector()
     A.apply_device(x, y, _ffi.HH_APPLY_PREC)
     t0 = time.perf_counter()
-    reps = 10 if Msw.dense else 2
+    reps = 10 if Msw.dense or n <= 1023 else 2
     for _ in range(reps):
         A.apply_device(x, y, _ffi.HH_APPLY_PREC)
     A.ctx.synchronize()
     t_apply = (time.perf_counter() - t0) / reps
-    t0 = time.perf_counter()
-    u, info, hist = H.gmres(A, f.ravel(), rtol=1e-3, restart=20, maxiter=300, M=Msw,
-                            callback=lambda r: None, callback_type="legacy", return_history=True)
-    t_solve = time.perf_counter() - t0
+    hist, info, t_solve = [], None, 0.0
+    if maxiter > 0:
+        t0 = time.perf_counter()
+        u, info, hist = H.gmres(A, f.ravel(), rtol=1e-3, restart=20, maxiter=maxiter, M=Msw,
+                                callback=lambda r: None, callback_type="legacy",
+                                return_history=True)
+        t_solve = time.perf_counter() - t0
     gbs = ""
     if Msw.dense:
         alg = (2 * (n - b) + b + 1) * n * n * 16
         gbs = f" ({alg / t_apply / 1e9:.0f} GB/s algorithmic, dense)"
-    line = (f"n={n} b={b} wn={wn} form={form}: setup {t_setup*1e3:.1f} ms, apply {t_apply*1e3:.2f} ms{gbs}, "
+    kind = "dense" if Msw.dense else ("partitioned" if Msw.partitioned else "sequential")
+    line = (f"n={n} b={b} wn={wn} form={form} ({kind}): setup {t_setup*1e3:.1f} ms, apply {t_apply*1e3:.2f} ms{gbs}, "
             f"corrected-sweep GMRES {len(hist)} its info={info} in {t_solve:.3f} s")
     if n <= 255 and os.path.isdir(os.path.join(ROOT, "oracle")):
         from oracle import helmholtz_oracle as O

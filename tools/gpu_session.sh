@@ -15,7 +15,7 @@
 #   pmc[:ARGS]           FETCH_SIZE and WRITE_SIZE, one rocprofv3 --pmc pass each, of
 #                        tools/prof_stencil.py ARGS (default --iters 20)
 #   pmcset               the same at every BASELINE config's grid, summarised into pmc_traffic.json
-#   py:SCRIPT[,ARGS]     python tools/SCRIPT ARGS (diagnostics, tuning sweeps)
+#   py:SCRIPT[,ARGS]     python tools/SCRIPT ARGS (diagnostics, tuning sweeps; limit PY_SECS, 420)
 #   rocpy:SCRIPT[,ARGS]  the same under rocprofv3 --kernel-trace --stats
 # example: tools/gpu_session.sh r03a tests smoke bench driver rocprof pmc
 set -u
@@ -75,7 +75,7 @@ for st in "$@"; do
                  "$OUT/${nm}_WRITE_SIZE/run_counter_collection.csv" --n "$pn" --medium "$pm" \
                  --stencil "$ps" --merge "$OUT/pmc_traffic.json" || true
              done ;;
-    py)      run "py_$(slug "$arg")" 420 python "tools/${A[0]}" "${A[@]:1}" ;;
+    py)      run "py_$(slug "$arg")" "${PY_SECS:-420}" python "tools/${A[0]}" "${A[@]:1}" ;;
     rocpy)   name="rocpy_$(slug "$arg")"
              run "$name" 420 rocprofv3 --kernel-trace --stats -d "$OUT/$name" -o run \
                --output-format csv -- python3 "tools/${A[0]}" "${A[@]:1}" ;;
