@@ -221,6 +221,9 @@ struct hh_op {
   double2* sw_T = nullptr;      // dense transfer matrices (sweep_dense.hip), or null
   double2* sw_Pf = nullptr;     // chunk products of the partitioned solves, or null
   double2* sw_Pb = nullptr;
+  double2* sw_Pw = nullptr;     // workgroup maps of the multi-workgroup partitioned solves
+  unsigned long long* sw_gran = nullptr;  // their grid-exchange granules
+  int sw_wgs = 0;               // requested workgroups per partitioned solve (0: by n)
   unsigned long long* sw_chain = nullptr;  // granules of the persistent apply chain, or null
   unsigned sw_seq = 0;                     // its launch sequence number
   double2* sw_u = nullptr;      // dense apply scratch (n^2)
@@ -617,8 +620,15 @@ void sweep_apply(hh_op* op, const double2* r, double2* out, bool asis) {
   launch_scale_copy(r, out, op->nloc, 1.0, s, op->stop_flag);
   SweepArgs a = op->sweep;
   a.stop = op->stop_flag;
+  // the partitioned sweeps tag their grid exchange with a per-launch sequence number
+  auto next_seq = [&] {
+    a.seq = (++op->sw_seq) & 0x1ffffu;
+    if (a.seq == 0) a.seq = op->sw_seq = 1;  // (tag 0 is the zeroed buffer)
+  };
+  next_seq();
   launch_sweep(a, 1, out, op->sw_uF, 0, s);
   launch_sweep(a, 2, out, op->sw_uF, asis ? 1 : 0, s);
+  next_seq();
   launch_sweep(a, 3, out, op->sw_uF, 0, s);
   HIPC(hipGetLastError());
 }
@@ -747,16 +757,18 @@ void read_dev(hh_op* op, const double* dsrc, double* hdst, int count) {
 // ran a chained sweep apply checks the word here (one synchronising read; nothing for the other
 // preconditioners) and clears it only after the check, so no timeout is lost or reported twice.
 void check_sweep_chain(hh_op* op) {
-  if (!op->sw_chain || !is_sweep(op->pkind)) return;
+  const bool grid = op->sw_chain || (!op->sw_T && op->sweep.chunks > 0 && op->sweep.G > 1);
+  if (!grid || !is_sweep(op->pkind)) return;
   double w = 0.0;
   read_dev(op, op->red + kRedTimeout, &w, 1);
   unsigned tmo = 0;
   std::memcpy(&tmo, &w, sizeof(unsigned));
   if (tmo != 0) {
     HIPC(hipMemset(op->red + kRedTimeout, 0, sizeof(double)));
-    fail(HH_ERR_STATE, "sweeping preconditioner: the persistent apply chain timed out "
-                       "(workgroups not co-resident?); HH_SWEEP_CHAIN=0 selects one launch "
-                       "per GEMV");
+    fail(HH_ERR_STATE, "sweeping preconditioner: a grid-wide wait of the persistent apply "
+                       "chain or of the partitioned solves timed out (workgroups not "
+                       "co-resident?); HH_SWEEP_CHAIN=0 / hh_op_sweep_workgroups(op, 1) select "
+                       "forms without grid waits");
   }
 }
 
@@ -1148,6 +1160,8 @@ static void op_release(hh_op* op) {
   dfree(op->sw_P);
   dfree(op->sw_Pf);
   dfree(op->sw_Pb);
+  dfree(op->sw_Pw);
+  dfree(op->sw_gran);
   dfree(op->sw_y);
   dfree(op->sw_uF);
   dfree(op->sw_const);
@@ -1242,38 +1256,68 @@ static void sweep_dense_configure(hh_op* op) {
 }
 
 // Partitioned block-Thomas solves (sweep.hip bt_solve_chunked) for the forward / backward
-// sweeps when the block-Thomas form is in use: the chunk products Psi_f / Psi_b (2 x the
-// factors' memory) formed once here.  Mode 3, the dense form, n < 2 columns per chunk or a lack
-// of memory keep the sequential solves.
+// sweeps when the block-Thomas form is in use: G workgroups of kSweepChunks chunks each share
+// every solve (G by n: ~4 columns per chunk, at most sweep_part_max_wgs(B) and the CU count;
+// hh_op_sweep_workgroups overrides it).  The chunk products Psi_f / Psi_b (2 x the factors'
+// memory) and the workgroup maps are formed once here.  Mode 3, the dense form, n < 2 columns
+// per chunk or a lack of memory keep the sequential solves.
+static void sweep_part_release(hh_op* op) {
+  dfree(op->sw_Pf);
+  dfree(op->sw_Pb);
+  dfree(op->sw_Pw);
+  dfree(op->sw_gran);
+  op->sw_Pf = op->sw_Pb = op->sw_Pw = nullptr;
+  op->sw_gran = nullptr;
+  SweepArgs& a = op->sweep;
+  a.chunks = 0;
+  a.G = 0;
+  a.Pf = a.Pb = a.Pw = nullptr;
+  a.gran = nullptr;
+}
+
+static int sweep_part_wgs(hh_op* op) {
+  const int n = op->n, B = sweep_block(op->b);
+  int cus = 0;
+  HIPC(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, op->ctx->device));
+  int G = op->sw_wgs > 0 ? op->sw_wgs : n / (4 * kSweepChunks);
+  G = std::min({G, sweep_part_max_wgs(B), cus, n / (2 * kSweepChunks)});
+  return std::max(G, 1);
+}
+
 static void sweep_chunk_configure(hh_op* op) {
   SweepArgs& a = op->sweep;
   const int n = op->n, B = sweep_block(op->b);
   const bool want = !op->sw_T && (op->sw_mode == -1 || op->sw_mode == 0) &&
                     n >= 2 * kSweepChunks;
   if (!want) {
-    dfree(op->sw_Pf);
-    dfree(op->sw_Pb);
-    op->sw_Pf = op->sw_Pb = nullptr;
-    a.chunks = 0;
-    a.Pf = a.Pb = nullptr;
+    sweep_part_release(op);
     return;
   }
-  if (op->sw_Pf) return;
+  const int G = sweep_part_wgs(op);
+  if (op->sw_Pf && a.G == G) return;
+  sweep_part_release(op);
   const size_t elems = (size_t)a.nsys * n * B * B;
+  const size_t welems = (size_t)a.nsys * G * 2 * B * B;
   size_t free_b = 0, total_b = 0;
   HIPC(hipMemGetInfo(&free_b, &total_b));
-  if (2 * elems * sizeof(double2) > free_b / 10 * 8) return;  // sequential solves
-  op->sw_Pf = dalloc<double2>(elems);
+  if ((2 * elems + welems) * sizeof(double2) > free_b / 10 * 8) return;  // sequential solves
   try {
+    op->sw_Pf = dalloc<double2>(elems);
     op->sw_Pb = dalloc<double2>(elems);
+    op->sw_Pw = dalloc<double2>(welems);
+    op->sw_gran = dalloc<unsigned long long>(sweep_part_granules(G));
   } catch (...) {
-    dfree(op->sw_Pf);
-    op->sw_Pf = nullptr;
+    sweep_part_release(op);
     throw;
   }
-  a.chunks = kSweepChunks;
+  HIPC(hipMemset(op->sw_gran, 0, sweep_part_granules(G) * sizeof(unsigned long long)));
+  a.chunks = kSweepChunks * G;
+  a.G = G;
   a.Pf = op->sw_Pf;
   a.Pb = op->sw_Pb;
+  a.Pw = op->sw_Pw;
+  a.gran = op->sw_gran;
+  a.timeout = reinterpret_cast<unsigned*>(op->red + kRedTimeout);
   launch_sweep(a, 4, nullptr, nullptr, 0, op->ctx->stream);
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(op->ctx->stream));
@@ -1730,6 +1774,17 @@ HH_API int hh_op_sweep_mode(hh_op* op, int mode, int* active) {
     sweep_chunk_configure(op);
   }
   if (active) *active = op->sw_T ? 1 : (op->sweep.chunks > 0 ? 2 : 0);
+  GUARD_END
+}
+
+HH_API int hh_op_sweep_workgroups(hh_op* op, int workgroups, int* active) {
+  GUARD_BEGIN
+  REQUIRE(op, "null op");
+  REQUIRE(workgroups >= 0 && workgroups <= 1024, "workgroups must be in [0, 1024]");
+  HIPC(hipSetDevice(op->ctx->device));
+  op->sw_wgs = workgroups;
+  if (op->sw_P) sweep_chunk_configure(op);
+  if (active) *active = (!op->sw_T && op->sweep.chunks > 0) ? op->sweep.G : 0;
   GUARD_END
 }
 

@@ -22,6 +22,7 @@
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
 #include "sweep.hpp"
+#include "hh_error.hpp"
 
 #include <type_traits>
 
@@ -313,14 +314,19 @@ __device__ __forceinline__ void bt_solve(const SweepArgs& a, int s, const SolveI
 
 // ------------------------------------------------------- partitioned (chunked) solves
 // The forward recurrence y_i = P_i (r_i - L_i y_{i-1}) = c_i + M_i y_{i-1} and the backward one
-// x_i = y_i + N_i x_{i+1} (M_i = -P_i L_i, N_i = -P_i U_i) are linear in the carried vector, so
+// x_i = y_i + N_i x_{i+1} (M_i = -P_i L_i, N_i = -P_i U_i) are affine in the carried vector, so
 // with the columns split into K chunks [lo_k, hi_k):
 //   y_i = yL_i + Psi_f[i] y_{lo_k - 1},   Psi_f[i] = M_i M_{i-1} .. M_{lo_k}
 //   x_i = xL_i + Psi_b[i] x_{hi_k},       Psi_b[i] = N_i N_{i+1} .. N_{hi_k - 1}
-// where yL / xL run the recurrence inside the chunk from a zero carry.  A solve is then: every
-// chunk's local recurrence at once (one wave per chunk), the K chunk boundaries in sequence
-// (one B x B matvec each), and a parallel fix-up of every column -- dependent depth ~2 (n / K +
-// K) steps instead of 2 n.  The Psi products are operator data, formed once at setup.
+// where yL / xL run the recurrence inside the chunk from a zero carry.  The chunks are grouped
+// kSweepChunks to a workgroup and G workgroups share a solve; the chunk-end maps compose into
+// one map per workgroup, Phi_f(g) = Psi_f[end_15] .. Psi_f[end_0] (Phi_b likewise), so a
+// carry crosses a workgroup in one B x B step.  A solve is then: every chunk's local
+// recurrence at once, a chain over the workgroup's 16 chunk boundaries, ONE exchange of the
+// workgroups' zero-carry end vectors, a chain over the other workgroups' maps, the chunk chain
+// again with the true carry, and a parallel fix-up of every column -- dependent depth
+// ~2 (n / K + 2 kSweepChunks + G) steps instead of 2 n.  Psi and Phi are operator data,
+// formed once at setup.
 __device__ __forceinline__ int chunk_lo(int n, int K, int k) { return n * k / K; }  // n K < 2^31
 
 __device__ __forceinline__ void wave_sync() {
@@ -329,14 +335,15 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Setup: Psi_f and Psi_b of one (system, chunk) per wave.  Lanes (g, j): row j, columns
-// [g KG, (g+1) KG) of the running product, which every lane reads whole from LDS.
+// Setup: Psi_f and Psi_b of one (system, chunk) per wave (K = a.chunks chunks per system).
+// Lanes (g, j): row j, columns [g KG, (g+1) KG) of the running product, which every lane
+// reads whole from LDS.
 template <int B>
 __global__ __launch_bounds__(kSW) void sweep_chunk_setup_kernel(const SweepArgs a) {
   constexpr int KG = B / kGroups;
   constexpr size_t PS = (size_t)B * B;
   __shared__ double2 Q[2][B][B];
-  constexpr int K = kSweepChunks;
+  const int K = a.chunks;
   const int n = a.n;
   const int s = blockIdx.x / K, k = blockIdx.x % K;
   const int lo = chunk_lo(n, K, k), hi = chunk_lo(n, K, k + 1);
@@ -387,8 +394,73 @@ __global__ __launch_bounds__(kSW) void sweep_chunk_setup_kernel(const SweepArgs 
   }
 }
 
+// Setup: the workgroup maps of one (system, workgroup) per wave (after the chunk products):
+// Phi_f(g) = Psi_f[end_15] .. Psi_f[end_0] and Phi_b(g) = Psi_b[lo_0] .. Psi_b[lo_15] over the
+// workgroup's kSweepChunks chunks (end_k / lo_k: the chunk's last / first column).
 template <int B>
-constexpr int chunk_ring() { return B <= 8 ? 4 : (B == 12 ? 2 : 3); }  // (no spills at 256 VGPRs)
+__global__ __launch_bounds__(kSW) void sweep_wg_setup_kernel(const SweepArgs a) {
+  constexpr int KG = B / kGroups;
+  constexpr size_t PS = (size_t)B * B;
+  __shared__ double2 Q[2][B][B];
+  const int n = a.n, G = a.G, K = a.chunks;
+  const int s = blockIdx.x / G, wg = blockIdx.x % G;
+  const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+  const bool row = j < B;
+  const int jl = row ? j : B - 1;
+  const double2 z = make_double2(0.0, 0.0);
+  for (int dir = 0; dir < 2; ++dir) {
+    const double2* src = (dir == 0 ? a.Pf : a.Pb) + (size_t)s * n * PS;
+    double2* out = a.Pw + (((size_t)s * G + wg) * 2 + dir) * PS;
+    for (int q = 0; q < kSweepChunks; ++q) {  // forward: chunks in order; backward: from the last
+      const int k = kSweepChunks * wg + (dir == 0 ? q : kSweepChunks - 1 - q);
+      const int col = dir == 0 ? chunk_lo(n, K, k + 1) - 1 : chunk_lo(n, K, k);
+      double2 prow[B];
+      sfor<0, B>([&](auto mc) {
+        constexpr int m = decltype(mc)::value;
+        prow[m] = src[((size_t)col * B + jl) * B + m];
+      });
+      double2 v[KG];
+      sfor<0, KG>([&](auto c2) {
+        constexpr int c = decltype(c2)::value;
+        const int cx = g * KG + c;
+        double2 acc = z;
+        if (q == 0) {
+          sfor<0, B>([&](auto mc) {
+            constexpr int m = decltype(mc)::value;
+            acc = csel(m == cx, prow[m], acc);
+          });
+        } else {
+          sfor<0, B>([&](auto mc) {
+            constexpr int m = decltype(mc)::value;
+            acc = cfma(prow[m], Q[(q - 1) & 1][m][cx], acc);
+          });
+        }
+        v[c] = acc;
+      });
+      if (row) {
+        sfor<0, KG>([&](auto c2) {
+          constexpr int c = decltype(c2)::value;
+          Q[q & 1][j][g * KG + c] = v[c];
+          if (q == kSweepChunks - 1) out[(size_t)j * B + g * KG + c] = v[c];
+        });
+      }
+      wave_sync();
+    }
+  }
+}
+
+template <int B>
+constexpr int chunk_ring() { return B <= 4 ? 4 : (B == 8 ? 3 : 2); }  // (no spills at 256 VGPRs)
+template <int B>
+constexpr int part_max_wgs() { return B <= 12 ? 32 : 12; }  // (LDS of the grid chain's maps)
+constexpr int kPartThreads = kSweepChunks / 2 * kSW;      // 8 waves, two chunks each
+constexpr unsigned kPartSpin = 1u << 20;                   // ~1 s of polling per wait
+// dynamic LDS of a partitioned solve: the chain maps [kSweepChunks + G - 1][B B], then the
+// other workgroups' published vectors [G][16]
+template <int B>
+size_t part_lds_bytes(int G) {
+  return ((size_t)(kSweepChunks + G - 1) * B * B + (size_t)G * 16) * sizeof(double2);
+}
 
 // base[byte offset]: a scalar base plus a 32-bit lane offset in bytes is the form the
 // global_load/store saddr addressing takes (no 64-bit address pair per lane)
@@ -406,38 +478,73 @@ __device__ __forceinline__ double sum2(double v) {
   return __hiloint2double(h16[0], l16[0]) + __hiloint2double(h16[1], l16[1]);
 }
 
-// One partitioned solve by a block of kSweepChunks / 2 waves, with the SolveIO contract of
-// bt_solve.  Each 32-lane half of a wave owns one chunk (chunk c = 2 w + h): lanes (g, j) of
-// the half -- row j of the block, columns [g KG, (g+1) KG), KG = B / 2 -- so the two chunks of
-// a wave step in lockstep (their lengths differ by at most one column: the shorter one's last
-// step runs on clamped data and is not stored).  Half-wave chunks give 16 chunks with 8 waves,
-// i.e. 256 VGPRs per lane instead of the 128 a 16-wave block allows.  ys: sweep_chunk_scratch.
-//   1. forward, chunk-local (every half): yL_i = P_i (r_i - L_i yL_{i-1}), from yL_{lo-1} = 0
-//   2. forward boundaries (wave 0, K - 1 steps): y_{hi_k - 1} = yL + Psi_f y_{hi_{k-1} - 1}
-//   3. forward fix-up (rows independent): y_i = yL_i + Psi_f[i] y_{lo-1}; then backward,
-//      chunk-local: xL_i = y_i - P_i U_i xL_{i+1} (a wave reads back only its own rows)
-//   4. backward boundaries (wave 0): x_{lo_k} = xL_{lo_k} + Psi_b x_{lo_{k+1}}
-//   5. fix-up + output (rows independent, prefetched like 1 / 3): x_i = xL_i + Psi_b[i] x_{hi}
-// (chunk 0 in 3 and chunk K-1 in 5 multiply their Psi rows by an LDS zero vector instead of
-// branching: both halves run one instruction stream.)  A ring slot of KG = 6 double2 is 24
-// VGPRs at B = 12, so no phase keeps two matrix rings.
+// Granule tags of the grid exchange: launch sequence number, solve (round) and direction.  A
+// slot [dir][round & 1][g] is rewritten two rounds later at the earliest, which no reader of it
+// can reach first (each round's backward exchange needs every later workgroup past the forward
+// one, and the next round's forward exchange every earlier workgroup past this backward one).
+__device__ __forceinline__ unsigned part_tag(unsigned seq, int round, int dir) {
+  return (seq << 15) | ((unsigned)(round & 0x3fff) << 1) | (unsigned)dir;
+}
+using gu64p = __attribute__((address_space(1))) unsigned long long*;
+__device__ __forceinline__ void st_gran4(unsigned long long* p, unsigned tag, double2 v) {
+  const unsigned long long tt = (unsigned long long)tag << 32;
+  const unsigned long long hx = (unsigned long long)__double_as_longlong(v.x);
+  const unsigned long long hy = (unsigned long long)__double_as_longlong(v.y);
+  __hip_atomic_store((gu64p)p, tt | (hx >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((gu64p)(p + 1), tt | (hx & 0xffffffffull), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((gu64p)(p + 2), tt | (hy >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((gu64p)(p + 3), tt | (hy & 0xffffffffull), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One partitioned solve, with the SolveIO contract of bt_solve, by workgroup wg = blockIdx.x of
+// a.G (all co-resident).  Each 32-lane half of a wave owns one chunk (local chunk cl = 2 w + h,
+// global chunk kSweepChunks wg + cl): lanes (g, j) of the half -- row j of the block, columns
+// [g KG, (g+1) KG), KG = B / 2 -- so the two chunks of a wave step in lockstep (their lengths
+// differ by at most one column: the shorter one's last step runs on clamped data and is not
+// stored).  Half-wave chunks give 16 chunks with 8 waves, i.e. 256 VGPRs per lane.  ys:
+// sweep_chunk_scratch.  Per direction (forward shown; backward mirrors it from the right):
+//   1. chunk-local (every half): yL_i = P_i (r_i - L_i yL_{i-1}), from yL_{lo-1} = 0
+//   2. the chain maps staged in LDS (chunk ends' Psi_f, earlier workgroups' Phi_f); wave 0:
+//      chunk boundaries from a zero workgroup carry, y_end_k = yL_end_k + Psi_f y_end_{k-1},
+//      the last one published as granules; waves 1..7 meanwhile poll the earlier workgroups'
+//   3. wave 0: the workgroup's carry y_in = chain of the earlier workgroups' vectors through
+//      their Phi_f, then the chunk boundaries again from y_in (G = 1: step 2 alone)
+//   4. fix-up (rows independent): y_i = yL_i + Psi_f[i] y_{lo-1}; then backward, chunk-local:
+//      xL_i = y_i - P_i U_i xL_{i+1} (a wave reads back only its own rows); 2-3 backward; then
+//   5. fix-up + output (rows independent, prefetched like 1 / 4): x_i = xL_i + Psi_b[i] x_{hi}
+// (chunk 0 in 4 and chunk 15 in 5 multiply their Psi rows by the workgroup carry, zero for the
+// first / last workgroup, instead of branching: both halves run one instruction stream.)  A
+// ring slot of KG = 6 double2 is 24 VGPRs at B = 12, so no phase keeps two matrix rings.  ok:
+// false once a grid wait of this workgroup timed out (no further waits; garbage output and
+// a.timeout set for the host).
 template <int B, bool SR, bool SO>
-__device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, const SolveIO& io,
-                                                 double2* ys) {
+__device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int round,
+                                                 const SolveIO& io, double2* ys, bool& ok) {
   constexpr int KG = B / 2;
   constexpr int D = chunk_ring<B>();
-  constexpr int K = kSweepChunks;
-  constexpr size_t PS = (size_t)B * B;
+  constexpr int KL = kSweepChunks;
+  constexpr int PS = B * B;
   constexpr unsigned PSB = (unsigned)PS * 16u;  // bytes of one B x B matrix
-  __shared__ double2 tl[K][2][16];
-  __shared__ double2 bf[K + 1][16], bb[K + 1][16];  // [K]: zeros
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63, h = lane >> 5, g = (lane >> 4) & 1, j = lane & 15;
-  const int c = 2 * w + h;  // this half's chunk
-  const int n = a.n;
+  constexpr int NQ = 4 * B;                     // granules of one published vector
+  extern __shared__ double2 part_lds[];
+  __shared__ double2 tl[KL][2][16];
+  __shared__ double2 bf[KL + 2][16], bb[KL + 2][16];  // [KL]: workgroup carry, [KL + 1]: zeros
+  __shared__ double2 gv[2][16];
+  __shared__ double2 yvl[KL][16];  // the chunk-end (forward) / chunk-start (backward) vectors
+  const int tid = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, h = lane >> 5, g = (lane >> 4) & 1, j = lane & 15;
+  const int n = a.n, G = a.G, wg = blockIdx.x, K = KL * G;
+  double2* mats = part_lds;                                 // [KL + G - 1][PS]
+  double2* gin = part_lds + (size_t)(KL + G - 1) * PS;      // [G][16]
+  const int cl = 2 * w + h;  // this half's local chunk
+  const int c = KL * wg + cl;
   const int lo = chunk_lo(n, K, c), hi = chunk_lo(n, K, c + 1), len = hi - lo;
-  const int m0 = chunk_lo(n, K, 2 * w + 1);
-  const int lenw = max(m0 - chunk_lo(n, K, 2 * w), chunk_lo(n, K, 2 * w + 2) - m0);  // both halves
+  const int m0 = chunk_lo(n, K, KL * wg + 2 * w + 1);
+  const int lenw = max(m0 - chunk_lo(n, K, KL * wg + 2 * w),
+                       chunk_lo(n, K, KL * wg + 2 * w + 2) - m0);  // both halves
   const int last = len - 1;  // (n >= 2 K: every chunk has >= 2 columns)
   const bool row = j < B && j < a.b;
   const int jl = j < B ? j : B - 1;
@@ -448,7 +555,8 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, cons
   const unsigned ooff =
       (row && j >= io.out_first) ? (unsigned)((j - io.out_first) * io.out_ld) * 16u : 0u;
   const unsigned lofs = (unsigned)(jl * B + g * KG) * 16u;  // row jl, this lane's columns
-  const unsigned dofs = ((unsigned)(n * 16) + threadIdx.x) * 16u;  // this lane's dummy slot
+  const unsigned dofs =
+      ((unsigned)(n * 16) + (unsigned)wg * kPartThreads + (unsigned)tid) * 16u;  // dummy slot
   const size_t sbase = (size_t)s * n * PS;
   const double2* P = a.P + sbase;
   const double2* Pf = a.Pf + sbase;
@@ -464,8 +572,8 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, cons
     sfor<0, KG>([&](auto cc) { m[decltype(cc)::value] = at(base, o + 16u * decltype(cc)::value); });
   };
   auto yget = [&](int i) { return at(ys, ((unsigned)i * 16u + (unsigned)jl) * 16u); };
-  auto yput = [&](bool ok, int i, double2 v) {
-    at(ys, ok ? ((unsigned)i * 16u + (unsigned)j) * 16u : dofs) = v;
+  auto yput = [&](bool ok_, int i, double2 v) {
+    at(ys, ok_ ? ((unsigned)i * 16u + (unsigned)j) * 16u : dofs) = v;
   };
   // this lane's KG entries against entries [g KG, (g+1) KG) of an LDS 16-vector, summed over
   // the half's two lane groups
@@ -477,10 +585,157 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, cons
     });
     return make_double2(sum2(acc.x), sum2(acc.y));
   };
-  if (threadIdx.x < 16) {
-    bf[K][threadIdx.x] = z;
-    bb[K][threadIdx.x] = z;
-  }
+  // the same with row jl of staged map mi (LDS)
+  auto rowdot_m = [&](int mi, const double2* vec) {
+    const double2* mr = mats + mi * PS + jl * B + g * KG;
+    double2 acc = z;
+    sfor<0, KG>([&](auto cc) {
+      constexpr int q = decltype(cc)::value;
+      acc = cfma(mr[q], vec[g * KG + q], acc);
+    });
+    return make_double2(sum2(acc.x), sum2(acc.y));
+  };
+  // the chain maps of direction dir into LDS: map k < KL is local chunk k's end map (forward:
+  // Psi_f at its last column; backward: Psi_b at its first), map KL + q the q-th other
+  // workgroup's Phi (forward: workgroups 0 .. wg-1; backward: wg+1 .. G-1)
+  auto stage = [&](int dir) {
+    const int tot = (KL + (dir == 0 ? wg : G - 1 - wg)) * PS;
+    const double2* cp = dir == 0 ? Pf : Pb;
+    for (int e0 = tid; e0 < tot; e0 += 4 * kPartThreads) {
+      double2 v[4];
+      sfor<0, 4>([&](auto uc) {
+        const int e = min(e0 + (int)decltype(uc)::value * kPartThreads, tot - 1);
+        const int mi = e / PS, off = e - mi * PS;
+        const double2* src;
+        if (mi < KL) {
+          const int k = KL * wg + mi;
+          src = cp + (size_t)(dir == 0 ? chunk_lo(n, K, k + 1) - 1 : chunk_lo(n, K, k)) * PS + off;
+        } else {
+          const int og = dir == 0 ? mi - KL : wg + 1 + (mi - KL);
+          src = a.Pw + (((size_t)s * G + og) * 2 + dir) * PS + off;
+        }
+        v[decltype(uc)::value] = *src;
+      });
+      sfor<0, 4>([&](auto uc) {
+        const int e = e0 + (int)decltype(uc)::value * kPartThreads;
+        if (e < tot) mats[e] = v[decltype(uc)::value];
+      });
+    }
+  };
+  // waves 1..7: wait for the vectors the grid chain needs (forward: workgroups 0 .. wg-1,
+  // backward: wg+1 .. G-1) and unpack them into gin
+  auto poll = [&](int dir) {
+    const int first = dir == 0 ? 0 : wg + 1;
+    const int nq = (dir == 0 ? wg : G - 1 - wg) * NQ;
+    const int q0 = tid - kSW;
+    if (q0 < 0 || q0 >= nq || !ok) return;
+    constexpr int PQ = 4;
+    constexpr int STEP = kPartThreads - kSW;
+    const unsigned tg = part_tag(a.seq, round, dir);
+    const unsigned long long* gb =
+        a.gran + (size_t)(dir * 2 + (round & 1)) * G * kSweepGranStride;
+    unsigned long long v[PQ];
+    unsigned spins = 0;
+    for (;;) {
+      sfor<0, PQ>([&](auto pc) {
+        const int q = min(q0 + (int)decltype(pc)::value * STEP, nq - 1);
+        v[decltype(pc)::value] = __hip_atomic_load(
+            (gu64p)(gb + (size_t)(first + q / NQ) * kSweepGranStride + q % NQ), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+      });
+      bool all = true;
+      sfor<0, PQ>([&](auto pc) {
+        const int q = q0 + (int)decltype(pc)::value * STEP;
+        all = all && (q >= nq || (unsigned)(v[decltype(pc)::value] >> 32) == tg);
+      });
+      if (all) break;
+      if (++spins > kPartSpin) {
+        ok = false;
+        __hip_atomic_store((__attribute__((address_space(1))) unsigned*)a.timeout, 1u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    unsigned* g32 = reinterpret_cast<unsigned*>(gin);
+    sfor<0, PQ>([&](auto pc) {
+      const int q = q0 + (int)decltype(pc)::value * STEP;
+      if (q < nq) {  // granule r of a vector: row r / 4, part r % 4 = x hi, x lo, y hi, y lo
+        const int gi = q / NQ, r = q % NQ;
+        g32[(gi * 16 + (r >> 2)) * 4 + ((r & 3) ^ 1)] = (unsigned)v[decltype(pc)::value];
+      }
+    });
+  };
+  // wave 0: chain over the local chunk boundaries, bv[k] = yv[k] + map_k bv[prev], prev = the
+  // neighbour chunk (forward k - 1, backward k + 1) or `start` for the first step
+  auto chain = [&](auto fwdc, double2 (*bv)[16], int start) {
+    constexpr bool fwd = decltype(fwdc)::value;
+    double2 v = z;
+    sfor<0, KL>([&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      constexpr int k = fwd ? q : KL - 1 - q;
+      const int prev = q == 0 ? start : (fwd ? k - 1 : k + 1);
+      v = cadd(yvl[k][jl], rowdot_m(k, &bv[prev][0]));
+      if (lane < 16) bv[k][lane] = v;
+      wave_sync();
+    });
+    return v;
+  };
+  // wave 0: the workgroup's carry from the other workgroups' vectors (gin) through their maps,
+  // into bv[KL] (forward: from workgroup 0 up; backward: from workgroup G-1 down)
+  auto gchain = [&](double2 (*bv)[16], int dir) {
+    const int cnt = dir == 0 ? wg : G - 1 - wg;
+    if (lane < 16) gv[0][lane] = z;
+    wave_sync();
+    int cur = 0;
+    for (int q = 0; q < cnt; ++q) {
+      const int gi = dir == 0 ? q : cnt - 1 - q;
+      const double2 v = cadd(gin[gi * 16 + jl], rowdot_m(KL + gi, &gv[cur][0]));
+      if (lane < 16) gv[cur ^ 1][lane] = v;
+      wave_sync();
+      cur ^= 1;
+    }
+    if (lane < 16) bv[KL][lane] = gv[cur][lane];
+    wave_sync();
+  };
+  // steps 2-3 of one direction (after the chunk-local pass and its barrier)
+  auto boundaries = [&](auto dirc, double2 (*bv)[16]) {
+    constexpr int dir = decltype(dirc)::value;
+    constexpr bool fwd = dir == 0;
+    const auto fwdc = std::integral_constant<bool, fwd>{};
+    stage(dir);
+    if (tid < KL * 16) {  // (rows j >= B: copies of row B - 1, never used)
+      const int k = tid >> 4;
+      yvl[k][tid & 15] = at(ys, ((unsigned)(fwd ? chunk_lo(n, K, KL * wg + k + 1) - 1
+                                                : chunk_lo(n, K, KL * wg + k)) * 16u +
+                                 (unsigned)min(tid & 15, B - 1)) * 16u);
+    }
+    if (tid < 16) {
+      bv[KL][tid] = z;
+      bv[KL + 1][tid] = z;
+    }
+    __syncthreads();
+    if (G == 1) {
+      if (w == 0) chain(fwdc, bv, KL + 1);
+    } else {
+      const int cnt = fwd ? wg : G - 1 - wg;
+      if (w == 0) {
+        const double2 v = chain(fwdc, bv, KL + 1);
+        const bool other = fwd ? wg + 1 < G : wg > 0;  // someone reads it
+        if (other && lane < B)
+          st_gran4(a.gran + ((size_t)(dir * 2 + (round & 1)) * G + wg) * kSweepGranStride +
+                       4 * lane, part_tag(a.seq, round, dir), v);
+      } else {
+        poll(dir);
+      }
+      ok = __syncthreads_and(ok);
+      if (w == 0 && cnt > 0) {
+        gchain(bv, dir);
+        chain(fwdc, bv, KL);
+      }
+    }
+    __syncthreads();
+  };
 
   // ---- 1. forward, chunk-local ----
   {
@@ -502,44 +757,18 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, cons
         const int q = q0 + r;
         double2 rr = csel(has_rhs, rq[r], z);
         if constexpr (SR) rr = cmul(rr, cmul(io.rmul, sq[r]));
-        tl[c][r & 1][j] = csub(rr, cmul(cmul(cq[r], R2), y));
+        tl[cl][r & 1][j] = csub(rr, cmul(cmul(cq[r], R2), y));
         wave_sync();
-        y = rowdot(Pq[r], &tl[c][r & 1][0]);
+        y = rowdot(Pq[r], &tl[cl][r & 1][0]);
         yput(ystore && q < len, lo + q, y);
         ld(qc, q + D);
       });
     }
   }
   __syncthreads();
-  // ---- 2. forward boundaries (wave 0; both halves compute the same values) ----
-  if (w == 0) {
-    double2 v = yget(chunk_lo(n, K, 1) - 1);
-    if (lane < 16) bf[0][j] = v;
-    double2 mq[D][KG], yq[D];
-    auto ld = [&](auto qc, int k) {
-      constexpr int r = decltype(qc)::value;
-      const int e = chunk_lo(n, K, min(k, K - 1) + 1) - 1;
-      ld_row(mq[r], Pf, e);
-      yq[r] = yget(e);
-    };
-    sfor<0, D>([&](auto qc) { ld(qc, 1 + decltype(qc)::value); });
-    wave_sync();
-#pragma unroll 1
-    for (int k0 = 1; k0 < K; k0 += D) {
-      sfor<0, D>([&](auto qc) {
-        constexpr int r = decltype(qc)::value;
-        const int k = k0 + r;
-        if (k < K) {  // (wave-uniform)
-          v = cadd(yq[r], rowdot(mq[r], &bf[k - 1][0]));
-          if (lane < 16) bf[k][j] = v;
-          wave_sync();
-        }
-        ld(qc, k + D);
-      });
-    }
-  }
-  __syncthreads();
-  // ---- 3. forward fix-up (rows independent): y_i = yL_i + Psi_f[i] y_{lo-1} ----
+  // ---- 2-3. forward boundaries ----
+  boundaries(std::integral_constant<int, 0>{}, bf);
+  // ---- 4. forward fix-up (rows independent): y_i = yL_i + Psi_f[i] y_{lo-1} ----
   {
     double2 mq[D][KG], yq[D];
     auto ld = [&](auto qc, int q) {
@@ -549,7 +778,7 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, cons
       yq[r] = yget(i);
     };
     sfor<0, D>([&](auto qc) { ld(qc, decltype(qc)::value); });
-    const double2* carry = &bf[c > 0 ? c - 1 : K][0];
+    const double2* carry = &bf[cl > 0 ? cl - 1 : KL][0];
     for (int q0 = 0; q0 < lenw; q0 += D) {
       sfor<0, D>([&](auto qc) {
         constexpr int r = decltype(qc)::value;
@@ -560,7 +789,7 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, cons
       });
     }
   }
-  // ---- 3b. backward, chunk-local: xL_i = y_i - P_i U_i xL_{i+1} (own rows: no barrier) ----
+  // ---- 4b. backward, chunk-local: xL_i = y_i - P_i U_i xL_{i+1} (own rows: no barrier) ----
   {
     double2 Pq[D][KG], cq[D], yq[D];
     auto ld = [&](auto qc, int q) {
@@ -577,43 +806,17 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, cons
         constexpr int r = decltype(qc)::value;
         __builtin_amdgcn_sched_barrier(0);
         const int q = q0 + r;
-        tl[c][r & 1][j] = cmul(cmul(cq[r], R2), x);
+        tl[cl][r & 1][j] = cmul(cmul(cq[r], R2), x);
         wave_sync();
-        x = csub(yq[r], rowdot(Pq[r], &tl[c][r & 1][0]));
+        x = csub(yq[r], rowdot(Pq[r], &tl[cl][r & 1][0]));
         yput(ystore && q < len, hi - 1 - q, x);
         ld(qc, q + D);
       });
     }
   }
   __syncthreads();
-  // ---- 4. backward boundaries (wave 0) ----
-  if (w == 0) {
-    double2 v = yget(chunk_lo(n, K, K - 1));
-    if (lane < 16) bb[K - 1][j] = v;
-    double2 mq[D][KG], yq[D];
-    auto ld = [&](auto qc, int t) {  // t = 1 .. K-1: chunk k = K - 1 - t
-      constexpr int r = decltype(qc)::value;
-      const int e = chunk_lo(n, K, max(K - 1 - t, 0));
-      ld_row(mq[r], Pb, e);
-      yq[r] = yget(e);
-    };
-    sfor<0, D>([&](auto qc) { ld(qc, 1 + decltype(qc)::value); });
-    wave_sync();
-#pragma unroll 1
-    for (int t0 = 1; t0 < K; t0 += D) {
-      sfor<0, D>([&](auto qc) {
-        constexpr int r = decltype(qc)::value;
-        const int t = t0 + r, k = K - 1 - t;
-        if (t < K) {
-          v = cadd(yq[r], rowdot(mq[r], &bb[k + 1][0]));
-          if (lane < 16) bb[k][j] = v;
-          wave_sync();
-        }
-        ld(qc, t + D);
-      });
-    }
-  }
-  __syncthreads();
+  // ---- 2-3. backward boundaries ----
+  boundaries(std::integral_constant<int, 1>{}, bb);
   // ---- 5. fix-up + output ----
   {
     double2 mq[D][KG], xq[D], oq[D], sq[SO ? D : 1];
@@ -626,7 +829,7 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, cons
       if constexpr (SO) sq[r] = R1[i];
     };
     sfor<0, D>([&](auto qc) { ld(qc, decltype(qc)::value); });
-    const double2* carry = &bb[c < K - 1 ? c + 1 : K][0];
+    const double2* carry = &bb[cl < KL - 1 ? cl + 1 : KL][0];
     for (int q0 = 0; q0 < lenw; q0 += D) {
       sfor<0, D>([&](auto qc) {
         constexpr int r = decltype(qc)::value;
@@ -660,37 +863,57 @@ __device__ __forceinline__ SolveIO solve_io(const double2* rhs, int rhs_first, d
 }
 
 // the sequential sweeps' solves: one wave walking the columns, or (CH) the partitioned solve
-// of one workgroup of kSweepChunks / 2 waves
+// of a.G workgroups of kSweepChunks / 2 waves (round: the solve's index in the launch)
 template <int B, bool SR, bool SO, bool CH>
-__device__ __forceinline__ void solve(const SweepArgs& a, int s, const SolveIO& io, double2* ys) {
+__device__ __forceinline__ void solve(const SweepArgs& a, int s, int round, const SolveIO& io,
+                                      double2* ys, bool& ok) {
   if constexpr (CH)
-    bt_solve_chunked<B, SR, SO>(a, s, io, ys);
+    bt_solve_chunked<B, SR, SO>(a, s, round, io, ys, ok);
   else
     bt_solve<B, SR, SO>(a, s, io, ys);
+}
+
+// the columns a workgroup of a partitioned launch owns (all n for the sequential one)
+template <bool CH>
+__device__ __forceinline__ void own_columns(const SweepArgs& a, int& c0, int& c1) {
+  c0 = 0;
+  c1 = a.n;
+  if constexpr (CH) {
+    const int K = kSweepChunks * a.G;
+    c0 = chunk_lo(a.n, K, kSweepChunks * (int)blockIdx.x);
+    c1 = chunk_lo(a.n, K, kSweepChunks * ((int)blockIdx.x + 1));
+  }
 }
 
 // Algorithm 2.4 pieces.  u: layer-major [n][n] (layer j at u + j n).
 // forward sweep (code.py:363-370): TFuF = HF^-1 u[0:b] -> uF; u[b] -= S_b * TFuF[b-1];
 // for m = b+1..n-1: u[m] -= S_m * T_m u[m-1]  (S_m = BS_m R1[i], folded into the solve).
+// Partitioned: a workgroup reads and writes only its own columns of u and uF between solves.
 template <int B, bool CH>
-__global__ __launch_bounds__(CH ? kSweepChunks / 2 * kSW : kSW) void sweep_forward_kernel(
+__global__ __launch_bounds__(CH ? kPartThreads : kSW) void sweep_forward_kernel(
     const SweepArgs a, double2* u, double2* uF) {
   if (a.stop && *a.stop) return;
   const int n = a.n, b = a.b;
   const double2 one = make_double2(1.0, 0.0);
   double2* ys = a.yscr;
-  solve<B, false, false, CH>(a, 0, solve_io(u, 0, one, uF, 0, 0.0, one, n), ys);
+  bool ok = true;
+  int round = 0;
+  solve<B, false, false, CH>(a, 0, round++, solve_io(u, 0, one, uF, 0, 0.0, one, n), ys, ok);
   const double2* R1 = a.tab_i + 2 * n;
+  int c0, c1;
+  own_columns<CH>(a, c0, c1);
   {
     const double2 BS = a.tab_glob[4 * b + 1];  // c3 of global layer b (code.py:150-153)
-    for (int i = threadIdx.x; i < n; i += blockDim.x)
+    for (int i = c0 + threadIdx.x; i < c1; i += blockDim.x)
       u[(size_t)b * n + i] = csub(u[(size_t)b * n + i], cmul(cmul(BS, R1[i]), uF[(size_t)(b - 1) * n + i]));
   }
   __syncthreads();
   for (int m = b + 1; m < n; ++m) {  // system s = m - b covers layers m-b .. m-1
     const double2 BS = a.tab_glob[4 * m + 1];
-    solve<B, false, true, CH>(a, m - b, solve_io(u + (size_t)(m - 1) * n, b - 1, one,
-                                               u + (size_t)m * n, b - 1, 1.0, cneg(BS), n), ys);
+    solve<B, false, true, CH>(a, m - b, round++,
+                              solve_io(u + (size_t)(m - 1) * n, b - 1, one, u + (size_t)m * n,
+                                       b - 1, 1.0, cneg(BS), n),
+                              ys, ok);
   }
 }
 
@@ -715,22 +938,53 @@ __global__ __launch_bounds__(kSW) void sweep_middle_kernel(const SweepArgs a, do
 // F correction (code.py:381-384): uF -= HF^-1 [0 .. 0, N_{b-1} u[b]]; u[0:b] = uF.
 // N_{m-1} = BN_{m-1} R1[i] is folded into the solve's right-hand-side load.
 template <int B, bool CH>
-__global__ __launch_bounds__(CH ? kSweepChunks / 2 * kSW : kSW) void sweep_backward_kernel(
+__global__ __launch_bounds__(CH ? kPartThreads : kSW) void sweep_backward_kernel(
     const SweepArgs a, double2* u, double2* uF) {
   if (a.stop && *a.stop) return;
   const int n = a.n, b = a.b;
   double2* ys = a.yscr;
   const double2 mone = make_double2(-1.0, 0.0);
+  bool ok = true;
+  int round = 0;
   for (int m = n - 1; m >= b + 1; --m) {
     const double2 BN = a.tab_glob[4 * (m - 1) + 2];  // c4 of global layer m-1 (code.py:131-140)
-    solve<B, true, false, CH>(a, m - b, solve_io(u + (size_t)m * n, b - 1, BN,
-                                               u + (size_t)(m - 1) * n, b - 1, 1.0, mone, n), ys);
+    solve<B, true, false, CH>(a, m - b, round++,
+                              solve_io(u + (size_t)m * n, b - 1, BN, u + (size_t)(m - 1) * n,
+                                       b - 1, 1.0, mone, n),
+                              ys, ok);
   }
   // H_F is block diagonal: only its last layer sees the (last-layer-only) right-hand side
   const double2 BN = a.tab_glob[4 * (b - 1) + 2];
-  solve<B, true, false, CH>(a, 0, solve_io(u + (size_t)b * n, b - 1, BN, uF + (size_t)(b - 1) * n,
-                                          b - 1, 1.0, mone, n), ys);
-  for (size_t p = threadIdx.x; p < (size_t)b * n; p += blockDim.x) u[p] = uF[p];
+  solve<B, true, false, CH>(a, 0, round++,
+                            solve_io(u + (size_t)b * n, b - 1, BN, uF + (size_t)(b - 1) * n, b - 1,
+                                     1.0, mone, n),
+                            ys, ok);
+  int c0, c1;
+  own_columns<CH>(a, c0, c1);
+  for (int l = 0; l < b; ++l)
+    for (int i = c0 + threadIdx.x; i < c1; i += blockDim.x)
+      u[(size_t)l * n + i] = uF[(size_t)l * n + i];
+}
+
+// a partitioned sweep: G workgroups of kPartThreads, all co-resident (a cooperative launch
+// when G > 1, so a grid that cannot be placed fails at launch instead of waiting forever)
+template <int B>
+void launch_part(const void* fn, const SweepArgs& a, double2* u, double2* uF, hipStream_t st) {
+  const size_t lds = part_lds_bytes<B>(a.G);
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e == hipSuccess) {
+    SweepArgs arg = a;
+    void* params[] = {&arg, &u, &uF};
+    e = a.G > 1 ? hipLaunchCooperativeKernel(fn, dim3(a.G), dim3(kPartThreads), params,
+                                             (unsigned)lds, st)
+                : hipLaunchKernel(fn, dim3(1), dim3(kPartThreads), params, lds, st);
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    fail(HH_ERR_HIP, "sweeping preconditioner: launch of the partitioned sweep over %d "
+                     "workgroups (%zu B of LDS each) failed (%s)",
+         a.G, lds, hipGetErrorString(e));
+  }
 }
 
 template <int B>
@@ -741,8 +995,7 @@ void launch_all(const SweepArgs& a, int what, double2* u, double2* uF, int asis,
       break;
     case 1:
       if (a.chunks > 0)
-        hipLaunchKernelGGL((sweep_forward_kernel<B, true>), dim3(1), dim3(kSweepChunks / 2 * kSW), 0, st,
-                           a, u, uF);
+        launch_part<B>(reinterpret_cast<const void*>(&sweep_forward_kernel<B, true>), a, u, uF, st);
       else
         hipLaunchKernelGGL((sweep_forward_kernel<B, false>), dim3(1), dim3(kSW), 0, st, a, u, uF);
       break;
@@ -752,14 +1005,14 @@ void launch_all(const SweepArgs& a, int what, double2* u, double2* uF, int asis,
       break;
     case 3:
       if (a.chunks > 0)
-        hipLaunchKernelGGL((sweep_backward_kernel<B, true>), dim3(1), dim3(kSweepChunks / 2 * kSW), 0, st,
-                           a, u, uF);
+        launch_part<B>(reinterpret_cast<const void*>(&sweep_backward_kernel<B, true>), a, u, uF, st);
       else
         hipLaunchKernelGGL((sweep_backward_kernel<B, false>), dim3(1), dim3(kSW), 0, st, a, u, uF);
       break;
     case 4:
-      hipLaunchKernelGGL((sweep_chunk_setup_kernel<B>), dim3(a.nsys * kSweepChunks), dim3(kSW), 0, st,
-                         a);
+      hipLaunchKernelGGL((sweep_chunk_setup_kernel<B>), dim3(a.nsys * a.chunks), dim3(kSW), 0,
+                         st, a);
+      hipLaunchKernelGGL((sweep_wg_setup_kernel<B>), dim3(a.nsys * a.G), dim3(kSW), 0, st, a);
       break;
     default:
       break;
@@ -769,7 +1022,12 @@ void launch_all(const SweepArgs& a, int what, double2* u, double2* uF, int asis,
 }  // namespace
 
 size_t sweep_scratch_per_wave(int n) { return (size_t)(n + kMaxRing) * 16 + 64; }
-size_t sweep_chunk_scratch(int n) { return (size_t)n * 16 + kSweepChunks * kSW; }
+size_t sweep_chunk_scratch(int n) { return (size_t)n * 16 + (size_t)32 * kPartThreads; }
+int sweep_part_max_wgs(int B) {
+  return B == 4 ? part_max_wgs<4>() : B == 8 ? part_max_wgs<8>() : B == 12 ? part_max_wgs<12>()
+                                                                          : part_max_wgs<16>();
+}
+size_t sweep_part_granules(int G) { return (size_t)2 * 2 * G * kSweepGranStride; }
 
 int sweep_block(int b) { return b <= 4 ? 4 : (b <= 8 ? 8 : (b <= 12 ? 12 : (b <= 16 ? 16 : 0))); }
 

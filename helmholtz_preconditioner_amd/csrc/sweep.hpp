@@ -25,19 +25,35 @@ struct SweepArgs {
   int chunks;
   double2* Pf;
   double2* Pb;
+  // multi-workgroup partitioned solves: G workgroups (one persistent cooperative launch per
+  // sweep), kSweepChunks chunks each (chunks = kSweepChunks G).  Pw [nsys][G][2][B][B]: per
+  // workgroup the product of its forward (0) / backward (1) chunk maps (sweep_wg_setup_kernel).
+  // Carries cross workgroups as tagged granules, gran [2 dir][2 parity][G][kSweepGranStride].
+  int G;
+  double2* Pw;
+  unsigned long long* gran;
+  unsigned* timeout;  // set when a grid wait gives up (the output is then garbage)
+  unsigned seq;       // launch sequence number of the granule tags (1 .. 2^17 - 1)
 };
 
 int sweep_block(int b);
 size_t sweep_scratch_per_wave(int n);  // padded block size B (4, 8, 12, 16) or 0 if b > 16
 // what: 0 factor (one wave per system), 1 forward sweep, 2 middle sweep, 3 backward sweep,
-// 4 the chunk products Psi_f / Psi_b (after 0; needs a.chunks > 0, Pf, Pb).  With a.chunks > 0
-// the forward and backward sweeps run every solve partitioned over the chunks: one workgroup
-// of kSweepChunks / 2 waves, dependent depth ~2 (n / chunks + chunks) steps instead of 2 n.
+// 4 the chunk products Psi_f / Psi_b and the workgroup products Pw (after 0; needs a.chunks =
+// kSweepChunks a.G > 0, Pf, Pb, Pw).  With a.chunks > 0 the forward and backward sweeps run
+// every solve partitioned over the chunks: a.G workgroups of kSweepChunks / 2 waves (one
+// cooperative launch per sweep when G > 1), dependent depth ~2 (n / chunks + 2 kSweepChunks
+// + G) steps instead of 2 n.
 void launch_sweep(const SweepArgs& a, int what, double2* u, double2* uF, int asis,
                   hipStream_t st);
-constexpr int kSweepChunks = 16;  // chunks per partitioned solve (two per wave)
-// scratch (double2) of one partitioned solve: the n B-vectors + the chunk boundary vectors
+constexpr int kSweepChunks = 16;  // chunks per workgroup of a partitioned solve (two per wave)
+constexpr int kSweepGranStride = 64;  // u64 granules per (direction, parity, workgroup)
+// scratch (double2) of one partitioned solve: the n B-vectors + per-thread dummy slots
 size_t sweep_chunk_scratch(int n);
+// largest workgroup count of a partitioned solve for block size B (LDS of the grid chain)
+int sweep_part_max_wgs(int B);
+// u64 granules of SweepArgs::gran for G workgroups
+size_t sweep_part_granules(int G);
 
 // Dense-transfer form (sweep_dense.hip): n matrices of n x n -- A_ll^-1 (l < b) of H_F, then
 // T_m (m = b+1 .. n) -- formed at setup from the block-Thomas factors; the apply is a GEMV chain.

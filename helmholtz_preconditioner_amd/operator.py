@@ -393,7 +393,8 @@ class Sweeping(DevicePreconditioner):
 
     FORMS = {"auto": -1, "thomas": 0, "dense": 1, "dense-launches": 2, "thomas-sequential": 3}
 
-    def __init__(self, A: DeviceOperator, reference: bool = False, form: str = "auto"):
+    def __init__(self, A: DeviceOperator, reference: bool = False, form: str = "auto",
+                 workgroups: int = 0):
         """``form``: ``"dense"`` forms the n matrices T_m (n^3 x 16 B of HBM) at setup and
         applies M as a chain of GEMVs; ``"thomas"`` keeps O(n^2 b^2) block-Thomas factors
         and solves, each forward / backward-sweep solve partitioned over 16 column chunks
@@ -401,18 +402,23 @@ class Sweeping(DevicePreconditioner):
         the unpartitioned solves (2n dependent steps each, least memory); ``"auto"`` picks
         dense when n <= 2048 and it fits, else ``"thomas"``; ``"dense-launches"`` is the dense
         form with one launch per GEMV instead of the persistent chain (n <= 1024).  Same
-        results to rounding (the two dense forms bit for bit)."""
+        results to rounding (the two dense forms bit for bit).  ``workgroups``: how many
+        workgroups share each partitioned solve (0: by n; ``hh_op_sweep_workgroups``)."""
         self.kind = _ffi.HH_PREC_SWEEP_REF if reference else _ffi.HH_PREC_SWEEP
         if form not in self.FORMS:
             raise ValueError(f"form must be one of {sorted(self.FORMS)}")
         self.form = form
+        self.requested_workgroups = int(workgroups)
         super().__init__(A)
 
     def configure(self):
         A = self.A
-        active = ctypes.c_int()
+        active, wgs = ctypes.c_int(), ctypes.c_int()
+        check(lib.hh_op_sweep_workgroups(A.handle, self.requested_workgroups, ctypes.byref(wgs)))
         check(lib.hh_op_sweep_mode(A.handle, self.FORMS[self.form], ctypes.byref(active)))
         super().configure()
         check(lib.hh_op_sweep_mode(A.handle, self.FORMS[self.form], ctypes.byref(active)))
+        check(lib.hh_op_sweep_workgroups(A.handle, self.requested_workgroups, ctypes.byref(wgs)))
         self.dense = active.value == 1
         self.partitioned = active.value == 2  # chunked block-Thomas solves
+        self.workgroups = wgs.value  # workgroups per partitioned solve (0: not partitioned)

@@ -289,8 +289,9 @@ int hh_op_sl_fusion(hh_op* op, int enable);
 /* Sweeping preconditioner form (speed / memory only; results agree to rounding):
  *   mode -1 (default) dense transfer matrices when n <= 2048 and the n^3 x 16 B fit in HBM,
  *           else as mode 0;  0 block-Thomas solves, the forward / backward sweeps' solves
- *           partitioned over 16 column chunks (chunk products: 2 x the factors' O(n^2 b^2)
- *           memory; dependent depth ~2 (n/16 + 16) steps per solve) when n >= 32 and they fit,
+ *           partitioned over 16 column chunks per workgroup and G workgroups (chunk products:
+ *           2 x the factors' O(n^2 b^2) memory; dependent depth ~2 (n/16G + 32 + G) steps per
+ *           solve; hh_op_sweep_workgroups) when n >= 32 and they fit,
  *           else sequential;  1 dense transfer matrices (error if they do not fit), their
  *           GEMV chain as ONE persistent cooperative launch when n <= 1024 (else one launch per
  *           GEMV);  2 dense, one launch per GEMV always (HH_SWEEP_CHAIN=0 does the same for
@@ -300,6 +301,14 @@ int hh_op_sl_fusion(hh_op* op, int enable);
  * active (optional) receives 1 when the dense form is in use, 2 for partitioned solves,
  * 0 for sequential ones. */
 int hh_op_sweep_mode(hh_op* op, int mode, int* active);
+/* Workgroups sharing each partitioned block-Thomas solve (speed only; results agree to
+ * rounding): 0 (default) by n (about 4 columns per chunk, at most 32 -- 12 for PML widths
+ * b > 12 -- and the CU count), else that many, clamped to the same limits and to 2 columns
+ * per chunk.  G > 1 runs each forward / backward sweep as one cooperative launch of G
+ * workgroups that exchange the solves' chunk carries through device memory.  Applies at the
+ * next sweeping setup, or at once if the operator is already factored.  active (optional)
+ * receives the workgroup count in use, 0 when the solves are not partitioned. */
+int hh_op_sweep_workgroups(hh_op* op, int workgroups, int* active);
 /* Process-wide tuning of the Krylov streaming kernels (multidot / update): non-temporal
  * basis loads on (1) / off (0) / by vector length (-1, default: on above 2^21 rank-local
  * unknowns) and the streaming grid size (0 = by vector length: 512 blocks up to 2^21

@@ -197,20 +197,27 @@ def test_sweep_thomas_as_is_matches_reference_golden(ctx, name, form):
     assert relerr(M @ rand_complex(n * n, 3), z["u_x"]) < 1e-10
 
 
-@pytest.mark.parametrize("n,b,kind", [(32, 5, "c1"), (33, 12, "c2"), (61, 5, "c1"),
-                                      (96, 12, "c1"), (130, 8, "const"), (200, 16, "c2"),
-                                      (257, 3, "c1")])
-def test_sweep_partitioned_vs_sequential_and_oracle(ctx, n, b, kind):
-    """ragged chunks (n not a multiple of 8), every block size B = 4, 8, 12, 16, both sweeps"""
+@pytest.mark.parametrize("n,b,kind,wgs", [(32, 5, "c1", 0), (33, 12, "c2", 0), (61, 5, "c1", 0),
+                                          (96, 12, "c1", 3), (130, 8, "const", 4),
+                                          (200, 16, "c2", 0), (257, 3, "c1", 0),
+                                          (257, 3, "c1", 8), (331, 12, "c2", 0),
+                                          (331, 12, "c2", 2), (700, 12, "c1", 0),
+                                          (700, 16, "c1", 0)])
+def test_sweep_partitioned_vs_sequential_and_oracle(ctx, n, b, kind, wgs):
+    """ragged chunks (n not a multiple of 8), every block size B = 4, 8, 12, 16, both sweeps,
+    one workgroup and several (wgs 0: by n -- 700: 10 workgroups, every solve's carries cross
+    workgroups through the granule exchange)"""
     om, h, eta = O.problem_params(n, b, 5.0, 2.0)
     cm = medium(kind, n)
     A = H.build_A_matrix(b, 81.0, eta, om, h, n, cm, context=ctx)
     x = rand_complex(n * n, n + 3)
     st = O.SweepState(b, 81.0, eta, om, h, n, cm) if n <= 200 else None
+    want = min(wgs if wgs else n // 64, 32 if b <= 12 else 12, n // 32) or 1
     for reference in (False, True):
-        Mp = H.Sweeping(A, reference=reference, form="thomas")
+        Mp = H.Sweeping(A, reference=reference, form="thomas", workgroups=wgs)
         yp = Mp @ x
         assert Mp.partitioned and not Mp.dense
+        assert Mp.workgroups == max(want, 1)
         Ms = H.Sweeping(A, reference=reference, form="thomas-sequential")
         ys = Ms @ x
         assert not Ms.partitioned and not Ms.dense
@@ -247,3 +254,18 @@ def test_sweep_partitioned_large_linearity(ctx):
     mx, my, mxy = M @ x, M @ y, M @ (x + 2j * y)
     assert np.all(np.isfinite(mxy))
     assert relerr(mxy, mx + 2j * my) < 1e-10
+
+
+def test_sweep_partitioned_workgroups_agree_with_dense(ctx):
+    """n = 1023 (the dense form's largest persistent-chain size): the partitioned apply over
+    1, 4 and 15 (auto) workgroups agrees with the dense transfer form to rounding"""
+    n, b = 1023, 12
+    om, h, eta = O.problem_params(n, b, 128.0, 2.0)
+    A = H.build_A_matrix(b, 100.0, eta, om, h, n, O.init_c1_mat(.5, .5, n), context=ctx)
+    x = rand_complex(n * n, 11)
+    yd = H.Sweeping(A, form="dense") @ x
+    for wgs, want in ((1, 1), (4, 4), (0, 15)):
+        M = H.Sweeping(A, form="thomas", workgroups=wgs)
+        y = M @ x
+        assert M.partitioned and M.workgroups == want
+        assert relerr(y, yd) < 1e-10

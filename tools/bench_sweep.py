@@ -1,7 +1,7 @@
 """Sweeping preconditioner (row F1) timings on the device vs the reference's SuperLU path
 (oracle restatement of algo2_3 / algo2_4 on this host's CPU).
 usage: python tools/bench_sweep.py [--form dense|thomas|thomas-sequential|auto] [--maxiter K]
-                                   [n ...]
+                                   [--wgs G] [n ...]
 --maxiter 0 skips the GMRES solve (default 300; large n with the solve forms takes ~1 s/apply)
 
 Dense-form apply algorithmic bytes: every transfer matrix read once by the fused
@@ -19,12 +19,14 @@ import helmholtz_preconditioner_amd as H  # noqa: E402
 from helmholtz_preconditioner_amd import _ffi  # noqa: E402
 
 args = sys.argv[1:]
-form, maxiter = "auto", 300
+form, maxiter, wgs = "auto", 300, 0
 while args and args[0].startswith("--"):
     if args[0] == "--form":
         form = args[1]
     elif args[0] == "--maxiter":
         maxiter = int(args[1])
+    elif args[0] == "--wgs":
+        wgs = int(args[1])
     args = args[2:]
 ns = [int(v) for v in args] or [127, 255, 511, 1023]
 for n in ns:
@@ -34,7 +36,7 @@ for n in ns:
     A = H.build_A_matrix(b, C, eta, om, h, n, cm)
     A.ctx.synchronize()
     t0 = time.perf_counter()
-    Msw = H.Sweeping(A, form=form)
+    Msw = H.Sweeping(A, form=form, workgroups=wgs)
     Msw.configure()
     A.ctx.synchronize()
     t_setup = time.perf_counter() - t0
@@ -57,7 +59,8 @@ for n in ns:
     if Msw.dense:
         alg = (2 * (n - b) + b + 1) * n * n * 16
         gbs = f" ({alg / t_apply / 1e9:.0f} GB/s algorithmic, dense)"
-    kind = "dense" if Msw.dense else ("partitioned" if Msw.partitioned else "sequential")
+    kind = "dense" if Msw.dense else (f"partitioned, {Msw.workgroups} workgroups" if Msw.partitioned
+                                      else "sequential")
     line = (f"n={n} b={b} wn={wn} form={form} ({kind}): setup {t_setup*1e3:.1f} ms, apply {t_apply*1e3:.2f} ms{gbs}, "
             f"corrected-sweep GMRES {len(hist)} its info={info} in {t_solve:.3f} s")
     if n <= 255 and os.path.isdir(os.path.join(ROOT, "oracle")):
