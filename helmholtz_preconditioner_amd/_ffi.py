@@ -95,6 +95,7 @@ SIGNATURES = [
     ("hh_op_tune", c_int, [c_void_p, c_int, c_int, c_int]),
     ("hh_op_sweep_mode", c_int, [c_void_p, c_int, c_ip]),
     ("hh_op_sweep_workgroups", c_int, [c_void_p, c_int, c_ip]),
+    ("hh_op_sweep_profile", c_int, [c_void_p, c_int, c_dp, c_int]),
     ("hh_tune_krylov", c_int, [c_int, c_int]),
     ("hh_op_probe_stream", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_dp, c_ip]),
     ("hh_op_probe_stream_set", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int,

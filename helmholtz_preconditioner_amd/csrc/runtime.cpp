@@ -224,6 +224,7 @@ struct hh_op {
   double2* sw_Pw = nullptr;     // workgroup maps of the multi-workgroup partitioned solves
   unsigned long long* sw_gran = nullptr;  // their grid-exchange granules
   int sw_wgs = 0;               // requested workgroups per partitioned solve (0: by n)
+  unsigned long long* sw_prof = nullptr;  // diagnostic phase ticks (hh_op_sweep_profile)
   unsigned long long* sw_chain = nullptr;  // granules of the persistent apply chain, or null
   unsigned sw_seq = 0;                     // its launch sequence number
   double2* sw_u = nullptr;      // dense apply scratch (n^2)
@@ -1162,6 +1163,7 @@ static void op_release(hh_op* op) {
   dfree(op->sw_Pb);
   dfree(op->sw_Pw);
   dfree(op->sw_gran);
+  dfree(op->sw_prof);
   dfree(op->sw_y);
   dfree(op->sw_uF);
   dfree(op->sw_const);
@@ -1280,8 +1282,11 @@ static int sweep_part_wgs(hh_op* op) {
   int cus = 0;
   HIPC(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, op->ctx->device));
   int G = op->sw_wgs > 0 ? op->sw_wgs : n / (4 * kSweepChunks);
-  G = std::min({G, sweep_part_max_wgs(B), cus, n / (2 * kSweepChunks)});
-  return std::max(G, 1);
+  G = std::max(1, std::min({G, sweep_part_max_wgs(B), cus, n / (2 * kSweepChunks)}));
+  if (op->sw_wgs == 0)  // by n: the largest G <= that whose B-vectors fit in LDS, if any
+    for (int g2 = G; g2 >= 1; --g2)
+      if (sweep_part_ys_lds(B, g2, n)) return g2;
+  return G;
 }
 
 static void sweep_chunk_configure(hh_op* op) {
@@ -1297,7 +1302,7 @@ static void sweep_chunk_configure(hh_op* op) {
   if (op->sw_Pf && a.G == G) return;
   sweep_part_release(op);
   const size_t elems = (size_t)a.nsys * n * B * B;
-  const size_t welems = (size_t)a.nsys * G * 2 * B * B;
+  const size_t welems = (size_t)a.nsys * G * 2 * kSweepChunks * B * B;
   size_t free_b = 0, total_b = 0;
   HIPC(hipMemGetInfo(&free_b, &total_b));
   if ((2 * elems + welems) * sizeof(double2) > free_b / 10 * 8) return;  // sequential solves
@@ -1774,6 +1779,29 @@ HH_API int hh_op_sweep_mode(hh_op* op, int mode, int* active) {
     sweep_chunk_configure(op);
   }
   if (active) *active = op->sw_T ? 1 : (op->sweep.chunks > 0 ? 2 : 0);
+  GUARD_END
+}
+
+HH_API int hh_op_sweep_profile(hh_op* op, int enable, double* phase_us, int cap) {
+  GUARD_BEGIN
+  REQUIRE(op, "null op");
+  HIPC(hipSetDevice(op->ctx->device));
+  const size_t slots = (size_t)32 * kSweepProfSlots;
+  if (phase_us && op->sw_prof) {
+    std::vector<unsigned long long> t(slots);
+    HIPC(hipMemcpy(t.data(), op->sw_prof, slots * sizeof(unsigned long long),
+                   hipMemcpyDeviceToHost));
+    int khz = 100000;  // s_memrealtime: a constant 100 MHz clock on gfx9 (attribute in kHz)
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, op->ctx->device);
+    for (int q = 0; q < cap && q < (int)slots; ++q) phase_us[q] = t[q] * 1e3 / (khz > 0 ? khz : 100000);
+  }
+  if (enable && !op->sw_prof) op->sw_prof = dalloc<unsigned long long>(slots);
+  if (op->sw_prof) HIPC(hipMemset(op->sw_prof, 0, slots * sizeof(unsigned long long)));
+  if (!enable) {
+    dfree(op->sw_prof);
+    op->sw_prof = nullptr;
+  }
+  op->sweep.prof = op->sw_prof;
   GUARD_END
 }
 

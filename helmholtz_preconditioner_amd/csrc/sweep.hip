@@ -150,11 +150,11 @@ __global__ __launch_bounds__(kSW) void sweep_factor_kernel(const SweepArgs a) {
     }
     __syncthreads();
     if (row) {
-      double2* out = P + ((size_t)i * B + lane) * B;
+      double2* out = P + (size_t)i * B * B;
       sfor<0, B>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
         prev[k] = perm[lane][k];
-        out[k] = prev[k];
+        out[pidx<B>(lane, k)] = prev[k];
       });
     }
     Uprev = c.E;
@@ -227,7 +227,9 @@ __device__ __forceinline__ void bt_solve(const SweepArgs& a, int s, const SolveI
   const double2* rb = io.rhs + (size_t)(has_rhs ? j - io.rhs_first : 0) * io.rhs_ld;
   double2* ob = io.out + (size_t)(has_out ? j - io.out_first : 0) * io.out_ld;
   double2* dummy = ys + (size_t)(n + kMaxRing) * 16 + lane;
-  const double2* P = a.P + (size_t)s * n * PS + (size_t)jl * B + g * KG;
+  const double2* P = a.P + (size_t)s * n * PS;
+  int po[KG];  // this lane's entries (row jl, columns g KG + c) in the pidx order
+  sfor<0, KG>([&](auto cc) { po[decltype(cc)::value] = pidx<B>(jl, g * KG + decltype(cc)::value); });
   const double2 z = make_double2(0.0, 0.0);
   const double2 R2 = csel(row, a.tab_k[4 * jl], z);  // local-layer 1/s2: c1 = AW R2, c2 = AE R2
   const double2* AW = a.tab_i;
@@ -239,7 +241,7 @@ __device__ __forceinline__ void bt_solve(const SweepArgs& a, int s, const SolveI
   double2 Pf[D][KG], cf[D], rf[D], sf[SR ? D : 1];
   auto load_f = [&](auto qc, int i) {
     constexpr int q = decltype(qc)::value;
-    sfor<0, KG>([&](auto cc) { Pf[q][decltype(cc)::value] = P[(size_t)i * PS + decltype(cc)::value]; });
+    sfor<0, KG>([&](auto cc) { Pf[q][decltype(cc)::value] = P[(size_t)i * PS + po[decltype(cc)::value]]; });
     cf[q] = AW[i];
     rf[q] = rb[i];
     if constexpr (SR) sf[q] = R1[i];
@@ -282,7 +284,7 @@ __device__ __forceinline__ void bt_solve(const SweepArgs& a, int s, const SolveI
   double2 Pb[D][KG], cb[D], yb[D], obv[D], sb[SO ? D : 1];
   auto load_b = [&](auto qc, int i) {
     constexpr int q = decltype(qc)::value;
-    sfor<0, KG>([&](auto cc) { Pb[q][decltype(cc)::value] = P[(size_t)i * PS + decltype(cc)::value]; });
+    sfor<0, KG>([&](auto cc) { Pb[q][decltype(cc)::value] = P[(size_t)i * PS + po[decltype(cc)::value]]; });
     cb[q] = AE[i];
     yb[q] = ys[(size_t)i * 16 + jl];
     obv[q] = ob[i];
@@ -323,10 +325,10 @@ __device__ __forceinline__ void bt_solve(const SweepArgs& a, int s, const SolveI
 // one map per workgroup, Phi_f(g) = Psi_f[end_15] .. Psi_f[end_0] (Phi_b likewise), so a
 // carry crosses a workgroup in one B x B step.  A solve is then: every chunk's local
 // recurrence at once, a chain over the workgroup's 16 chunk boundaries, ONE exchange of the
-// workgroups' zero-carry end vectors, a chain over the other workgroups' maps, the chunk chain
-// again with the true carry, and a parallel fix-up of every column -- dependent depth
-// ~2 (n / K + 2 kSweepChunks + G) steps instead of 2 n.  Psi and Phi are operator data,
-// formed once at setup.
+// workgroups' zero-carry end vectors, a chain over the other workgroups' maps, one step per
+// chunk through the workgroup's prefix map, and a parallel fix-up of every column --
+// dependent depth ~2 (n / K + kSweepChunks + G) steps instead of 2 n.  Psi and the workgroup
+// maps are operator data, formed once at setup.
 __device__ __forceinline__ int chunk_lo(int n, int K, int k) { return n * k / K; }  // n K < 2^31
 
 __device__ __forceinline__ void wave_sync() {
@@ -362,7 +364,7 @@ __global__ __launch_bounds__(kSW) void sweep_chunk_setup_kernel(const SweepArgs 
       sfor<0, B>([&](auto mc) {
         constexpr int m = decltype(mc)::value;
         const double2 r2 = m < a.b ? a.tab_k[4 * m] : z;  // 0 on padding layers
-        prow[m] = cneg(cmul(P[((size_t)i * B + jl) * B + m], cmul(cc, r2)));
+        prow[m] = cneg(cmul(P[(size_t)i * PS + pidx<B>(jl, m)], cmul(cc, r2)));
       });
       double2 v[KG];
       sfor<0, KG>([&](auto c2) {
@@ -386,7 +388,7 @@ __global__ __launch_bounds__(kSW) void sweep_chunk_setup_kernel(const SweepArgs 
         sfor<0, KG>([&](auto c2) {
           constexpr int c = decltype(c2)::value;
           Q[q & 1][j][g * KG + c] = v[c];
-          out[((size_t)i * B + j) * B + g * KG + c] = v[c];
+          out[(size_t)i * PS + pidx<B>(j, g * KG + c)] = v[c];
         });
       }
       wave_sync();
@@ -394,9 +396,11 @@ __global__ __launch_bounds__(kSW) void sweep_chunk_setup_kernel(const SweepArgs 
   }
 }
 
-// Setup: the workgroup maps of one (system, workgroup) per wave (after the chunk products):
-// Phi_f(g) = Psi_f[end_15] .. Psi_f[end_0] and Phi_b(g) = Psi_b[lo_0] .. Psi_b[lo_15] over the
-// workgroup's kSweepChunks chunks (end_k / lo_k: the chunk's last / first column).
+// Setup: the workgroup maps of one (system, workgroup) per wave (after the chunk products),
+// with F_k = Psi_f[end_k], B_k = Psi_b[lo_k] the chunk maps (end_k / lo_k: the chunk's last /
+// first column): forward Pw[..][0][q] = F_q .. F_0 (the map from the workgroup's carry to the
+// end of chunk q), backward Pw[..][1][q] = B_{15-q} .. B_15 (from the carry past the workgroup
+// to the start of chunk 15 - q); [15] is the whole workgroup's map Phi.
 template <int B>
 __global__ __launch_bounds__(kSW) void sweep_wg_setup_kernel(const SweepArgs a) {
   constexpr int KG = B / kGroups;
@@ -410,14 +414,14 @@ __global__ __launch_bounds__(kSW) void sweep_wg_setup_kernel(const SweepArgs a) 
   const double2 z = make_double2(0.0, 0.0);
   for (int dir = 0; dir < 2; ++dir) {
     const double2* src = (dir == 0 ? a.Pf : a.Pb) + (size_t)s * n * PS;
-    double2* out = a.Pw + (((size_t)s * G + wg) * 2 + dir) * PS;
+    double2* out = a.Pw + (((size_t)s * G + wg) * 2 + dir) * kSweepChunks * PS;
     for (int q = 0; q < kSweepChunks; ++q) {  // forward: chunks in order; backward: from the last
       const int k = kSweepChunks * wg + (dir == 0 ? q : kSweepChunks - 1 - q);
       const int col = dir == 0 ? chunk_lo(n, K, k + 1) - 1 : chunk_lo(n, K, k);
       double2 prow[B];
       sfor<0, B>([&](auto mc) {
         constexpr int m = decltype(mc)::value;
-        prow[m] = src[((size_t)col * B + jl) * B + m];
+        prow[m] = src[(size_t)col * PS + pidx<B>(jl, m)];
       });
       double2 v[KG];
       sfor<0, KG>([&](auto c2) {
@@ -441,7 +445,7 @@ __global__ __launch_bounds__(kSW) void sweep_wg_setup_kernel(const SweepArgs a) 
         sfor<0, KG>([&](auto c2) {
           constexpr int c = decltype(c2)::value;
           Q[q & 1][j][g * KG + c] = v[c];
-          if (q == kSweepChunks - 1) out[(size_t)j * B + g * KG + c] = v[c];
+          out[(size_t)q * PS + pidx<B>(j, g * KG + c)] = v[c];
         });
       }
       wave_sync();
@@ -457,10 +461,18 @@ constexpr int kPartThreads = kSweepChunks / 2 * kSW;      // 8 waves, two chunks
 constexpr unsigned kPartSpin = 1u << 20;                   // ~1 s of polling per wait
 // dynamic LDS of a partitioned solve: the chain maps [kSweepChunks + G - 1][B B], then the
 // other workgroups' published vectors [G][16]
+// the most columns one workgroup owns (n K < 2^31: chunk_lo exact) + 1
+__host__ __device__ inline int part_ys_cols(int n, int G) { return (n + G - 1) / G + 1; }
+// double2 of the fixed part (tl, bf, bb, gv, yvl of bt_solve_chunked)
+constexpr int kPartFixedLds = kSweepChunks * 2 * 16 + 2 * (kSweepChunks + 2) * 16 + 2 * 16 +
+                              kSweepChunks * 16;
 template <int B>
-size_t part_lds_bytes(int G) {
-  return ((size_t)(kSweepChunks + G - 1) * B * B + (size_t)G * 16) * sizeof(double2);
+size_t part_lds_bytes(int G, int n, bool ly) {
+  return ((size_t)kPartFixedLds + (size_t)(kSweepChunks + G - 1) * B * B + kSW + (size_t)G * 16 +
+          (ly ? (size_t)part_ys_cols(n, G) * B + kSW : 0)) * sizeof(double2);
 }
+constexpr size_t kPartStaticLds = 256;  // (anything the compiler adds beside the dynamic block)
+constexpr size_t kPartLdsBudget = 160 * 1024;
 
 // base[byte offset]: a scalar base plus a 32-bit lane offset in bytes is the form the
 // global_load/store saddr addressing takes (no 64-bit address pair per lane)
@@ -510,8 +522,10 @@ __device__ __forceinline__ void st_gran4(unsigned long long* p, unsigned tag, do
 //      chunk boundaries from a zero workgroup carry, y_end_k = yL_end_k + Psi_f y_end_{k-1},
 //      the last one published as granules; waves 1..7 meanwhile poll the earlier workgroups'
 //   3. wave 0: the workgroup's carry y_in = chain of the earlier workgroups' vectors through
-//      their Phi_f, then the chunk boundaries again from y_in (G = 1: step 2 alone)
-//   4. fix-up (rows independent): y_i = yL_i + Psi_f[i] y_{lo-1}; then backward, chunk-local:
+//      their Phi_f (G = 1: step 2 alone)
+//   4. every half: its chunk's carry y_{lo-1} = the zero-carry chain's value + the workgroup's
+//      prefix map (Pw) applied to y_in; fix-up (rows independent): y_i = yL_i + Psi_f[i] y_{lo-1};
+//      then backward, chunk-local:
 //      xL_i = y_i - P_i U_i xL_{i+1} (a wave reads back only its own rows); 2-3 backward; then
 //   5. fix-up + output (rows independent, prefetched like 1 / 4): x_i = xL_i + Psi_b[i] x_{hi}
 // (chunk 0 in 4 and chunk 15 in 5 multiply their Psi rows by the workgroup carry, zero for the
@@ -519,26 +533,37 @@ __device__ __forceinline__ void st_gran4(unsigned long long* p, unsigned tag, do
 // ring slot of KG = 6 double2 is 24 VGPRs at B = 12, so no phase keeps two matrix rings.  ok:
 // false once a grid wait of this workgroup timed out (no further waits; garbage output and
 // a.timeout set for the host).
-template <int B, bool SR, bool SO>
+template <int B, bool SR, bool SO, bool LY>
 __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int round,
-                                                 const SolveIO& io, double2* ys, bool& ok) {
+                                                 const SolveIO& io, double2* ys, bool& ok,
+                                                 unsigned long long (&tk)[kSweepProfSlots]) {
   constexpr int KG = B / 2;
   constexpr int D = chunk_ring<B>();
   constexpr int KL = kSweepChunks;
   constexpr int PS = B * B;
   constexpr unsigned PSB = (unsigned)PS * 16u;  // bytes of one B x B matrix
   constexpr int NQ = 4 * B;                     // granules of one published vector
+  // all LDS is carved from the dynamic block (one copy however many instantiations a kernel
+  // calls): the per-chunk step vectors tl, the chunk boundaries bf / bb ([KL]: workgroup carry,
+  // [KL + 1]: zeros), the grid chain's ping-pong gv, the chunk-end (forward) / chunk-start
+  // (backward) vectors yvl, then the chain maps, the grid vectors and (LY) the B-vectors
   extern __shared__ double2 part_lds[];
-  __shared__ double2 tl[KL][2][16];
-  __shared__ double2 bf[KL + 2][16], bb[KL + 2][16];  // [KL]: workgroup carry, [KL + 1]: zeros
-  __shared__ double2 gv[2][16];
-  __shared__ double2 yvl[KL][16];  // the chunk-end (forward) / chunk-start (backward) vectors
+  auto tl = reinterpret_cast<double2 (*)[2][16]>(part_lds);
+  auto bf = reinterpret_cast<double2 (*)[16]>(part_lds + KL * 2 * 16);
+  auto bb = bf + (KL + 2);
+  auto gv = bb + (KL + 2);
+  auto yvl = gv + 2;
   const int tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, h = lane >> 5, g = (lane >> 4) & 1, j = lane & 15;
   const int n = a.n, G = a.G, wg = blockIdx.x, K = KL * G;
-  double2* mats = part_lds;                                 // [KL + G - 1][PS]
-  double2* gin = part_lds + (size_t)(KL + G - 1) * PS;      // [G][16]
+  double2* mats = part_lds + kPartFixedLds;                 // [KL + G - 1][PS]
+  double2* gin = mats + (size_t)(KL + G - 1) * PS + kSW;     // [G][16] (after the DMA slack)
+  // LY: the workgroup's B-vectors (y, then x) in LDS, [column - c0w][B] + a junk slot per
+  // lane: no global store in the dependent loops (a wait for a ring load would also wait for
+  // every older store, and a store takes ~1 us to retire)
+  double2* ysl = gin + (size_t)G * 16;
+  const int c0w = chunk_lo(n, K, KL * wg);
   const int cl = 2 * w + h;  // this half's local chunk
   const int c = KL * wg + cl;
   const int lo = chunk_lo(n, K, c), hi = chunk_lo(n, K, c + 1), len = hi - lo;
@@ -554,7 +579,8 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
   const unsigned roff = has_rhs ? (unsigned)((j - io.rhs_first) * io.rhs_ld) * 16u : 0u;
   const unsigned ooff =
       (row && j >= io.out_first) ? (unsigned)((j - io.out_first) * io.out_ld) * 16u : 0u;
-  const unsigned lofs = (unsigned)(jl * B + g * KG) * 16u;  // row jl, this lane's columns
+  const unsigned lofs = (unsigned)pidx<B>(jl, g * KG) * 16u;  // row jl, this lane's columns
+  constexpr unsigned QS = 2u * B * 16u;  // byte step between a lane's consecutive entries
   const unsigned dofs =
       ((unsigned)(n * 16) + (unsigned)wg * kPartThreads + (unsigned)tid) * 16u;  // dummy slot
   const size_t sbase = (size_t)s * n * PS;
@@ -569,11 +595,15 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
   const bool ystore = g == 0 && j < B;
   auto ld_row = [&](double2 (&m)[KG], const double2* base, int i) {
     const unsigned o = (unsigned)i * PSB + lofs;
-    sfor<0, KG>([&](auto cc) { m[decltype(cc)::value] = at(base, o + 16u * decltype(cc)::value); });
+    sfor<0, KG>([&](auto cc) { m[decltype(cc)::value] = at(base, o + QS * decltype(cc)::value); });
   };
-  auto yget = [&](int i) { return at(ys, ((unsigned)i * 16u + (unsigned)jl) * 16u); };
+  auto yget = [&](int i) {
+    if constexpr (LY) return ysl[(i - c0w) * B + jl];
+    else return at(ys, ((unsigned)i * 16u + (unsigned)jl) * 16u);
+  };
   auto yput = [&](bool ok_, int i, double2 v) {
-    at(ys, ok_ ? ((unsigned)i * 16u + (unsigned)j) * 16u : dofs) = v;
+    if constexpr (LY) ysl[ok_ ? (i - c0w) * B + j : part_ys_cols(n, G) * B + lane] = v;
+    else at(ys, ok_ ? ((unsigned)i * 16u + (unsigned)j) * 16u : dofs) = v;
   };
   // this lane's KG entries against entries [g KG, (g+1) KG) of an LDS 16-vector, summed over
   // the half's two lane groups
@@ -585,41 +615,30 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
     });
     return make_double2(sum2(acc.x), sum2(acc.y));
   };
-  // the same with row jl of staged map mi (LDS)
-  auto rowdot_m = [&](int mi, const double2* vec) {
-    const double2* mr = mats + mi * PS + jl * B + g * KG;
-    double2 acc = z;
-    sfor<0, KG>([&](auto cc) {
-      constexpr int q = decltype(cc)::value;
-      acc = cfma(mr[q], vec[g * KG + q], acc);
-    });
-    return make_double2(sum2(acc.x), sum2(acc.y));
-  };
   // the chain maps of direction dir into LDS: map k < KL is local chunk k's end map (forward:
   // Psi_f at its last column; backward: Psi_b at its first), map KL + q the q-th other
-  // workgroup's Phi (forward: workgroups 0 .. wg-1; backward: wg+1 .. G-1)
+  // workgroup's Phi (forward: workgroups 0 .. wg-1; backward: wg+1 .. G-1).  By LDS DMA
+  // (global_load_lds: no registers, lane-linear 1 KB per wave instruction, per-lane sources),
+  // issued at the start of a chunk-local phase so its latency overlaps that phase's first ring
+  // loads; the barrier before the maps are read waits for it.  (The last instruction may write
+  // up to 63 entries past the maps: the region has that slack.)
   auto stage = [&](int dir) {
     const int tot = (KL + (dir == 0 ? wg : G - 1 - wg)) * PS;
     const double2* cp = dir == 0 ? Pf : Pb;
-    for (int e0 = tid; e0 < tot; e0 += 4 * kPartThreads) {
-      double2 v[4];
-      sfor<0, 4>([&](auto uc) {
-        const int e = min(e0 + (int)decltype(uc)::value * kPartThreads, tot - 1);
-        const int mi = e / PS, off = e - mi * PS;
-        const double2* src;
-        if (mi < KL) {
-          const int k = KL * wg + mi;
-          src = cp + (size_t)(dir == 0 ? chunk_lo(n, K, k + 1) - 1 : chunk_lo(n, K, k)) * PS + off;
-        } else {
-          const int og = dir == 0 ? mi - KL : wg + 1 + (mi - KL);
-          src = a.Pw + (((size_t)s * G + og) * 2 + dir) * PS + off;
-        }
-        v[decltype(uc)::value] = *src;
-      });
-      sfor<0, 4>([&](auto uc) {
-        const int e = e0 + (int)decltype(uc)::value * kPartThreads;
-        if (e < tot) mats[e] = v[decltype(uc)::value];
-      });
+    for (int e0 = w * kSW; e0 < tot; e0 += kPartThreads) {
+      const int e = min(e0 + lane, tot - 1);
+      const int mi = e / PS, off = e - mi * PS;
+      const double2* src;
+      if (mi < KL) {
+        const int k = KL * wg + mi;
+        src = cp + (size_t)(dir == 0 ? chunk_lo(n, K, k + 1) - 1 : chunk_lo(n, K, k)) * PS + off;
+      } else {
+        const int og = dir == 0 ? mi - KL : wg + 1 + (mi - KL);
+        src = a.Pw + ((((size_t)s * G + og) * 2 + dir) * KL + KL - 1) * PS + off;
+      }
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(mats + e0), 16,
+                                       0, 0);
     }
   };
   // waves 1..7: wait for the vectors the grid chain needs (forward: workgroups 0 .. wg-1,
@@ -668,14 +687,23 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
   };
   // wave 0: chain over the local chunk boundaries, bv[k] = yv[k] + map_k bv[prev], prev = the
   // neighbour chunk (forward k - 1, backward k + 1) or `start` for the first step
+  // (a staged map's row entries into registers: issued a step ahead of their use, so a step
+  // waits only on the vector it depends on)
+  auto ldm = [&](double2 (&m)[KG], int mi) {
+    const double2* mr = mats + mi * PS + pidx<B>(jl, g * KG);
+    sfor<0, KG>([&](auto cc) { m[decltype(cc)::value] = mr[decltype(cc)::value * 2 * B]; });
+  };
   auto chain = [&](auto fwdc, double2 (*bv)[16], int start) {
     constexpr bool fwd = decltype(fwdc)::value;
     double2 v = z;
+    double2 mq[2][KG];
+    ldm(mq[0], fwd ? 0 : KL - 1);
     sfor<0, KL>([&](auto qc) {
       constexpr int q = decltype(qc)::value;
       constexpr int k = fwd ? q : KL - 1 - q;
+      if constexpr (q + 1 < KL) ldm(mq[(q + 1) & 1], fwd ? k + 1 : k - 1);
       const int prev = q == 0 ? start : (fwd ? k - 1 : k + 1);
-      v = cadd(yvl[k][jl], rowdot_m(k, &bv[prev][0]));
+      v = cadd(yvl[k][jl], rowdot(mq[q & 1], &bv[prev][0]));
       if (lane < 16) bv[k][lane] = v;
       wave_sync();
     });
@@ -688,33 +716,49 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
     if (lane < 16) gv[0][lane] = z;
     wave_sync();
     int cur = 0;
+    double2 m[KG];
+    ldm(m, KL + (dir == 0 ? 0 : max(cnt - 1, 0)));
     for (int q = 0; q < cnt; ++q) {
       const int gi = dir == 0 ? q : cnt - 1 - q;
-      const double2 v = cadd(gin[gi * 16 + jl], rowdot_m(KL + gi, &gv[cur][0]));
+      double2 mn[KG];  // the next step's map (clamped: valid LDS, unused on the last step)
+      ldm(mn, KL + (dir == 0 ? min(q + 1, cnt - 1) : max(cnt - 2 - q, 0)));
+      const double2 v = cadd(gin[gi * 16 + jl], rowdot(m, &gv[cur][0]));
       if (lane < 16) gv[cur ^ 1][lane] = v;
       wave_sync();
       cur ^= 1;
+      sfor<0, KG>([&](auto cc) { m[decltype(cc)::value] = mn[decltype(cc)::value]; });
     }
     if (lane < 16) bv[KL][lane] = gv[cur][lane];
     wave_sync();
+  };
+  // phase timing (diagnostic): thread 0's wall clock at phase ends, into tk[slot]
+  const bool prof = a.prof != nullptr && tid == 0;
+  unsigned long long tmark = prof ? wall_clock64() : 0;
+  auto mark = [&](int slot) {
+    if (prof) {
+      const unsigned long long now = wall_clock64();
+      tk[slot] += now - tmark;
+      tmark = now;
+    }
   };
   // steps 2-3 of one direction (after the chunk-local pass and its barrier)
   auto boundaries = [&](auto dirc, double2 (*bv)[16]) {
     constexpr int dir = decltype(dirc)::value;
     constexpr bool fwd = dir == 0;
     const auto fwdc = std::integral_constant<bool, fwd>{};
-    stage(dir);
     if (tid < KL * 16) {  // (rows j >= B: copies of row B - 1, never used)
       const int k = tid >> 4;
-      yvl[k][tid & 15] = at(ys, ((unsigned)(fwd ? chunk_lo(n, K, KL * wg + k + 1) - 1
-                                                : chunk_lo(n, K, KL * wg + k)) * 16u +
-                                 (unsigned)min(tid & 15, B - 1)) * 16u);
+      const int col = fwd ? chunk_lo(n, K, KL * wg + k + 1) - 1 : chunk_lo(n, K, KL * wg + k);
+      const int row = min(tid & 15, B - 1);
+      if constexpr (LY) yvl[k][tid & 15] = ysl[(col - c0w) * B + row];
+      else yvl[k][tid & 15] = at(ys, ((unsigned)col * 16u + (unsigned)row) * 16u);
     }
     if (tid < 16) {
       bv[KL][tid] = z;
       bv[KL + 1][tid] = z;
     }
     __syncthreads();
+    mark(fwd ? 1 : 5);  // chunk-end vectors + barrier (the maps' DMA already waited for)
     if (G == 1) {
       if (w == 0) chain(fwdc, bv, KL + 1);
     } else {
@@ -729,15 +773,35 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
         poll(dir);
       }
       ok = __syncthreads_and(ok);
-      if (w == 0 && cnt > 0) {
-        gchain(bv, dir);
-        chain(fwdc, bv, KL);
-      }
+      mark(fwd ? 2 : 6);  // zero-carry chain + publish | polls
+      if (w == 0 && cnt > 0) gchain(bv, dir);
     }
     __syncthreads();
+    mark(fwd ? 3 : 7);  // grid chain
+  };
+  // the true carry into this half's chunk (forward: y at the end of chunk cl - 1; backward: x
+  // at the start of chunk cl + 1) -- the zero-carry chain's value plus the workgroup carry
+  // bv[KL] through the workgroup's prefix / suffix map, Pw[s][wg][dir][idx]: one B x B step per
+  // chunk instead of the chain again.  Chunk 0 (forward) / 15 (backward) takes bv[KL] itself.
+  // Returns the LDS vector to use (tl[cl][0] when it had to be formed).
+  auto carry_in = [&](auto dirc, double2 (*bv)[16]) -> const double2* {
+    constexpr int dir = decltype(dirc)::value;
+    const bool edge = dir == 0 ? cl == 0 : cl == KL - 1;  // (per half)
+    const int nb = dir == 0 ? cl - 1 : cl + 1;            // neighbour chunk
+    const bool has_in = dir == 0 ? wg > 0 : wg < G - 1;   // (block-uniform) nonzero bv[KL]
+    if (!has_in) return &bv[edge ? KL : nb][0];
+    const int idx = dir == 0 ? max(cl - 1, 0) : max(KL - 2 - cl, 0);  // (edge: unused, clamped)
+    double2 m[KG];
+    ld_row(m, a.Pw + (((size_t)s * G + wg) * 2 + dir) * KL * PS, idx);
+    const double2 v = cadd(bv[edge ? KL + 1 : nb][jl], rowdot(m, &bv[KL][0]));
+    if (g == 0) tl[cl][0][j] = csel(edge, bv[KL][jl], v);
+    wave_sync();
+    __builtin_amdgcn_sched_barrier(0);  // (keep the next ring's loads out of this step's span)
+    return &tl[cl][0][0];
   };
 
-  // ---- 1. forward, chunk-local ----
+  // ---- 1. forward, chunk-local (the forward chain maps on their way to LDS meanwhile) ----
+  stage(0);
   {
     double2 Pq[D][KG], cq[D], rq[D], sq[SR ? D : 1];
     auto ld = [&](auto qc, int q) {
@@ -766,6 +830,7 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
     }
   }
   __syncthreads();
+  mark(0);  // chunk-local forward
   // ---- 2-3. forward boundaries ----
   boundaries(std::integral_constant<int, 0>{}, bf);
   // ---- 4. forward fix-up (rows independent): y_i = yL_i + Psi_f[i] y_{lo-1} ----
@@ -777,8 +842,9 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
       ld_row(mq[r], Pf, i);
       yq[r] = yget(i);
     };
+    const double2* carry = carry_in(std::integral_constant<int, 0>{}, bf);
+    stage(1);  // the backward chain maps, overlapping this phase
     sfor<0, D>([&](auto qc) { ld(qc, decltype(qc)::value); });
-    const double2* carry = &bf[cl > 0 ? cl - 1 : KL][0];
     for (int q0 = 0; q0 < lenw; q0 += D) {
       sfor<0, D>([&](auto qc) {
         constexpr int r = decltype(qc)::value;
@@ -815,6 +881,7 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
     }
   }
   __syncthreads();
+  mark(4);  // forward fix-up + chunk-local backward
   // ---- 2-3. backward boundaries ----
   boundaries(std::integral_constant<int, 1>{}, bb);
   // ---- 5. fix-up + output ----
@@ -828,8 +895,8 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
       oq[r] = at(io.out, (unsigned)i * 16u + ooff);
       if constexpr (SO) sq[r] = R1[i];
     };
+    const double2* carry = carry_in(std::integral_constant<int, 1>{}, bb);
     sfor<0, D>([&](auto qc) { ld(qc, decltype(qc)::value); });
-    const double2* carry = &bb[cl < KL - 1 ? cl + 1 : KL][0];
     for (int q0 = 0; q0 < lenw; q0 += D) {
       sfor<0, D>([&](auto qc) {
         constexpr int r = decltype(qc)::value;
@@ -844,6 +911,7 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
     }
   }
   __syncthreads();
+  mark(8);  // fix-up + output
 }
 
 __device__ __forceinline__ SolveIO solve_io(const double2* rhs, int rhs_first, double2 rmul,
@@ -864,13 +932,23 @@ __device__ __forceinline__ SolveIO solve_io(const double2* rhs, int rhs_first, d
 
 // the sequential sweeps' solves: one wave walking the columns, or (CH) the partitioned solve
 // of a.G workgroups of kSweepChunks / 2 waves (round: the solve's index in the launch)
-template <int B, bool SR, bool SO, bool CH>
+template <int B, bool SR, bool SO, bool CH, bool LY>
 __device__ __forceinline__ void solve(const SweepArgs& a, int s, int round, const SolveIO& io,
-                                      double2* ys, bool& ok) {
+                                      double2* ys, bool& ok,
+                                      unsigned long long (&tk)[kSweepProfSlots]) {
   if constexpr (CH)
-    bt_solve_chunked<B, SR, SO>(a, s, round, io, ys, ok);
+    bt_solve_chunked<B, SR, SO, LY>(a, s, round, io, ys, ok, tk);
   else
     bt_solve<B, SR, SO>(a, s, io, ys);
+}
+
+// diagnostic phase ticks of a partitioned launch: thread 0 of each workgroup adds its sums
+template <bool CH>
+__device__ __forceinline__ void prof_flush(const SweepArgs& a, const unsigned long long (&tk)[kSweepProfSlots]) {
+  if constexpr (CH) {
+    if (a.prof != nullptr && threadIdx.x == 0)
+      for (int q = 0; q < 9; ++q) a.prof[(size_t)blockIdx.x * kSweepProfSlots + q] += tk[q];
+  }
 }
 
 // the columns a workgroup of a partitioned launch owns (all n for the sequential one)
@@ -889,7 +967,7 @@ __device__ __forceinline__ void own_columns(const SweepArgs& a, int& c0, int& c1
 // forward sweep (code.py:363-370): TFuF = HF^-1 u[0:b] -> uF; u[b] -= S_b * TFuF[b-1];
 // for m = b+1..n-1: u[m] -= S_m * T_m u[m-1]  (S_m = BS_m R1[i], folded into the solve).
 // Partitioned: a workgroup reads and writes only its own columns of u and uF between solves.
-template <int B, bool CH>
+template <int B, bool CH, bool LY = false>
 __global__ __launch_bounds__(CH ? kPartThreads : kSW) void sweep_forward_kernel(
     const SweepArgs a, double2* u, double2* uF) {
   if (a.stop && *a.stop) return;
@@ -898,7 +976,8 @@ __global__ __launch_bounds__(CH ? kPartThreads : kSW) void sweep_forward_kernel(
   double2* ys = a.yscr;
   bool ok = true;
   int round = 0;
-  solve<B, false, false, CH>(a, 0, round++, solve_io(u, 0, one, uF, 0, 0.0, one, n), ys, ok);
+  unsigned long long tk[kSweepProfSlots] = {};
+  solve<B, false, false, CH, LY>(a, 0, round++, solve_io(u, 0, one, uF, 0, 0.0, one, n), ys, ok, tk);
   const double2* R1 = a.tab_i + 2 * n;
   int c0, c1;
   own_columns<CH>(a, c0, c1);
@@ -910,11 +989,12 @@ __global__ __launch_bounds__(CH ? kPartThreads : kSW) void sweep_forward_kernel(
   __syncthreads();
   for (int m = b + 1; m < n; ++m) {  // system s = m - b covers layers m-b .. m-1
     const double2 BS = a.tab_glob[4 * m + 1];
-    solve<B, false, true, CH>(a, m - b, round++,
+    solve<B, false, true, CH, LY>(a, m - b, round++,
                               solve_io(u + (size_t)(m - 1) * n, b - 1, one, u + (size_t)m * n,
                                        b - 1, 1.0, cneg(BS), n),
-                              ys, ok);
+                              ys, ok, tk);
   }
+  prof_flush<CH>(a, tk);
 }
 
 // middle sweep (code.py:372-375): for m = b+1..n: u[m-1] = T_m u[m-1] (corrected) or
@@ -937,7 +1017,7 @@ __global__ __launch_bounds__(kSW) void sweep_middle_kernel(const SweepArgs a, do
 // backward sweep (code.py:376-380): for m = n-1..b+1: u[m-1] -= T_m (N_{m-1} u[m]);
 // F correction (code.py:381-384): uF -= HF^-1 [0 .. 0, N_{b-1} u[b]]; u[0:b] = uF.
 // N_{m-1} = BN_{m-1} R1[i] is folded into the solve's right-hand-side load.
-template <int B, bool CH>
+template <int B, bool CH, bool LY = false>
 __global__ __launch_bounds__(CH ? kPartThreads : kSW) void sweep_backward_kernel(
     const SweepArgs a, double2* u, double2* uF) {
   if (a.stop && *a.stop) return;
@@ -946,19 +1026,21 @@ __global__ __launch_bounds__(CH ? kPartThreads : kSW) void sweep_backward_kernel
   const double2 mone = make_double2(-1.0, 0.0);
   bool ok = true;
   int round = 0;
+  unsigned long long tk[kSweepProfSlots] = {};
   for (int m = n - 1; m >= b + 1; --m) {
     const double2 BN = a.tab_glob[4 * (m - 1) + 2];  // c4 of global layer m-1 (code.py:131-140)
-    solve<B, true, false, CH>(a, m - b, round++,
+    solve<B, true, false, CH, LY>(a, m - b, round++,
                               solve_io(u + (size_t)m * n, b - 1, BN, u + (size_t)(m - 1) * n,
                                        b - 1, 1.0, mone, n),
-                              ys, ok);
+                              ys, ok, tk);
   }
   // H_F is block diagonal: only its last layer sees the (last-layer-only) right-hand side
   const double2 BN = a.tab_glob[4 * (b - 1) + 2];
-  solve<B, true, false, CH>(a, 0, round++,
+  solve<B, true, false, CH, LY>(a, 0, round++,
                             solve_io(u + (size_t)b * n, b - 1, BN, uF + (size_t)(b - 1) * n, b - 1,
                                      1.0, mone, n),
-                            ys, ok);
+                            ys, ok, tk);
+  prof_flush<CH>(a, tk);
   int c0, c1;
   own_columns<CH>(a, c0, c1);
   for (int l = 0; l < b; ++l)
@@ -969,8 +1051,9 @@ __global__ __launch_bounds__(CH ? kPartThreads : kSW) void sweep_backward_kernel
 // a partitioned sweep: G workgroups of kPartThreads, all co-resident (a cooperative launch
 // when G > 1, so a grid that cannot be placed fails at launch instead of waiting forever)
 template <int B>
-void launch_part(const void* fn, const SweepArgs& a, double2* u, double2* uF, hipStream_t st) {
-  const size_t lds = part_lds_bytes<B>(a.G);
+void launch_part(const void* fn, const SweepArgs& a, double2* u, double2* uF, hipStream_t st,
+                 bool ly) {
+  const size_t lds = part_lds_bytes<B>(a.G, a.n, ly);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e == hipSuccess) {
     SweepArgs arg = a;
@@ -987,6 +1070,12 @@ void launch_part(const void* fn, const SweepArgs& a, double2* u, double2* uF, hi
   }
 }
 
+// the B-vectors of a partitioned solve in LDS when they fit beside the chain maps
+template <int B>
+bool part_ys_lds(int G, int n) {
+  return part_lds_bytes<B>(G, n, true) + kPartStaticLds <= kPartLdsBudget;
+}
+
 template <int B>
 void launch_all(const SweepArgs& a, int what, double2* u, double2* uF, int asis, hipStream_t st) {
   switch (what) {
@@ -994,8 +1083,12 @@ void launch_all(const SweepArgs& a, int what, double2* u, double2* uF, int asis,
       hipLaunchKernelGGL((sweep_factor_kernel<B>), dim3(a.nsys), dim3(kSW), 0, st, a);
       break;
     case 1:
-      if (a.chunks > 0)
-        launch_part<B>(reinterpret_cast<const void*>(&sweep_forward_kernel<B, true>), a, u, uF, st);
+      if (a.chunks > 0 && part_ys_lds<B>(a.G, a.n))
+        launch_part<B>(reinterpret_cast<const void*>(&sweep_forward_kernel<B, true, true>), a, u,
+                       uF, st, true);
+      else if (a.chunks > 0)
+        launch_part<B>(reinterpret_cast<const void*>(&sweep_forward_kernel<B, true, false>), a, u,
+                       uF, st, false);
       else
         hipLaunchKernelGGL((sweep_forward_kernel<B, false>), dim3(1), dim3(kSW), 0, st, a, u, uF);
       break;
@@ -1004,8 +1097,12 @@ void launch_all(const SweepArgs& a, int what, double2* u, double2* uF, int asis,
                          asis);
       break;
     case 3:
-      if (a.chunks > 0)
-        launch_part<B>(reinterpret_cast<const void*>(&sweep_backward_kernel<B, true>), a, u, uF, st);
+      if (a.chunks > 0 && part_ys_lds<B>(a.G, a.n))
+        launch_part<B>(reinterpret_cast<const void*>(&sweep_backward_kernel<B, true, true>), a, u,
+                       uF, st, true);
+      else if (a.chunks > 0)
+        launch_part<B>(reinterpret_cast<const void*>(&sweep_backward_kernel<B, true, false>), a, u,
+                       uF, st, false);
       else
         hipLaunchKernelGGL((sweep_backward_kernel<B, false>), dim3(1), dim3(kSW), 0, st, a, u, uF);
       break;
@@ -1026,6 +1123,10 @@ size_t sweep_chunk_scratch(int n) { return (size_t)n * 16 + (size_t)32 * kPartTh
 int sweep_part_max_wgs(int B) {
   return B == 4 ? part_max_wgs<4>() : B == 8 ? part_max_wgs<8>() : B == 12 ? part_max_wgs<12>()
                                                                           : part_max_wgs<16>();
+}
+bool sweep_part_ys_lds(int B, int G, int n) {
+  return B == 4 ? part_ys_lds<4>(G, n) : B == 8 ? part_ys_lds<8>(G, n)
+       : B == 12 ? part_ys_lds<12>(G, n) : part_ys_lds<16>(G, n);
 }
 size_t sweep_part_granules(int G) { return (size_t)2 * 2 * G * kSweepGranStride; }
 

@@ -26,16 +26,30 @@ struct SweepArgs {
   double2* Pf;
   double2* Pb;
   // multi-workgroup partitioned solves: G workgroups (one persistent cooperative launch per
-  // sweep), kSweepChunks chunks each (chunks = kSweepChunks G).  Pw [nsys][G][2][B][B]: per
-  // workgroup the product of its forward (0) / backward (1) chunk maps (sweep_wg_setup_kernel).
+  // sweep), kSweepChunks chunks each (chunks = kSweepChunks G).  Pw [nsys][G][2][16][B][B]:
+  // per workgroup the prefix (forward, 0) / suffix (backward, 1) products of its chunk maps
+  // (sweep_wg_setup_kernel).
   // Carries cross workgroups as tagged granules, gran [2 dir][2 parity][G][kSweepGranStride].
   int G;
   double2* Pw;
   unsigned long long* gran;
   unsigned* timeout;  // set when a grid wait gives up (the output is then garbage)
   unsigned seq;       // launch sequence number of the granule tags (1 .. 2^17 - 1)
+  // diagnostic (hh_op_sweep_profile): per workgroup [G][kSweepProfSlots] s_memrealtime ticks of
+  // the partitioned solves' phases, accumulated by each workgroup's thread 0; null: off
+  unsigned long long* prof;
 };
+constexpr int kSweepProfSlots = 16;
 
+// Storage order of every B x B block-Thomas matrix (P, Psi_f, Psi_b, the workgroup maps):
+// entry (row j, column c) at pidx<B>(j, c) = (c % (B/2)) 2B + (c / (B/2)) B + j.  A half-wave
+// of the partitioned solve (lanes g 16 + j, row j, columns g B/2 + q) then loads, per q, 2B
+// contiguous entries -- coalesced, where row-major rows made every load instruction touch all
+// of the matrix's cache lines.
+template <int B>
+__host__ __device__ constexpr int pidx(int j, int c) {
+  return (c % (B / 2)) * 2 * B + (c / (B / 2)) * B + j;
+}
 int sweep_block(int b);
 size_t sweep_scratch_per_wave(int n);  // padded block size B (4, 8, 12, 16) or 0 if b > 16
 // what: 0 factor (one wave per system), 1 forward sweep, 2 middle sweep, 3 backward sweep,
@@ -52,6 +66,8 @@ constexpr int kSweepGranStride = 64;  // u64 granules per (direction, parity, wo
 size_t sweep_chunk_scratch(int n);
 // largest workgroup count of a partitioned solve for block size B (LDS of the grid chain)
 int sweep_part_max_wgs(int B);
+// whether a partitioned solve over G workgroups keeps its B-vectors in LDS (else in yscr)
+bool sweep_part_ys_lds(int B, int G, int n);
 // u64 granules of SweepArgs::gran for G workgroups
 size_t sweep_part_granules(int G);
 

@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kSetupThreads) void dense_setup_kernel(const SweepA
       double2 acc = z;
       ufor<0, B>([&](auto lc) {
         constexpr int l = decltype(lc)::value;
-        acc = cfma(pl[j * B + l], t[l], acc);
+        acc = cfma(pl[pidx<B>(j, l)], t[l], acc);
       });
       y[j] = acc;
       Yi[(size_t)j * kSetupThreads] = acc;
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kSetupThreads) void dense_setup_kernel(const SweepA
         double2 acc = z;
         ufor<0, B>([&](auto lc) {
           constexpr int l = decltype(lc)::value;
-          acc = cfma(pl[j * B + l], t[l], acc);
+          acc = cfma(pl[pidx<B>(j, l)], t[l], acc);
         });
         const double2 yi = below ? z : Yi[(size_t)j * kSetupThreads];
         y[j] = csub(yi, acc);
