@@ -200,6 +200,38 @@ struct GivensState {
   int* ctrl;          // [0] stop flag of the queued cycle, [1] last column executed
   int restart;
 };
+// One pass over the Krylov basis per lagged GMRES inner iteration (krylov.hip
+// fused_iter_kernel; single rank and slab, 5-point operator, M = none or Jacobi): the update of
+// iteration K-1, u_K = w_{K-1} - sum_{k<K} c_k u_k (c_k = d_k s_k^2 from the raw dots and the
+// basis scales, as update_kernel), written to V + K ldv with its |u_K|^2 partials (npart); then
+// w_K = M A (s_K u_K) into wout and the next projection's partials <u_k, w_K>, k <= K, and
+// |w_K|^2 (partials, width 2 (K + 1) + 2) -- multidot_kernel's quantities.  Every basis vector
+// is read from HBM once per iteration instead of twice.
+struct FusedArgs {
+  const double2* V;
+  size_t ldv;
+  const double2* win;      // w_{K-1}
+  double2* wout;           // w_K
+  double2* uout;           // u_K (= V + K ldv)
+  const double* raw;       // raw dots d_k (2 K doubles) of w_{K-1}
+  const double* vscale;    // s_k, k < K
+  const double* sin;       // s_K, the scale of the SpMV input (gmres_lag_kernel's estimate)
+  const double2* tab_i;
+  const double2* tab_j;
+  const double* invc2;     // or nullptr (constant medium)
+  double invc2_const;
+  int n;
+  int rows;                // rows per band (grid: fused_iter_blocks)
+  int jac;                 // 1: Jacobi M
+  double* partials;
+  double* npart;
+  const int* stop;
+};
+constexpr int kFusedMaxK = 20;  // K <= this (restart <= kFusedMaxK + 1)
+int fused_iter_rows(int n);
+int fused_iter_blocks(int n, int rows);
+void launch_fused_iter(int K, const FusedArgs& a, int blocks, hipStream_t stream);
+
 // After multidot+update reductions: column `col` of H from raw dots (red_dots, 2*(col+1)
 // doubles + |w|^2 at [2*(col+1)]) and |w_new|^2 (red_norm[0]).  Then scipy's inner-loop
 // exit test (iterative.py:792-795) on the device: presid <= ptol, breakdown, or

@@ -10,6 +10,7 @@
 // Every reduction is two-level and fixed-order (wave butterfly -> LDS -> per-block partial ->
 // one block per output summing partials in index order), so results are reproducible
 // run to run and identical on every rank after the RCCL allreduce.
+#include <algorithm>
 #include <cstdlib>
 
 #include "hh_internal.hpp"
@@ -583,6 +584,164 @@ bool krylov_rev() {
   return rev;
 }
 
+// One-pass lagged GMRES iteration (FusedArgs, hh_internal.hpp).  A 256-thread block owns a
+// 256-column strip of a band of `rows` grid rows and marches it: per row r it forms u_K on row
+// r + 1 (w_{K-1} and the K basis vectors of that row: the iteration's only HBM read of them),
+// applies the stencil (+ Jacobi) to row r from a three-row register ring (W/E neighbours through
+// a double-buffered LDS row; the strip's two edge columns' u_K formed by the edge waves from
+// broadcast loads), stores u_K and w_K of row r and adds row r's <u_k, w_K> -- the u_k re-read,
+// one row after the first read, from L2.  The band's two halo rows of u_K are formed, never
+// stored (each is a neighbouring band's own row): (rows + 2) / rows of the basis rows are read.
+// Tiles are dealt to XCDs in contiguous runs (block b -> XCD b % 8), so a band's halo rows are
+// mostly read on the XCD that owns them.  Arithmetic per point: update_kernel's coefficient
+// and term order, stencil.hip's operator (bit-identical to the three launches it replaces,
+// except the inner products' summation order).
+// by-value select (a select of lvalues would become a select of addresses)
+__device__ __forceinline__ double2 csel(bool c, double2 a, double2 b) {
+  return make_double2(c ? a.x : b.x, c ? a.y : b.y);
+}
+
+template <int K, bool CONSTC>
+__global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
+  if (a.stop && *a.stop) return;
+  __shared__ double2 coef[K];
+  __shared__ double2 urow[2][kT + 2];
+  const int n = a.n, R = a.rows;
+  const int tiles_x = (n + kT - 1) / kT, bands = (n + R - 1) / R, T = tiles_x * bands;
+  const int per_xcd = (T + 7) / 8;
+  const int tile = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+  const bool live = tile < T;
+  const int tx = live ? tile % tiles_x : 0, ty = live ? tile / tiles_x : 0;
+  const int t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
+  const int i0 = tx * kT, i = i0 + t;
+  const bool act = i < n;
+  const int ic = min(i, n - 1);
+  const int rb = ty * R, re = min(rb + R, n);
+  // the strip's edge columns: wave 0 forms u_K at i0 - 1, the last wave at i0 + kT
+  const bool ew = wv == 0, ee = wv == kT / kWave - 1;
+  const int ie = min(max(ew ? i0 - 1 : i0 + kT, 0), n - 1);
+  const bool ehas = (ew && i0 > 0) || (ee && i0 + kT < n);
+  if (t < K) {
+    const double sk = a.vscale[t];
+    const double2 hk = cscale(make_double2(a.raw[2 * t], a.raw[2 * t + 1]), sk);
+    coef[t] = cscale(hk, sk);
+  }
+  __syncthreads();
+  const double sin = *a.sin;
+  const double2 z = make_double2(0.0, 0.0);
+  // u_K at (r, col); rows off the grid are zero (loads from clamped rows, selected by value).
+  // kz: an opaque zero redefined every row, so neither the coefficients' LDS reads nor the
+  // per-vector addresses become loop-invariant / strength-reduced registers (4 + 2-6 VGPRs per
+  // basis vector otherwise, i.e. one wave per SIMD at K >= 11)
+  int kz = 0;
+  auto unew = [&](int r, int col) {
+    __builtin_amdgcn_sched_barrier(0);  // (calls and batches do not interleave: registers)
+    const size_t p = (size_t)min(max(r, 0), n - 1) * n + col;
+    double2 w = a.win[p];
+    constexpr int kB = 4;
+    // a runtime loop over batches (an unrolled one kept ~16 VGPRs per basis vector live:
+    // one wave per SIMD from K = 11)
+#pragma unroll 1
+    for (int k0 = 0; k0 < K; k0 += kB) {
+      double2 v[kB];
+#pragma unroll
+      for (int q = 0; q < kB; ++q) v[q] = a.V[(size_t)min(k0 + q, K - 1) * a.ldv + p];
+#pragma unroll
+      for (int q = 0; q < kB; ++q)
+        if (k0 + q < K) w = csub(w, cmul(coef[k0 + q + kz], v[q]));
+    }
+    return csel(r >= 0 && r < n, w, z);
+  };
+  const double2 AW = a.tab_i[ic], AE = a.tab_i[n + ic], R1 = a.tab_i[2 * n + ic];
+  double2 acc[K + 1];
+#pragma unroll
+  for (int k = 0; k <= K; ++k) acc[k] = z;
+  double nw = 0.0, nu = 0.0;
+  if (live) {
+    double2 uS = unew(rb - 1, ic), uC = unew(rb, ic);
+    int buf = 0;
+    for (int r0 = rb; r0 < re; ++r0) {
+      int r = r0;
+      asm volatile("" : "+s"(r), "+s"(kz));
+      const double2 uN = unew(r + 1, ic);
+      // (every wave, so no branch: the edge waves' value is used, the others' is a broadcast
+      // recomputation of a column the strip owns; a branch let the compiler interleave the two
+      // updates' loads and keep both sets live)
+      const double2 ue = unew(r, ie);
+      urow[buf][1 + t] = csel(act, uC, z);
+      if (ew && lane == 0) urow[buf][0] = csel(ehas, ue, z);
+      if (ee && lane == kWave - 1) urow[buf][kT + 1] = csel(ehas, ue, z);
+      __syncthreads();
+      const double2 uW = urow[buf][t], uE = urow[buf][t + 2];
+      const double* q = reinterpret_cast<const double*>(a.tab_j) + 8 * (size_t)r;
+      const double2 R2 = make_double2(q[0], q[1]), BS = make_double2(q[2], q[3]);
+      const double2 BN = make_double2(q[4], q[5]), OM = make_double2(q[6], q[7]);
+      const size_t p = (size_t)r * n + ic;
+      const double icv = CONSTC ? a.invc2_const : a.invc2[p];
+      const double2 W = cmul(AW, R2);
+      const double2 E = cmul(AE, R2);
+      const double2 S = cmul(BS, R1);
+      const double2 N = cmul(BN, R1);
+      const double2 M = cscale(cmul(OM, R1), icv);
+      const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
+      const double2 D = csub(M, sum4);
+      double2 Au = cmul(S, uS);
+      Au = cfma(W, uW, Au);
+      Au = cfma(D, uC, Au);
+      Au = cfma(E, uE, Au);
+      Au = cfma(N, uN, Au);
+      const double2 w = csel(act, a.jac ? cscale(cdiv(Au, D), sin) : cscale(Au, sin), z);
+      if (act) {
+        a.wout[p] = w;
+        a.uout[p] = uC;
+      }
+      const double2 uo = csel(act, uC, z);
+      nu = fma(uo.x, uo.x, fma(uo.y, uo.y, nu));
+      nw = fma(w.x, w.x, fma(w.y, w.y, nw));
+      // (batches of 8 re-reads in flight: all K at once would hold 4 K more VGPRs)
+#pragma unroll
+      for (int k0 = 0; k0 < K; k0 += 8) {
+        double2 v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = a.V[(size_t)min(k0 + q, K - 1) * a.ldv + p];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (k0 + q < K) acc[k0 + q] = cfma_conj(v[q], w, acc[k0 + q]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      acc[K] = cfma_conj(uo, w, acc[K]);
+      uS = uC;
+      uC = uN;
+      buf ^= 1;
+    }
+  }
+  double v[2 * (K + 1) + 1];
+#pragma unroll
+  for (int k = 0; k <= K; ++k) {
+    v[2 * k] = acc[k].x;
+    v[2 * k + 1] = acc[k].y;
+  }
+  v[2 * (K + 1)] = nw;
+  block_reduce_vec<2 * (K + 1) + 1>(v, a.partials, 2 * (K + 1) + 2);
+  double vn[1] = {nu};
+  block_reduce_vec<1>(vn, a.npart, kMaxNorms);
+}
+
+template <int K>
+void fused_launch(const FusedArgs& a, int blocks, hipStream_t s) {
+  if (a.invc2)
+    hipLaunchKernelGGL((fused_iter_kernel<K, false>), dim3(blocks), dim3(kT), 0, s, a);
+  else
+    hipLaunchKernelGGL((fused_iter_kernel<K, true>), dim3(blocks), dim3(kT), 0, s, a);
+}
+template <int... Ks>
+struct FTable {
+  using FN = void (*)(const FusedArgs&, int, hipStream_t);
+  static constexpr FN f[] = {fused_launch<Ks>...};
+};
+using FusedTable = FTable<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20>;
+static_assert(kFusedMaxK == 20, "table covers 1..kFusedMaxK");
+
 template <int K>
 void md_launch(const double2* V, size_t ldv, const double2* w, size_t len, double* part,
                int blocks, hipStream_t s, const int* stop, double* out, int cols,
@@ -650,6 +809,25 @@ using Table = KTable<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 
 static_assert(kMaxProj == 32, "table covers 1..kMaxProj");
 
 }  // namespace
+
+int fused_iter_rows(int n) {
+  static const int env = [] {
+    const char* e = std::getenv("HH_FUSED_ROWS");
+    return e ? std::atoi(e) : 0;
+  }();
+  const long tiles_x = (n + kT - 1) / kT;
+  int R = env > 0 ? env : (int)std::min<long>(32, std::max<long>(8, tiles_x * n / 1024));
+  // the partial rows (one per block) fit kMaxStreamBlocks
+  while ((long)tiles_x * ((n + R - 1) / R) > kMaxStreamBlocks) R *= 2;
+  return R;
+}
+int fused_iter_blocks(int n, int rows) {
+  const int T = (n + kT - 1) / kT * ((n + rows - 1) / rows);
+  return (T + 7) / 8 * 8;
+}
+void launch_fused_iter(int K, const FusedArgs& a, int blocks, hipStream_t stream) {
+  FusedTable::f[K - 1](a, blocks, stream);
+}
 
 void tune_krylov(int nt, int blocks) {
   g_krylov_nt = nt < 0 ? -1 : (nt != 0);

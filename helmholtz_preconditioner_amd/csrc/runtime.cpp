@@ -226,6 +226,7 @@ struct hh_op {
   int sw_wgs = 0;               // requested workgroups per partitioned solve (0: by n)
   unsigned long long* sw_prof = nullptr;  // diagnostic phase ticks (hh_op_sweep_profile)
   unsigned long long* sw_chain = nullptr;  // granules of the persistent apply chain, or null
+  double2* fw = nullptr;        // one-pass GMRES iteration: the w_j ping-pong pair [2][nloc]
   unsigned sw_seq = 0;                     // its launch sequence number
   double2* sw_u = nullptr;      // dense apply scratch (n^2)
   double2* sw_in = nullptr;     // dense apply: fixed input / output the captured graphs use
@@ -252,7 +253,8 @@ struct hh_op {
   hh_stats stats{};
   SpanTimer timer;
   int last_path = 0;  // the last hh_gmres: 0 regular cycle, 1 small-grid cycle kernel, 2 small
-                      // cycle refused at launch -> regular cycle (hh_op_last_solve_path)
+                      // cycle refused at launch -> regular cycle, 3 one-pass regular cycle
+                      // (hh_op_last_solve_path)
 };
 
 struct hh_vec {
@@ -757,6 +759,15 @@ void read_dev(hh_op* op, const double* dsrc, double* hdst, int count) {
 // timeout in red[kRedTimeout] instead of hanging; its output is then garbage.  Every path that
 // ran a chained sweep apply checks the word here (one synchronising read; nothing for the other
 // preconditioners) and clears it only after the check, so no timeout is lost or reported twice.
+// the one-pass iteration where it applies, unless HH_FUSED_ITER=0
+bool fused_default() {
+  static const bool on = [] {
+    const char* e = std::getenv("HH_FUSED_ITER");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 void check_sweep_chain(hh_op* op) {
   const bool grid = op->sw_chain || (!op->sw_T && op->sweep.chunks > 0 && op->sweep.G > 1);
   if (!grid || !is_sweep(op->pkind)) return;
@@ -1155,6 +1166,7 @@ static void op_release(hh_op* op) {
   dfree(op->V);
   dfree(op->gbuf);
   dfree(op->npart);
+  dfree(op->fw);
   dfree(op->small_scr);
   dfree(op->small_ticks);
   dfree(op->kcount);
@@ -1698,7 +1710,8 @@ HH_API int hh_op_set_stencil(hh_op* op, int points, double alpha, double c, doub
 HH_API int hh_op_set_krylov_mode(hh_op* op, int mode) {
   GUARD_BEGIN
   REQUIRE(op, "null op");
-  REQUIRE(mode >= 0 && mode <= 2, "krylov mode must be 0 (auto), 1 (two reductions) or 2 (one)");
+  REQUIRE(mode >= 0 && mode <= 3,
+          "krylov mode must be 0 (auto), 1 (two reductions), 2 (one) or 3 (one, one pass)");
   op->krylov_mode = mode;
   GUARD_END
 }
@@ -2006,7 +2019,18 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
   bool legacy = legacy_maxiter != 0;
   // collectives per inner iteration: one (lagged normalisation) by default across ranks, two on
   // one rank (no collective there; the exact-norm path keeps round 1's bit-for-bit results)
-  const bool lagged = !reorth && (op->krylov_mode == 2 || (op->krylov_mode == 0 && c->world > 1));
+  // one pass over the basis per inner iteration (krylov.hip fused_iter_kernel): the lagged
+  // iteration with the update, the next M A and the next projection in one streaming kernel;
+  // single rank and slab, 5-point, M none / Jacobi (mode 3, or by default where it applies)
+  const bool fused_ok = !reorth && c->world == 1 && op->slabs.size() == 1 && op->points == 5 &&
+                        (op->pkind == HH_PREC_NONE || op->pkind == HH_PREC_JACOBI) &&
+                        restart <= kFusedMaxK + 1;
+  // (by default from n = 1024: smaller grids give the pass too few tiles to stream at speed --
+  // n = 300: 16-25k it/s against 29-30k for the regular cycle, profiles/r03q)
+  const bool fused = fused_ok && (op->krylov_mode == 3 ||
+                                  (op->krylov_mode == 0 && fused_default() && op->n >= 1024));
+  const bool lagged = !reorth && !fused &&
+                      (op->krylov_mode == 2 || (op->krylov_mode == 0 && c->world > 1));
   // small single-rank grids: the whole cycle in one launch (gmres_small.hip) -- launch-bound
   // otherwise (five kernel boundaries per inner iteration at ~0.5 MB each)
   const bool small = !reorth && op->small_cycle != 0 && c->world == 1 && op->slabs.size() == 1 &&
@@ -2026,6 +2050,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     }
   }
 
+  if (fused && !op->fw) op->fw = dalloc<double2>(2 * L);
   double r0 = bnrm2;  // (x0 = 0: r = b)
   if (x_any) {
     residual(op, b, x, V, 4);  // V[0] = M (b - A x0); red[4..5]
@@ -2060,7 +2085,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     }
   };
   bool small_refused = false;
-  op->last_path = small ? 1 : 0;
+  op->last_path = small ? 1 : (fused ? 3 : 0);
   if (small) {
     // Small grids: whole-cycle launches (gmres_small.hip), each running up to kSmallBatch restart
     // cycles -- scipy's restart-loop decisions are taken on the device from the state below
@@ -2212,6 +2237,56 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     const long left = legacy ? maxiter - inner : (long)restart;
     const int stop_col = (int)std::min<long>(restart - 1, left - 1);
     op->stop_flag = g.ctrl;
+    if (fused) {
+      // the lagged iteration (below) with update(c2), M A(c2 + 1) and multidot(c2 + 1) in ONE
+      // pass over the basis (fused_iter_kernel): w_j lives in a ping-pong pair instead of V[j+1]
+      // (the pass writes u_{j+1} there while other tiles still read their halo rows of w_j)
+      const int* stp = g.ctrl;
+      double2* Wb[2] = {op->fw, op->fw + L};
+      apply_MA(op, V, g.sscale, Wb[0]);  // w_0 = M A (s_0 u_0)
+      launch_multidot(V, ldv, 1, Wb[0], L, op->partials, blocks, s, stp);
+      launch_reduce(op->partials, blocks, 4, 3, op->red + 16, s, stp);
+      launch_gmres_lag(g, 0, op->red + 16, op->red + 16 + 3, false, eps, ptol, stop_col, s);
+      const int frows = fused_iter_rows(op->n);
+      const int fblocks = fused_iter_blocks(op->n, frows);
+      for (int c2 = 0; c2 < stop_col; ++c2) {
+        const int K = c2 + 1, K2 = K + 1;
+        FusedArgs fa{};
+        fa.V = V;
+        fa.ldv = ldv;
+        fa.win = Wb[c2 & 1];
+        fa.wout = Wb[(c2 + 1) & 1];
+        fa.uout = V + (size_t)K * ldv;
+        fa.raw = op->red + 16;
+        fa.vscale = g.vscale;
+        fa.sin = g.sscale + K;
+        fa.tab_i = op->tab_i;
+        fa.tab_j = op->slabs[0].tab_j;
+        fa.invc2 = op->const_c ? nullptr : op->slabs[0].invc2;
+        fa.invc2_const = op->invc2_const;
+        fa.n = op->n;
+        fa.rows = frows;
+        fa.jac = op->pkind == HH_PREC_JACOBI ? 1 : 0;
+        fa.partials = op->partials;
+        fa.npart = op->npart;
+        fa.stop = stp;
+        launch_fused_iter(K, fa, fblocks, s);
+        op->stats.spmv_count++;
+        launch_reduce(op->partials, fblocks, 2 * K2 + 2, 2 * K2 + 1, op->red + 16, s, stp);
+        launch_reduce(op->npart, fblocks, kMaxNorms, 1, op->red + 16 + 2 * K2 + 1, s, stp);
+        launch_gmres_lag(g, c2 + 1, op->red + 16, op->red + 16 + 2 * K2 + 1, false, eps, ptol,
+                         stop_col, s);
+        HIPC(hipGetLastError());
+      }
+      {  // the last column's update and the norm that completes it
+        const int K = stop_col + 1;
+        launch_update(V, ldv, K, op->red + 16, g.vscale, Wb[stop_col & 1],
+                      V + (size_t)(stop_col + 1) * ldv, L, op->npart, blocks, s, stp);
+        launch_reduce(op->npart, blocks, kMaxNorms, 1, op->red + 8, s, stp);
+        launch_gmres_lag(g, stop_col + 1, nullptr, op->red + 8, true, eps, ptol, stop_col, s);
+        HIPC(hipGetLastError());
+      }
+    }
     for (int c2 = 0; c2 <= stop_col && lagged; ++c2) {
       // ONE allreduce per inner iteration (lagged normalisation, gmres_lag_kernel): the norm of
       // the vector the previous update wrote (u_c2, its partials kept in npart) travels with
@@ -2243,7 +2318,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         launch_gmres_lag(g, c2 + 1, nullptr, op->red + 8, true, eps, ptol, stop_col, s);
       }
     }
-    for (int c2 = 0; c2 <= stop_col && !lagged; ++c2) {
+    for (int c2 = 0; c2 <= stop_col && !lagged && !fused; ++c2) {
       double2* vcol = V + (size_t)c2 * ldv;
       double2* w = V + (size_t)(c2 + 1) * ldv;
       const int* stp = g.ctrl;

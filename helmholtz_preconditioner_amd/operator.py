@@ -268,13 +268,15 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
         (identical results; for A/B timing)."""
         check(lib.hh_op_sl_fusion(self.handle, int(bool(enable))))
 
-    KRYLOV_MODES = {"auto": 0, "two": 1, "one": 2}
+    KRYLOV_MODES = {"auto": 0, "two": 1, "one": 2, "fused": 3}
 
     def krylov_mode(self, mode: str = "auto"):
         """Global reductions per GMRES inner iteration: "two" (projections, then the updated
         vector's norm -- exact normalisation), "one" (lagged normalisation: one allreduce per
-        iteration), "auto" (one across ranks, two on a single rank).  Results agree to
-        rounding."""
+        iteration), "fused" ("one" with the update, the next M A and its projections in one
+        pass over the basis: single rank and slab, 5-point, M none / Jacobi, restart <= 21),
+        "auto" ("fused" where it applies, else one across ranks and two on a single rank).
+        Results agree to rounding."""
         if mode not in self.KRYLOV_MODES:
             raise ValueError(f"mode must be one of {sorted(self.KRYLOV_MODES)}")
         check(lib.hh_op_set_krylov_mode(self.handle, self.KRYLOV_MODES[mode]))
@@ -300,7 +302,8 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
         check(lib.hh_op_read_timing(self.handle, _ffi.dptr(ms), cnt))
         return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(_ffi.SPAN_NAMES)}
 
-    SOLVE_PATHS = {0: "regular", 1: "small-cycle", 2: "small-cycle refused -> regular"}
+    SOLVE_PATHS = {0: "regular", 1: "small-cycle", 2: "small-cycle refused -> regular",
+                   3: "one-pass"}
 
     def last_solve_path(self) -> str:
         """Cycle form the last ``gmres`` on this operator ran (hh_op_last_solve_path)."""

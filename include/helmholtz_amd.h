@@ -226,8 +226,12 @@ int hh_op_set_history_callback(hh_op* op, hh_gmres_history_callback cb, void* us
  * the previous iteration's update wrote travels with the projections (lagged normalisation: the
  * Hessenberg subdiagonal of column j is completed in iteration j+1, the SpMV input is scaled by a
  * Pythagorean estimate meanwhile; H, the residual history and x agree to rounding, one extra
- * collective per restart cycle).  mode 0 (default): one reduction (mode 2) across ranks, two
- * (mode 1) on a single rank.  CGS2 (reorth) always uses mode 1. */
+ * collective per restart cycle).  mode 3: mode 2 with the update of iteration j, the M A of
+ * iteration j+1 and its projections in ONE pass over the basis (each basis vector read from HBM
+ * once per iteration instead of twice; single rank and slab, 5-point operator, M none or
+ * Jacobi, restart <= 21; elsewhere as mode 0).  mode 0 (default): mode 3 where it applies
+ * (HH_FUSED_ITER=0: not), else one reduction (mode 2) across ranks and two (mode 1) on a single
+ * rank.  CGS2 (reorth) always uses mode 1. */
 int hh_op_set_krylov_mode(hh_op* op, int mode);
 /* Whole-cycle GMRES kernel for small grids (no reference counterpart): a restart cycle of
  * hh_gmres as ONE launch whose workgroups keep the Krylov basis on chip and meet once per inner
@@ -242,7 +246,8 @@ int hh_op_set_small_cycle(hh_op* op, int mode);
 /* Which cycle form the last hh_gmres on `op` ran: 0 the regular per-launch cycle, 1 the
  * small-grid whole-cycle kernel, 2 the small-grid kernel refused at its first launch -- its
  * n + 1 workgroups could not be co-resident -- so the regular cycle ran the whole solve
- * instead (same results to rounding; no partial state). */
+ * instead (same results to rounding; no partial state), 3 the regular cycle with the one-pass
+ * iteration (hh_op_set_krylov_mode 3). */
 int hh_op_last_solve_path(hh_op* op, int* path);
 /* Diagnostic: phase timing of the small-grid cycle kernel (workgroup 0's wall clock summed over
  * the following solves): phase_us (optional, 8 doubles) receives the totals so far in us

@@ -1,6 +1,6 @@
 """A/B of the GMRES inner-iteration modes on one grid, interleaved in one process: "two"
-(projections, then the updated vector's norm) vs "one" (lagged normalisation, one reduction
-per iteration), BASELINE config 2 by default (1024^2, constant medium, wn 64, Jacobi,
+(projections, then the updated vector's norm), "one" (lagged normalisation, one reduction
+per iteration) and "fused" (one pass over the basis per iteration; env MODES selects), BASELINE config 2 by default (1024^2, constant medium, wn 64, Jacobi,
 GMRES(20), K = 100 inner iterations).  usage: python tools/ab_krylov_mode.py [n] [wn] [reps]"""
 import os
 import sys
@@ -15,12 +15,13 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 wn = float(sys.argv[2]) if len(sys.argv) > 2 else 64.0
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 K = 100
+MODES = [m for m in os.environ.get("MODES", "two,one,fused").split(",")]
 om, h, eta = H.problem_params(n, 12, wn, 2.0)
 A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.constant_c_mat(n))
 f = H.init_f1_mat(.5, .125, om, n).ravel()
 hist = {}
 for r in range(reps + 1):
-    for mode in ("two", "one"):
+    for mode in MODES:
         A.krylov_mode(mode)
         t0 = time.perf_counter()
         u, info, hh = H.gmres(A, f, rtol=1e-12, restart=20, maxiter=K, M="jacobi",
@@ -30,6 +31,8 @@ for r in range(reps + 1):
         hist[mode] = (u, np.asarray(hh))
         if r > 0:
             print(f"n={n} mode={mode}: {len(hh) / dt:9.1f} it/s", flush=True)
-(u2, h2), (u1, h1) = hist["two"], hist["one"]
-print(f"history max rel diff {np.max(np.abs(h1 - h2) / h2):.2e}, "
-      f"field rel diff {np.linalg.norm(u1 - u2) / np.linalg.norm(u2):.2e}")
+u2, h2 = hist[MODES[0]]
+for m in MODES[1:]:
+    u1, h1 = hist[m]
+    print(f"{m} vs {MODES[0]}: history max rel diff {np.max(np.abs(h1 - h2) / h2):.2e}, "
+          f"field rel diff {np.linalg.norm(u1 - u2) / np.linalg.norm(u2):.2e}")

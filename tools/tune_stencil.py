@@ -23,9 +23,9 @@ p.add_argument("--medium", default="marmousi")
 p.add_argument("--rotate", type=int, default=1,
                help="distinct (x, y) pairs applied round-robin (>1: no cross-launch cache reuse)")
 a = p.parse_args()
-variants = [int(v) for v in a.variants.split(",")]
-rpbs = [int(v) for v in a.rpbs.split(",")]
-grids = [int(v) for v in a.grids.split(",")]
+variants = [int(v) for v in a.variants.replace("/", ",").split(",")]  # (/: gpu_session.sh args)
+rpbs = [int(v) for v in a.rpbs.replace("/", ",").split(",")]
+grids = [int(v) for v in a.grids.replace("/", ",").split(",")]
 
 
 def vname(v):
