@@ -487,6 +487,10 @@ def main():
             "ms_per_iter": round(tg * 1e3 / its, 4),
             "algorithmic_GBps": round(gbytes / tg / 1e9, 1),
             "final_rel_presid": float(hist[-1]) if its else None,
+            # cycle form (hh_op_last_solve_path): "one-pass" = update + next M A + projections in
+            # one pass over the basis (krylov.hip fused_iter_kernel; the bytes counted above stay
+            # the CGS-minimal formula of SURVEY 8d, which that pass moves ~half of)
+            "solve_path": A.last_solve_path(),
         }
 
     R = max(1, args.rotate)
