@@ -203,10 +203,10 @@ struct GivensState {
 // One pass over the Krylov basis per lagged GMRES inner iteration (krylov.hip
 // fused_iter_kernel; single rank and slab, 5-point operator, M = none or Jacobi): the update of
 // iteration K-1, u_K = w_{K-1} - sum_{k<K} c_k u_k (c_k = d_k s_k^2 from the raw dots and the
-// basis scales, as update_kernel), written to V + K ldv with its |u_K|^2 partials (npart); then
-// w_K = M A (s_K u_K) into wout and the next projection's partials <u_k, w_K>, k <= K, and
-// |w_K|^2 (partials, width 2 (K + 1) + 2) -- multidot_kernel's quantities.  Every basis vector
-// is read from HBM once per iteration instead of twice.
+// basis scales, as update_kernel), written to V + K ldv; then w_K = M A (s_K u_K) into wout;
+// per block ONE partial row (width 2 (K + 1) + 2): <u_k, w_K> for k <= K and |w_K|^2 --
+// multidot_kernel's quantities -- then |u_K|^2.  Every basis vector is read from HBM once per
+// iteration instead of twice.
 struct FusedArgs {
   const double2* V;
   size_t ldv;
@@ -224,7 +224,6 @@ struct FusedArgs {
   int rows;                // rows per band (grid: fused_iter_blocks)
   int jac;                 // 1: Jacobi M
   double* partials;
-  double* npart;
   const int* stop;
 };
 constexpr int kFusedMaxK = 20;  // K <= this (restart <= kFusedMaxK + 1)

@@ -638,7 +638,7 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
     __builtin_amdgcn_sched_barrier(0);  // (calls and batches do not interleave: registers)
     const size_t p = (size_t)min(max(r, 0), n - 1) * n + col;
     double2 w = a.win[p];
-    constexpr int kB = 4;
+    constexpr int kB = 8;
     // a runtime loop over batches (an unrolled one kept ~16 VGPRs per basis vector live:
     // one wave per SIMD from K = 11)
 #pragma unroll 1
@@ -664,10 +664,8 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
       int r = r0;
       asm volatile("" : "+s"(r), "+s"(kz));
       const double2 uN = unew(r + 1, ic);
-      // (every wave, so no branch: the edge waves' value is used, the others' is a broadcast
-      // recomputation of a column the strip owns; a branch let the compiler interleave the two
-      // updates' loads and keep both sets live)
-      const double2 ue = unew(r, ie);
+      double2 ue = z;
+      if (ew || ee) ue = unew(r, ie);  // (wave-uniform: the two edge waves only)
       urow[buf][1 + t] = csel(act, uC, z);
       if (ew && lane == 0) urow[buf][0] = csel(ehas, ue, z);
       if (ee && lane == kWave - 1) urow[buf][kT + 1] = csel(ehas, ue, z);
@@ -715,16 +713,17 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
       buf ^= 1;
     }
   }
-  double v[2 * (K + 1) + 1];
+  // one partial row: the K + 1 dots, |w_K|^2, then |u_K|^2 -- one reduce launch lands the last
+  // exactly where gmres_lag_kernel reads sigma_K^2 (red + 16 + 2 (K + 1) + 1)
+  double v[2 * (K + 1) + 2];
 #pragma unroll
   for (int k = 0; k <= K; ++k) {
     v[2 * k] = acc[k].x;
     v[2 * k + 1] = acc[k].y;
   }
   v[2 * (K + 1)] = nw;
-  block_reduce_vec<2 * (K + 1) + 1>(v, a.partials, 2 * (K + 1) + 2);
-  double vn[1] = {nu};
-  block_reduce_vec<1>(vn, a.npart, kMaxNorms);
+  v[2 * (K + 1) + 1] = nu;
+  block_reduce_vec<2 * (K + 1) + 2>(v, a.partials, 2 * (K + 1) + 2);
 }
 
 template <int K>

@@ -2268,12 +2268,11 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         fa.rows = frows;
         fa.jac = op->pkind == HH_PREC_JACOBI ? 1 : 0;
         fa.partials = op->partials;
-        fa.npart = op->npart;
         fa.stop = stp;
         launch_fused_iter(K, fa, fblocks, s);
         op->stats.spmv_count++;
-        launch_reduce(op->partials, fblocks, 2 * K2 + 2, 2 * K2 + 1, op->red + 16, s, stp);
-        launch_reduce(op->npart, fblocks, kMaxNorms, 1, op->red + 16 + 2 * K2 + 1, s, stp);
+        // (dots, |w|^2 and |u|^2 in one partial row: one reduce)
+        launch_reduce(op->partials, fblocks, 2 * K2 + 2, 2 * K2 + 2, op->red + 16, s, stp);
         launch_gmres_lag(g, c2 + 1, op->red + 16, op->red + 16 + 2 * K2 + 1, false, eps, ptol,
                          stop_col, s);
         HIPC(hipGetLastError());
