@@ -223,6 +223,9 @@ struct FusedArgs {
   int n;
   int rows;                // rows per band (grid: fused_iter_blocks)
   int jac;                 // 1: Jacobi M
+  int sl;                  // 1: the two-sweep shifted-Laplace M (fused_sl_iter_kernel)
+  double2 mshift;          // SL: mass-term multiplier of A_beta
+  double damping;          // SL: damped-Jacobi weight
   double* partials;
   const int* stop;
 };

@@ -2023,12 +2023,16 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
   // iteration with the update, the next M A and the next projection in one streaming kernel;
   // single rank and slab, 5-point, M none / Jacobi (mode 3, or by default where it applies)
   const bool fused_ok = !reorth && c->world == 1 && op->slabs.size() == 1 && op->points == 5 &&
-                        (op->pkind == HH_PREC_NONE || op->pkind == HH_PREC_JACOBI) &&
+                        (op->pkind == HH_PREC_NONE || op->pkind == HH_PREC_JACOBI ||
+                         (op->pkind == HH_PREC_SHIFTED_LAPLACE && op->sweeps == 2)) &&
                         restart <= kFusedMaxK + 1;
   // (by default from n = 1024: smaller grids give the pass too few tiles to stream at speed --
   // n = 300: 16-25k it/s against 29-30k for the regular cycle, profiles/r03q)
+  // (the shifted-Laplace pass is opt-in: 736 vs 755 it/s for the regular cycle at 4096^2,
+  // profiles/r03y -- two stencils and two complex divisions per point make it VALU-heavy)
   const bool fused = fused_ok && (op->krylov_mode == 3 ||
-                                  (op->krylov_mode == 0 && fused_default() && op->n >= 1024));
+                                  (op->krylov_mode == 0 && fused_default() && op->n >= 1024 &&
+                                   op->pkind != HH_PREC_SHIFTED_LAPLACE));
   const bool lagged = !reorth && !fused &&
                       (op->krylov_mode == 2 || (op->krylov_mode == 0 && c->world > 1));
   // small single-rank grids: the whole cycle in one launch (gmres_small.hip) -- launch-bound
@@ -2267,6 +2271,9 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         fa.n = op->n;
         fa.rows = frows;
         fa.jac = op->pkind == HH_PREC_JACOBI ? 1 : 0;
+        fa.sl = op->pkind == HH_PREC_SHIFTED_LAPLACE ? 1 : 0;
+        fa.mshift = op->mshift;
+        fa.damping = op->damping;
         fa.partials = op->partials;
         fa.stop = stp;
         launch_fused_iter(K, fa, fblocks, s);

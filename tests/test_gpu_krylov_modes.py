@@ -160,7 +160,8 @@ def test_fused_pass_matches_reference_golden(ctx, name):
 
 
 @pytest.mark.parametrize("n,kind,precond", [(300, "c1", "jacobi"), (513, "marmousi", None),
-                                            (1100, "const", "jacobi"), (257, "c2", None)])
+                                            (1100, "const", "jacobi"), (257, "c2", None),
+                                            (300, "marmousi", "sl"), (770, "c1", "sl")])
 @pytest.mark.parametrize("restart,K", [(20, 12), (7, 16), (1, 4), (21, 21)])
 def test_fused_pass_matches_lagged(ctx, n, kind, precond, restart, K):
     """the one-pass iteration against the lagged one it fuses (same arithmetic but the inner
@@ -171,6 +172,8 @@ def test_fused_pass_matches_lagged(ctx, n, kind, precond, restart, K):
     cm = medium(kind, n) if kind != "marmousi" else H.marmousi_like_c_mat(n)
     A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, context=ctx)
     f = O.init_f1_mat(.5, .125, om, n).ravel()
+    if precond == "sl":  # (the two-sweep shifted Laplace: fused_sl_iter_kernel)
+        precond = H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7)
     out = {}
     for mode in ("one", "fused"):
         A.krylov_mode(mode)
@@ -192,7 +195,8 @@ def test_fused_pass_matches_lagged(ctx, n, kind, precond, restart, K):
 
 def test_fused_pass_is_the_single_rank_default(ctx):
     """mode auto on one rank picks the one-pass iteration where it applies (n >= 1024, M none /
-    Jacobi, restart <= 21) and the regular cycle elsewhere (shifted Laplace, restart 30)"""
+    Jacobi, restart <= 21) and the regular cycle elsewhere (restart 30, shifted Laplace); mode
+    "fused" also runs the two-sweep shifted Laplace in one pass (not three sweeps)"""
     n = 1024
     om, h, eta = O.problem_params(n, 12, 64.0, 2.0)
     A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.constant_c_mat(n), context=ctx)
@@ -202,4 +206,10 @@ def test_fused_pass_is_the_single_rank_default(ctx):
     H.gmres(A, f, rtol=1e-12, restart=30, maxiter=5, M="jacobi")
     assert A.last_solve_path() == "regular"
     H.gmres(A, f, rtol=1e-12, restart=20, maxiter=3, M=H.ShiftedLaplace(A))
+    assert A.last_solve_path() == "regular"  # (the shifted-Laplace pass is opt-in: mode 3)
+    A.krylov_mode("fused")
+    H.gmres(A, f, rtol=1e-12, restart=20, maxiter=3, M=H.ShiftedLaplace(A))
+    assert A.last_solve_path() == "one-pass"
+    H.gmres(A, f, rtol=1e-12, restart=20, maxiter=3, M=H.ShiftedLaplace(A, sweeps=3))
     assert A.last_solve_path() == "regular"
+    A.krylov_mode("auto")
