@@ -859,6 +859,10 @@ __global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
     // u(L-1, ie), z1(L-2, ie).
     double2 uP = z, uC = z, Tm = z, z1a = z, z1b = z;
     double2 euP = z, euC = z, ez1b = z;
+    // row L-1's shifted diagonal and the reciprocal of its |.|^2 (cdiv's one division), handed
+    // to the second sweep of the next step, whose row it is
+    double2 Dbm = make_double2(1.0, 0.0);
+    double invm = 1.0;
     int buf = 0;
     for (int L0 = rb - 2; L0 <= re + 1; ++L0) {
       int L = L0;
@@ -893,7 +897,11 @@ __global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
       Au = cfma(c1.E, uE, Au);
       Au = cfma(c1.N, uN, Au);
       const double2 T1 = csel(act && v1, cscale(Au, sin), z);
-      const double2 z1c = csel(act && v1, cscale(cdiv(T1, c1.Db), damp), z);
+      const double inv1 = 1.0 / fma(c1.Db.x, c1.Db.x, c1.Db.y * c1.Db.y);
+      auto cdivr = [](double2 x, double2 b, double inv) {  // cdiv with the reciprocal given
+        return make_double2(fma(x.x, b.x, x.y * b.y) * inv, fma(x.y, b.x, -x.x * b.y) * inv);
+      };
+      const double2 z1c = csel(act && v1, cscale(cdivr(T1, c1.Db, inv1), damp), z);
       // the same at the edge column (edge waves; broadcast values)
       double2 ez1c = z;
       if (ew || ee) {
@@ -912,13 +920,18 @@ __global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
       const int r = L - 2;
       if (r >= rb && r < re) {  // (block-uniform)
         const size_t p = (size_t)r * n + ic;
-        const Co c2 = coefs(r, ic, icv_at(r, ic));
-        double2 Az = cmul(c2.S, z1a);
-        Az = cfma(c2.W, zW, Az);
-        Az = cfma(c2.Db, z1b, Az);
-        Az = cfma(c2.E, zE, Az);
-        Az = cfma(c2.N, z1c, Az);
-        const double2 w = csel(act, cadd(z1b, cscale(cdiv(csub(Tm, Az), c2.Db), damp)), z);
+        // row r's W, E, S, N (no mass term: its D_beta and reciprocal come from the last step)
+        const double* q = reinterpret_cast<const double*>(a.tab_j) + 8 * (size_t)r;
+        const double2 R2 = make_double2(q[0], q[1]), BS = make_double2(q[2], q[3]);
+        const double2 BN = make_double2(q[4], q[5]);
+        const double2 AW = a.tab_i[ic], AE = a.tab_i[n + ic], R1 = a.tab_i[2 * n + ic];
+        const double2 W2 = cmul(AW, R2), E2 = cmul(AE, R2), S2 = cmul(BS, R1), N2 = cmul(BN, R1);
+        double2 Az = cmul(S2, z1a);
+        Az = cfma(W2, zW, Az);
+        Az = cfma(Dbm, z1b, Az);
+        Az = cfma(E2, zE, Az);
+        Az = cfma(N2, z1c, Az);
+        const double2 w = csel(act, cadd(z1b, cscale(cdivr(csub(Tm, Az), Dbm, invm), damp)), z);
         if (act) {
           a.wout[p] = w;
           a.uout[p] = uP;
@@ -946,6 +959,8 @@ __global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
       euP = euC;
       euC = euN;
       ez1b = ez1c;
+      Dbm = c1.Db;
+      invm = inv1;
       buf ^= 1;
     }
   }

@@ -17,14 +17,17 @@ reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 K = 100
 MODES = [m for m in os.environ.get("MODES", "two,one,fused").split(",")]
 om, h, eta = H.problem_params(n, 12, wn, 2.0)
-A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.constant_c_mat(n))
+PRE = os.environ.get("PRECOND", "jacobi")  # jacobi | sl (config 3: Marmousi-like, SL beta 0.5)
+cm = H.marmousi_like_c_mat(n) if PRE == "sl" else H.constant_c_mat(n)
+A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm)
 f = H.init_f1_mat(.5, .125, om, n).ravel()
+M = H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7) if PRE == "sl" else "jacobi"
 hist = {}
 for r in range(reps + 1):
     for mode in MODES:
         A.krylov_mode(mode)
         t0 = time.perf_counter()
-        u, info, hh = H.gmres(A, f, rtol=1e-12, restart=20, maxiter=K, M="jacobi",
+        u, info, hh = H.gmres(A, f, rtol=1e-12, restart=20, maxiter=K, M=M,
                               callback=lambda x: None, callback_type="legacy",
                               return_history=True)
         dt = time.perf_counter() - t0
