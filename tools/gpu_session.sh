@@ -15,6 +15,7 @@
 #   pmc[:ARGS]           FETCH_SIZE and WRITE_SIZE, one rocprofv3 --pmc pass each, of
 #                        tools/prof_stencil.py ARGS (default --iters 20)
 #   pmcset               the same at every BASELINE config's grid, summarised into pmc_traffic.json
+#   pmcpy:SCRIPT[,ARGS]  FETCH_SIZE and WRITE_SIZE passes of python tools/SCRIPT ARGS
 #   py:SCRIPT[,ARGS]     python tools/SCRIPT ARGS (diagnostics, tuning sweeps; limit PY_SECS, 420)
 #   rocpy:SCRIPT[,ARGS]  the same under rocprofv3 --kernel-trace --stats
 # example: tools/gpu_session.sh r03a tests smoke bench driver rocprof pmc
@@ -74,6 +75,12 @@ for st in "$@"; do
                python3 tools/pmc_traffic.py "$OUT/${nm}_FETCH_SIZE/run_counter_collection.csv" \
                  "$OUT/${nm}_WRITE_SIZE/run_counter_collection.csv" --n "$pn" --medium "$pm" \
                  --stencil "$ps" --merge "$OUT/pmc_traffic.json" || true
+             done ;;
+    pmcpy)   # FETCH_SIZE / WRITE_SIZE passes (one rocprofv3 --pmc run each) of tools/SCRIPT ARGS
+             name="pmcpy_$(slug "$arg")"
+             for ctr in FETCH_SIZE WRITE_SIZE; do
+               run "${name}_$ctr" 300 rocprofv3 --pmc $ctr -d "$OUT/${name}_$ctr" -o run \
+                 --output-format csv -- python3 "tools/${A[0]}" "${A[@]:1}"
              done ;;
     py)      run "py_$(slug "$arg")" "${PY_SECS:-420}" python "tools/${A[0]}" "${A[@]:1}" ;;
     rocpy)   name="rocpy_$(slug "$arg")"
