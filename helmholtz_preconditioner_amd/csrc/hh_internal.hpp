@@ -230,6 +230,7 @@ struct FusedArgs {
   const int* stop;
 };
 constexpr int kFusedMaxK = 20;  // K <= this (restart <= kFusedMaxK + 1)
+constexpr int kFusedKeepDefault = 8;  // basis re-reads served from LDS (HH_FUSED_KEEP: 0, 4, 8)
 int fused_iter_rows(int n);
 int fused_iter_blocks(int n, int rows);
 void launch_fused_iter(int K, const FusedArgs& a, int blocks, hipStream_t stream);

@@ -589,8 +589,11 @@ bool krylov_rev() {
 // r + 1 (w_{K-1} and the K basis vectors of that row: the iteration's only HBM read of them),
 // applies the stencil (+ Jacobi) to row r from a three-row register ring (W/E neighbours through
 // a double-buffered LDS row; the strip's two edge columns' u_K formed by the edge waves from
-// broadcast loads), stores u_K and w_K of row r and adds row r's <u_k, w_K> -- the u_k re-read,
-// one row after the first read, from L2.  The band's two halo rows of u_K are formed, never
+// broadcast loads), stores u_K and w_K of row r and adds row r's <u_k, w_K> -- the u_k re-read
+// one row after the first read: the first KEEP of them from a two-row LDS copy each thread made
+// of its own column (no barrier: the same lane writes and reads), the rest from the memory
+// system (at 8192^2 the re-reads miss the L2: PMC FETCH ~2x the algorithmic reads,
+// profiles/r03zc/).  The band's two halo rows of u_K are formed, never
 // stored (each is a neighbouring band's own row): (rows + 2) / rows of the basis rows are read.
 // Tiles are dealt to XCDs in contiguous runs (block b -> XCD b % 8), so a band's halo rows are
 // mostly read on the XCD that owns them.  Arithmetic per point: update_kernel's coefficient
@@ -606,11 +609,14 @@ __device__ __forceinline__ double2 csel(bool c, double2 a, double2 b) {
   return make_double2(c ? a.x : b.x, c ? a.y : b.y);
 }
 
-template <int K, bool CONSTC>
+template <int K, bool CONSTC, int KEEP>
 __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
   if (a.stop && *a.stop) return;
+  constexpr int KL = KEEP < K ? KEEP : K;  // (<= the update's batch of 8: its first batch)
+  static_assert(KL <= 8, "kept vectors come from the update's first batch");
   __shared__ double2 coef[K];
   __shared__ double2 urow[2][kT + 2];
+  __shared__ double2 vkeep[KL > 0 ? 2 : 1][KL > 0 ? KL : 1][kT];  // [row & 1][k][lane]
   const int n = a.n, R = a.rows;
   const int tiles_x = (n + kT - 1) / kT, bands = (n + R - 1) / R, T = tiles_x * bands;
   const int per_xcd = (T + 7) / 8;
@@ -639,7 +645,7 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
   // per-vector addresses become loop-invariant / strength-reduced registers (4 + 2-6 VGPRs per
   // basis vector otherwise, i.e. one wave per SIMD at K >= 11)
   int kz = 0;
-  auto unew = [&](int r, int col) {
+  auto unew = [&](int r, int col, bool keep) {
     __builtin_amdgcn_sched_barrier(0);  // (calls and batches do not interleave: registers)
     const size_t p = (size_t)min(max(r, 0), n - 1) * n + col;
     double2 w = a.win[p];
@@ -651,6 +657,10 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
       double2 v[kB];
 #pragma unroll
       for (int q = 0; q < kB; ++q) v[q] = a.V[(size_t)min(k0 + q, K - 1) * a.ldv + p];
+      if (KL > 0 && keep && k0 == 0) {
+#pragma unroll
+        for (int q = 0; q < KL; ++q) vkeep[r & 1][q][threadIdx.x] = v[q];
+      }
 #pragma unroll
       for (int q = 0; q < kB; ++q)
         if (k0 + q < K) w = csub(w, cmul(coef[k0 + q + kz], v[q]));
@@ -678,12 +688,12 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
   for (int k = 0; k <= K; ++k) acc[k] = z;
   double nw = 0.0, nu = 0.0;
   if (live) {
-    double2 uS = unew(rb - 1, ic), uC = unew(rb, ic);
+    double2 uS = unew(rb - 1, ic, false), uC = unew(rb, ic, true);
     int buf = 0;
     for (int r0 = rb; r0 < re; ++r0) {
       int r = r0;
       asm volatile("" : "+s"(r), "+s"(kz));
-      const double2 uN = unew(r + 1, ic);
+      const double2 uN = unew(r + 1, ic, true);
       double2 ue = z;
       if (ew || ee) ue = unew1(r, ie);  // (wave-uniform: the two edge waves only)
       urow[buf][1 + t] = csel(act, uC, z);
@@ -721,7 +731,9 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
       for (int k0 = 0; k0 < K; k0 += 8) {
         double2 v[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = a.V[(size_t)min(k0 + q, K - 1) * a.ldv + p];
+        for (int q = 0; q < 8; ++q)
+          v[q] = k0 + q < KL ? vkeep[r & 1][k0 + q][t]
+                             : a.V[(size_t)min(k0 + q, K - 1) * a.ldv + p];
 #pragma unroll
         for (int q = 0; q < 8; ++q)
           if (k0 + q < K) acc[k0 + q] = cfma_conj(v[q], w, acc[k0 + q]);
@@ -975,6 +987,12 @@ __global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
   block_reduce_vec<2 * (K + 1) + 2>(v, a.partials, 2 * (K + 1) + 2);
 }
 
+// basis vectors whose re-read comes from the LDS copy (HH_FUSED_KEEP: 0, 4 or 8; read per
+// launch so one process can A/B it)
+int fused_keep() {
+  const char* e = std::getenv("HH_FUSED_KEEP");
+  return e ? std::atoi(e) : kFusedKeepDefault;
+}
 template <int K>
 void fused_launch(const FusedArgs& a, int blocks, hipStream_t s) {
   if (a.sl) {
@@ -984,10 +1002,23 @@ void fused_launch(const FusedArgs& a, int blocks, hipStream_t s) {
       hipLaunchKernelGGL((fused_sl_iter_kernel<K, true>), dim3(blocks), dim3(kT), 0, s, a);
     return;
   }
-  if (a.invc2)
-    hipLaunchKernelGGL((fused_iter_kernel<K, false>), dim3(blocks), dim3(kT), 0, s, a);
-  else
-    hipLaunchKernelGGL((fused_iter_kernel<K, true>), dim3(blocks), dim3(kT), 0, s, a);
+  const int keep = fused_keep();
+  if (keep >= 8) {
+    if (a.invc2)
+      hipLaunchKernelGGL((fused_iter_kernel<K, false, 8>), dim3(blocks), dim3(kT), 0, s, a);
+    else
+      hipLaunchKernelGGL((fused_iter_kernel<K, true, 8>), dim3(blocks), dim3(kT), 0, s, a);
+  } else if (keep >= 4) {
+    if (a.invc2)
+      hipLaunchKernelGGL((fused_iter_kernel<K, false, 4>), dim3(blocks), dim3(kT), 0, s, a);
+    else
+      hipLaunchKernelGGL((fused_iter_kernel<K, true, 4>), dim3(blocks), dim3(kT), 0, s, a);
+  } else {
+    if (a.invc2)
+      hipLaunchKernelGGL((fused_iter_kernel<K, false, 0>), dim3(blocks), dim3(kT), 0, s, a);
+    else
+      hipLaunchKernelGGL((fused_iter_kernel<K, true, 0>), dim3(blocks), dim3(kT), 0, s, a);
+  }
 }
 template <int... Ks>
 struct FTable {

@@ -213,3 +213,28 @@ def test_fused_pass_is_the_single_rank_default(ctx):
     H.gmres(A, f, rtol=1e-12, restart=20, maxiter=3, M=H.ShiftedLaplace(A, sweeps=3))
     assert A.last_solve_path() == "regular"
     A.krylov_mode("auto")
+
+
+@pytest.mark.parametrize("n,kind", [(300, "c1"), (1100, "marmousi")])
+def test_fused_pass_lds_kept_basis_is_bit_identical(ctx, n, kind, monkeypatch):
+    """HH_FUSED_KEEP (read per launch): the projections' re-read of the first 0 / 4 / 8 basis
+    vectors from the pass's own LDS copy instead of the memory system reads the same values in
+    the same order -- histories and fields bit-identical (K up to 20: the kept and re-read
+    vectors mixed in one pass)"""
+    om, h, eta = O.problem_params(n, 12, n / 40.0, 2.0)
+    cm = medium(kind, n) if kind != "marmousi" else H.marmousi_like_c_mat(n)
+    A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, context=ctx)
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    A.krylov_mode("fused")
+    out = []
+    for keep in ("0", "4", "8"):
+        monkeypatch.setenv("HH_FUSED_KEEP", keep)
+        hist = []
+        x, info = H.gmres(A, f, rtol=1e-12, restart=21, maxiter=25, M="jacobi",
+                          callback=hist.append, callback_type='legacy')
+        assert A.last_solve_path() == "one-pass"
+        out.append((x, np.array(hist)))
+    A.krylov_mode("auto")
+    for x, hh in out[1:]:
+        assert np.array_equal(hh, out[0][1])
+        assert np.array_equal(x, out[0][0])
