@@ -326,6 +326,29 @@ def gmres_bytes(args, its, bpp, N):
     return sum((bpp + pre) * N + 16 * (j + 2) * N + 16 * (j + 3) * N for j in js), fused
 
 
+def gmres_path_bytes(args, its, bpp, N, path):
+    """algorithmic bytes of `its` inner iterations on the path the solve actually ran, per
+    unknown: the one-pass iteration moves, at iteration j of a cycle, j = 0: the
+    cycle's first M A (bpp) + its projection (u_0, w_0: 32 B); j >= 1: ONE pass, w_{j-1} and
+    the j basis vectors read, u_j and w_j written -- 16 (j + 3) B, + 8 B of 1/c^2 for a
+    non-constant medium (the operator's bpp is 32 + 8 then) --; the cycle's last update adds
+    16 (R + 1) B.  The regular and lagged cycles move the CGS bytes of gmres_bytes (the SpMV,
+    then the basis twice).  Per-cycle extras (x update, residual) are left out of both, as in
+    gmres_bytes.  (PMC counters cannot run inside the timed solve: the pass's measured
+    traffic per K is in profiles/r04_pmc_fused.json.)"""
+    if path != "one-pass":
+        return gmres_bytes(args, its, bpp, N)[0]
+    R = args.restart
+    ic = bpp - 32 if args.stencil == 5 else 0
+    total = 0.0
+    for i in range(its):
+        j = i % R
+        total += (bpp + 32) * N if j == 0 else (16 * (j + 3) + ic) * N
+        if j == R - 1:
+            total += 16 * (R + 1) * N
+    return total
+
+
 def span_breakdown(H, A, ctx, args, its, f_host, R, applies=20):
     """Where an N-rank apply / GMRES iteration spends its time, per rank (diagnostic, after
     the timed legs, so the timed numbers carry no event overhead): HIP events around the halo
@@ -485,11 +508,17 @@ def main():
                               f"{', fused with the SpMV' if fused else ''})",
                         "jacobi": "Jacobi", "none": "none"}[args.precond],
             "ms_per_iter": round(tg * 1e3 / its, 4),
+            # the CGS-minimal bytes of SURVEY 8d (SpMV + the basis streamed twice) per second: a
+            # credit for the work, NOT a roofline fraction -- the one-pass path moves ~half of
+            # these bytes, so on that path this can approach or pass the HBM peak
             "algorithmic_GBps": round(gbytes / tg / 1e9, 1),
+            # the bytes the path it ran actually has to move (gmres_path_bytes) per second: the
+            # rate to hold against the 8 TB/s peak
+            "pass_GBps": round(gmres_path_bytes(args, its, bpp, float(n) * n,
+                                                A.last_solve_path()) / tg / 1e9, 1),
             "final_rel_presid": float(hist[-1]) if its else None,
             # cycle form (hh_op_last_solve_path): "one-pass" = update + next M A + projections in
-            # one pass over the basis (krylov.hip fused_iter_kernel; the bytes counted above stay
-            # the CGS-minimal formula of SURVEY 8d, which that pass moves ~half of)
+            # one pass over the basis (fused.hip fused_iter_kernel)
             "solve_path": A.last_solve_path(),
         }
 

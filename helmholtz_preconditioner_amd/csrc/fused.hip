@@ -1,0 +1,637 @@
+// One pass over the Krylov basis per GMRES inner iteration (`hh_op_set_krylov_mode`
+// 3): the update of iteration K-1 of the lagged-normalisation iteration (krylov.hip
+// gmres_lag_kernel), the next M A and the next projections in ONE streaming kernel.
+//
+// Replaces, per inner iteration of scipy.sparse.linalg.gmres (scipy 1.15.3
+// _isolve/iterative.py:748-800, which code.py:516 runs): the axpy loop of the orthogonalisation,
+// the psolve(matvec(v)) of the next iteration (code.py:510-516: A @ x and the M slot) and the
+// np.vdot projections of the next iteration -- three sweeps over the basis and the grid in one.
+//
+// A 256-thread block marches a 256-column strip of a band of rows.  Per row r it forms u_K on
+// row r + 1 (w_{K-1} and the K basis rows: the iteration's only HBM read of them), applies the
+// stencil (+ M) to row r from a three-row register ring (W/E neighbours through a
+// double-buffered LDS row; the strip's two edge columns' u_K formed by the two edge waves,
+// lane-parallel), stores u_K and w_K of row r and adds row r's <u_k, w_K>.  The projections
+// need the basis row r one step after the update read it: the first KEEP vectors come from a
+// one-row LDS copy of the thread's own column (written after row r's projections from the
+// registers that held row r + 1 since its load -- the same lane writes and reads, so no
+// barrier), the rest from the memory system.  A band re-forms its halo rows of u_K (never
+// stored: each is a neighbouring band's own row); across slabs of one rank it forms them in
+// place (FROW_MEM), across ranks it reads the neighbour's rows from the halo exchange
+// (FROW_HALO, formed by fused_edge_kernel before the exchange).  Tiles are dealt to XCDs in
+// contiguous runs (block b -> XCD b % 8), so a band's halo rows are mostly read on the XCD that
+// owns them.  Arithmetic per point: update_kernel's coefficient and term order, stencil.hip's
+// operator; only the inner products' summation order differs from the separate launches, and
+// the strip edge columns' u_K (halo values, summed by a shuffle tree) agree with the stored u_K
+// (k order) to rounding.
+#include <algorithm>
+#include <cstddef>
+#include <cstdlib>
+
+#include "hh_internal.hpp"
+#include "hh_complex.hpp"
+#include "hh_wave.hpp"
+
+namespace hh {
+namespace {
+
+constexpr int kT = 256;  // threads per block = columns per strip
+
+struct double2x2 {
+  double2 a, b;
+};
+__device__ __forceinline__ double2x2 make_double2x2(double2 a, double2 b) { return {a, b}; }
+
+// by-value select (a select of lvalues would become a select of addresses)
+__device__ __forceinline__ double2 csel(bool c, double2 a, double2 b) {
+  return make_double2(c ? a.x : b.x, c ? a.y : b.y);
+}
+
+// Global-address-space views: a row pointer made opaque to the optimiser (asm "+s", so neither
+// per-vector address registers nor strength-reduced pointers appear) must stay a GLOBAL pointer,
+// or every load through it becomes a flat load with a 64-bit VGPR address.
+typedef double d2v __attribute__((ext_vector_type(2)));
+using gd2 = const __attribute__((address_space(1))) d2v;
+__device__ __forceinline__ gd2* gptr(const double2* p) { return (gd2*)p; }
+// *(row + byte offset): `row` uniform (scalar registers), `boff` the lane's 32-bit byte offset --
+// the global_load saddr form: one VGPR of address for every vector of a row instead of a 64-bit
+// address per vector
+__device__ __forceinline__ double2 ld_at(gd2* row, unsigned boff) {
+  using gc = const __attribute__((address_space(1))) char;
+  const d2v v = *(gd2*)((gc*)row + boff);
+  return make_double2(v.x, v.y);
+}
+
+// The band of this block: tiles dealt to XCDs in contiguous runs.
+struct Band {
+  bool live;
+  int tx, rb, re;
+};
+__device__ __forceinline__ Band band_of(const FusedArgs& a) {
+  const int tiles_x = (a.n + kT - 1) / kT, T = tiles_x * a.bands;
+  const int per_xcd = (T + 7) / 8;
+  const int tile = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+  Band b;
+  b.live = tile < T;
+  b.tx = b.live ? tile % tiles_x : 0;
+  const int ty = b.live ? tile / tiles_x : 0;
+  const int step = a.row_step > 0 ? a.row_step : a.rows;
+  b.rb = a.row_begin + ty * step;
+  b.re = min(b.rb + a.rows, a.row_end);
+  return b;
+}
+
+// u_K at row r (uniform), column col, given the value formed from the (clamped) row: rows inside
+// [rlo, rhi) are formed from memory; the others are zero (FROW_ZERO) or the neighbour rank's
+// received rows (FROW_HALO; H halo rows per side)
+template <int H>
+__device__ __forceinline__ double2 row_value(const FusedArgs& a, int rlo, int rhi, int r, int col,
+                                             double2 formed) {
+  if (r >= rlo && r < rhi) return formed;
+  if (r < 0)
+    return a.lo_mode == FROW_HALO ? a.halo_lo[(size_t)(r + H) * a.n + col] : make_double2(0.0, 0.0);
+  return a.hi_mode == FROW_HALO ? a.halo_hi[(size_t)(r - a.nl) * a.n + col] : make_double2(0.0, 0.0);
+}
+
+template <int K>
+__device__ __forceinline__ void load_coef(const FusedArgs& a, double2* coef) {
+  const int t = threadIdx.x;
+  if (t < K) {
+    const double sk = a.vscale[t];
+    const double2 hk = cscale(make_double2(a.raw[2 * t], a.raw[2 * t + 1]), sk);
+    coef[t] = cscale(hk, sk);
+  }
+}
+
+// ------------------------------------------------------------------ M = none / Jacobi
+template <int K, bool CONSTC, int KEEP>
+__global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
+  if (a.stop && *a.stop) return;
+  constexpr int KL = KEEP < K ? KEEP : K;  // kept (LDS-served) projection re-reads
+  constexpr int kB = KL > 0 ? 4 : 8;       // batch of the remaining vectors' loads
+  __shared__ double2 coef[K];
+  __shared__ double2 urow[2][kT + 2];
+  __shared__ double2 vkeep[KL > 0 ? KL : 1][kT];  // basis row r, k < KL, [k][lane]
+  const int n = a.n, nl = a.nl;
+  const Band bd = band_of(a);
+  const int t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
+  const int i0 = bd.tx * kT, i = i0 + t;
+  const bool act = i < n;
+  const int ic = min(i, n - 1);
+  const int rb = bd.rb, re = bd.re;
+  // rows whose u_K is formed from memory: the slab, and the neighbouring slab's row on a
+  // FROW_MEM side
+  const int rlo = a.lo_mode == FROW_MEM ? -1 : 0, rhi = a.hi_mode == FROW_MEM ? nl + 1 : nl;
+  // the strip's edge columns: wave 0 forms u_K at i0 - 1, the last wave at i0 + kT
+  const bool ew = wv == 0, ee = wv == kT / kWave - 1;
+  const int ie = min(max(ew ? i0 - 1 : i0 + kT, 0), n - 1);
+  const bool ehas = (ew && i0 > 0) || (ee && i0 + kT < n);
+  load_coef<K>(a, coef);
+  __syncthreads();
+  const double sin = *a.sin;
+  const double2 z = make_double2(0.0, 0.0);
+  // kz: an opaque zero redefined every row, so neither the coefficients' LDS reads nor the
+  // per-vector addresses become loop-invariant / strength-reduced registers (4 + 2-6 VGPRs per
+  // basis vector otherwise)
+  int kz = 0;
+  // basis row r + 1 of the first KL vectors, held from the update's load until row r's
+  // projections are done, then copied to vkeep for row r + 1's projections
+  double2 hold[KL > 0 ? KL : 1];
+  // u_K at (r, col): w_{K-1} - sum_k c_k u_k in k order; the first KL loads issued together
+  // (one memory round trip), the rest in batches of kB in a runtime loop (a fully unrolled
+  // loop keeps ~16 VGPRs per vector live)
+  // (addresses: a row pointer + k ldv, uniform -- scalar registers --, plus the lane's 32-bit
+  // column offset: one VGPR for all K loads instead of a 64-bit address per vector)
+  auto unew = [&](int r, unsigned col) {
+    __builtin_amdgcn_sched_barrier(0);  // (calls and batches do not interleave: registers)
+    const int rc = min(max(r, rlo), rhi - 1);
+    gd2* vrow = gptr(a.V + (ptrdiff_t)rc * n);
+    gd2* wrow = gptr(a.win + (ptrdiff_t)rc * n);
+    // (opaque scalar row pointers: no per-vector strength-reduced address registers)
+    asm volatile("" : "+s"(vrow), "+s"(wrow));
+    const unsigned bo = col * (unsigned)sizeof(double2);
+    double2 w = ld_at(wrow, bo);
+    if constexpr (KL > 0) {
+#pragma unroll
+      for (int q = 0; q < KL; ++q) hold[q] = ld_at(vrow + (size_t)q * a.ldv, bo);
+      // (the coefficients' LDS reads in batches of 4: all KL in flight would hold 4 KL VGPRs
+      // next to the held row and the accumulators)
+#pragma unroll
+      for (int q0 = 0; q0 < KL; q0 += 4) {
+        double2 c[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c[q] = coef[min(q0 + q, KL - 1) + kz];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (q0 + q < KL) w = csub(w, cmul(c[q], hold[q0 + q]));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll 1
+    for (int k0 = KL; k0 < K; k0 += kB) {
+      double2 v[kB];
+#pragma unroll
+      for (int q = 0; q < kB; ++q) v[q] = ld_at(vrow + (size_t)min(k0 + q, K - 1) * a.ldv, bo);
+#pragma unroll
+      for (int q = 0; q < kB; ++q)
+        if (k0 + q < K) w = csub(w, cmul(coef[k0 + q + kz], v[q]));
+    }
+    // (w complete here: the update must not sink into row_value's branch, where its operands
+    // -- the held row and every coefficient -- would all be live at once)
+    asm volatile("" : "+v"(w.x), "+v"(w.y));
+    return row_value<1>(a, rlo, rhi, r, col, w);
+  };
+  // u_K at one point, lane-parallel (the edge waves: lane k of each half takes the term
+  // c_k u_k, summed by shuffles -- one load round trip instead of ceil(K / kB) batches)
+  auto unew1 = [&](int r, int c) {
+    const int k = lane & 31;
+    const int rc = min(max(r, rlo), rhi - 1);
+    const ptrdiff_t p = (ptrdiff_t)rc * n + c;
+    const double2 wv = a.win[p];
+    const double2 vk = (a.V + p)[(size_t)min(k, K - 1) * a.ldv];
+    double2 tk = csel(k < K, cmul(coef[min(k, K - 1)], vk), z);
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) {
+      tk.x += __shfl_xor(tk.x, off);
+      tk.y += __shfl_xor(tk.y, off);
+    }
+    return row_value<1>(a, rlo, rhi, r, c, csub(wv, tk));
+  };
+  const double2 AW = a.tab_i[ic], AE = a.tab_i[n + ic], R1 = a.tab_i[2 * n + ic];
+  double2 acc[K + 1];
+#pragma unroll
+  for (int k = 0; k <= K; ++k) acc[k] = z;
+  double nw = 0.0, nu = 0.0;
+  if (bd.live) {
+    double2 uS = unew(rb - 1, (unsigned)ic);
+    double2 uC = unew(rb, (unsigned)ic);
+    if constexpr (KL > 0) {
+#pragma unroll
+      for (int q = 0; q < KL; ++q) vkeep[q][t] = hold[q];
+    }
+    int buf = 0;
+    for (int r0 = rb; r0 < re; ++r0) {
+      int r = r0;
+      asm volatile("" : "+s"(r), "+s"(kz));
+      const double2 uN = unew(r + 1, (unsigned)ic);
+      double2 ue = z;
+      if (ew || ee) ue = unew1(r, ie);  // (wave-uniform: the two edge waves only)
+      urow[buf][1 + t] = csel(act, uC, z);
+      if (ew && lane == 0) urow[buf][0] = csel(ehas, ue, z);
+      if (ee && lane == kWave - 1) urow[buf][kT + 1] = csel(ehas, ue, z);
+      __syncthreads();
+      const double2 uW = urow[buf][t], uE = urow[buf][t + 2];
+      const double* q = reinterpret_cast<const double*>(a.tab_j) + 8 * (size_t)r;
+      const double2 R2 = make_double2(q[0], q[1]), BS = make_double2(q[2], q[3]);
+      const double2 BN = make_double2(q[4], q[5]), OM = make_double2(q[6], q[7]);
+      const size_t p = (size_t)r * n + ic;
+      const double icv = CONSTC ? a.invc2_const : a.invc2[p];
+      const double2 W = cmul(AW, R2);
+      const double2 E = cmul(AE, R2);
+      const double2 S = cmul(BS, R1);
+      const double2 N = cmul(BN, R1);
+      const double2 M = cscale(cmul(OM, R1), icv);
+      const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
+      const double2 D = csub(M, sum4);
+      double2 Au = cmul(S, uS);
+      Au = cfma(W, uW, Au);
+      Au = cfma(D, uC, Au);
+      Au = cfma(E, uE, Au);
+      Au = cfma(N, uN, Au);
+      const double2 w = csel(act, a.jac ? cscale(cdiv(Au, D), sin) : cscale(Au, sin), z);
+      if (act) {
+        a.wout[p] = w;
+        a.uout[p] = uC;
+      }
+      const double2 uo = csel(act, uC, z);
+      nu = fma(uo.x, uo.x, fma(uo.y, uo.y, nu));
+      nw = fma(w.x, w.x, fma(w.y, w.y, nw));
+      if constexpr (KL > 0) {
+        // (in batches of 4: all KL LDS reads in flight at once would hold 4 KL more VGPRs next
+        // to the held row and the accumulators)
+#pragma unroll
+        for (int k0 = 0; k0 < KL; k0 += 4) {
+          double2 v[4];
+#pragma unroll
+          for (int q2 = 0; q2 < 4; ++q2) v[q2] = vkeep[min(k0 + q2, KL - 1)][t];
+#pragma unroll
+          for (int q2 = 0; q2 < 4; ++q2)
+            if (k0 + q2 < KL) acc[k0 + q2] = cfma_conj(v[q2], w, acc[k0 + q2]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      // the remaining re-reads from the memory system, kB in flight
+      gd2* vr = gptr(a.V + (size_t)r * n);
+      asm volatile("" : "+s"(vr));
+#pragma unroll
+      for (int k0 = KL; k0 < K; k0 += kB) {
+        double2 v[kB];
+#pragma unroll
+        for (int q2 = 0; q2 < kB; ++q2)
+          v[q2] = ld_at(vr + (size_t)min(k0 + q2, K - 1) * a.ldv, (unsigned)ic * 16u);
+#pragma unroll
+        for (int q2 = 0; q2 < kB; ++q2)
+          if (k0 + q2 < K) acc[k0 + q2] = cfma_conj(v[q2], w, acc[k0 + q2]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      acc[K] = cfma_conj(uo, w, acc[K]);
+      if constexpr (KL > 0) {  // (row r + 1's basis for the next step's projections)
+#pragma unroll
+        for (int q2 = 0; q2 < KL; ++q2) vkeep[q2][t] = hold[q2];
+      }
+      uS = uC;
+      uC = uN;
+      buf ^= 1;
+    }
+  }
+  // one partial row: the K + 1 dots, |w_K|^2, then |u_K|^2 -- one reduce launch lands the last
+  // exactly where gmres_lag_kernel reads sigma_K^2 (red + 16 + 2 (K + 1) + 1)
+  double v[2 * (K + 1) + 2];
+#pragma unroll
+  for (int k = 0; k <= K; ++k) {
+    v[2 * k] = acc[k].x;
+    v[2 * k + 1] = acc[k].y;
+  }
+  v[2 * (K + 1)] = nw;
+  v[2 * (K + 1) + 1] = nu;
+  block_reduce_vec<2 * (K + 1) + 2>(v, a.partials, 2 * (K + 1) + 2);
+}
+
+// ------------------------------------------------------- M = two-sweep shifted Laplace
+// The same pass with M = the two-sweep shifted-Laplace smoother (stencil.hip EPI_SL_FIRST then
+// EPI_SL_SWEEP): T = s A u, z1 = damp T / D_beta, w = z1 + damp (T - A_beta z1) / D_beta.
+// Output row r needs z1 on rows r-1 .. r+1, i.e. u_K on rows r-2 .. r+2 and on two columns
+// beyond the strip on each side: per step L the block forms u_K on row L (own columns; the
+// edge waves also on the edge column and, one row behind, the outer column), T and z1 on row
+// L-1 (own columns; the edge waves on the edge column) and w on row L-2 -- rings of three u,
+// two T and three z1 rows, W/E neighbours of u (row L-1) and z1 (row L-2) through two
+// double-buffered LDS rows.  Rows and columns off the grid are zero for u, T and z1 alike
+// (the two-launch path's Dirichlet neighbours); the slab's tables hold rows -2 .. nl+1 and
+// invc2_halo the medium of rows -2, -1, nl, nl+1.
+template <int K, bool CONSTC>
+__global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
+  if (a.stop && *a.stop) return;
+  __shared__ double2 coef[K];
+  __shared__ double2 urow[2][kT + 2], zrow[2][kT + 2];
+  const int n = a.n, nl = a.nl;
+  const Band bd = band_of(a);
+  const int t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
+  const int i0 = bd.tx * kT, i = i0 + t;
+  const bool act = i < n;
+  const int ic = min(i, n - 1);
+  const int rb = bd.rb, re = bd.re;
+  const int rlo = a.lo_mode == FROW_MEM ? -2 : 0, rhi = a.hi_mode == FROW_MEM ? nl + 2 : nl;
+  // edge waves: wave 0 the W edge column i0-1 (outer i0-2, inner i0 = LDS slot 1), the last
+  // wave the E edge column i0+kT (outer i0+kT+1, inner i0+kT-1 = LDS slot kT)
+  const bool ew = wv == 0, ee = wv == kT / kWave - 1;
+  const int ie_raw = ew ? i0 - 1 : i0 + kT, io_raw = ew ? i0 - 2 : i0 + kT + 1;
+  const bool ehas = (ew || ee) && ie_raw >= 0 && ie_raw < n;
+  const bool ohas = (ew || ee) && io_raw >= 0 && io_raw < n;
+  const int ie = min(max(ie_raw, 0), n - 1), io = min(max(io_raw, 0), n - 1);
+  const int islot = ew ? 1 : kT;  // LDS slot of the edge column's inner neighbour
+  load_coef<K>(a, coef);
+  __syncthreads();
+  const double sin = *a.sin;
+  const double damp = a.damping;
+  const double2 mshift = a.mshift;
+  const double2 z = make_double2(0.0, 0.0);
+  int kz = 0;
+  auto unew = [&](int r, int col) {
+    __builtin_amdgcn_sched_barrier(0);
+    const int rc = min(max(r, rlo), rhi - 1);
+    const ptrdiff_t p = (ptrdiff_t)rc * n + col;
+    const double2* vp = a.V + p;
+    double2 w = a.win[p];
+    constexpr int kB = 8;
+#pragma unroll 1
+    for (int k0 = 0; k0 < K; k0 += kB) {
+      double2 v[kB];
+#pragma unroll
+      for (int q = 0; q < kB; ++q) v[q] = vp[(size_t)min(k0 + q, K - 1) * a.ldv];
+#pragma unroll
+      for (int q = 0; q < kB; ++q)
+        if (k0 + q < K) w = csub(w, cmul(coef[k0 + q + kz], v[q]));
+    }
+    return row_value<2>(a, rlo, rhi, r, col, w);
+  };
+  // u_K at two points at once, lane-parallel (the edge waves): half h of the wave takes point
+  // h, lane k of the half the term c_k u_k, the 32 terms summed by shuffles -- one load round
+  // trip instead of two chains of ceil(K / 8) batches (terms in a tree order: the strip that
+  // owns the column forms it in k order, so halo values agree to rounding)
+  auto unew2 = [&](int r1, int c1, int r2, int c2) {
+    const int h = lane >> 5, k = lane & 31;
+    const int r = h ? r2 : r1, c = h ? c2 : c1;
+    const int rc = min(max(r, rlo), rhi - 1);
+    const ptrdiff_t p = (ptrdiff_t)rc * n + c;
+    const double2 wv = a.win[p];
+    const double2 vk = (a.V + p)[(size_t)min(k, K - 1) * a.ldv];
+    double2 tk = csel(k < K, cmul(coef[min(k, K - 1)], vk), z);
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) {
+      tk.x += __shfl_xor(tk.x, off);
+      tk.y += __shfl_xor(tk.y, off);
+    }
+    const double2 ua = make_double2(__shfl(tk.x, 0), __shfl(tk.y, 0));
+    const double2 ub = make_double2(__shfl(tk.x, 32), __shfl(tk.y, 32));
+    const double2 wa = make_double2(__shfl(wv.x, 0), __shfl(wv.y, 0));
+    const double2 wb = make_double2(__shfl(wv.x, 32), __shfl(wv.y, 32));
+    return make_double2x2(row_value<2>(a, rlo, rhi, r1, c1, csub(wa, ua)),
+                          row_value<2>(a, rlo, rhi, r2, c2, csub(wb, ub)));
+  };
+  // row r of the grid?  (the slab, or a neighbour's row on a side that is not the boundary)
+  auto on_grid = [&](int r) {
+    return (r >= 0 && r < nl) || (r < 0 && a.lo_mode != FROW_ZERO) ||
+           (r >= nl && a.hi_mode != FROW_ZERO);
+  };
+  // the operator's coefficients at (row r, column c): W, E, S, N, D, D_beta (stencil.hip order)
+  struct Co {
+    double2 W, E, S, N, D, Db;
+  };
+  auto coefs = [&](int r, int c, double icv) {
+    const double* q = reinterpret_cast<const double*>(a.tab_j) + 8 * (ptrdiff_t)min(max(r, -2), nl + 1);
+    const double2 R2 = make_double2(q[0], q[1]), BS = make_double2(q[2], q[3]);
+    const double2 BN = make_double2(q[4], q[5]), OM = make_double2(q[6], q[7]);
+    const double2 AW = a.tab_i[c], AE = a.tab_i[n + c], R1 = a.tab_i[2 * n + c];
+    Co o;
+    o.W = cmul(AW, R2);
+    o.E = cmul(AE, R2);
+    o.S = cmul(BS, R1);
+    o.N = cmul(BN, R1);
+    const double2 M = cscale(cmul(OM, R1), icv);
+    const double2 sum4 = cadd(cadd(cadd(o.W, o.E), o.S), o.N);
+    o.D = csub(M, sum4);
+    o.Db = csub(cmul(M, mshift), sum4);
+    return o;
+  };
+  // 1/c^2 at (row r, column c): the slab's rows, or the two rows beyond each side
+  auto icv_at = [&](int r, int c) {
+    if constexpr (CONSTC) {
+      return a.invc2_const;
+    } else {
+      const int rc = min(max(r, -2), nl + 1);
+      const double* row = rc < 0 ? a.invc2_halo + (size_t)(rc + 2) * n
+                                 : (rc >= nl ? a.invc2_halo + (size_t)(rc - nl + 2) * n
+                                             : a.invc2 + (size_t)rc * n);
+      return row[c];
+    }
+  };
+  double2 acc[K + 1];
+#pragma unroll
+  for (int k = 0; k <= K; ++k) acc[k] = z;
+  double nw = 0.0, nu = 0.0;
+  if (bd.live) {
+    // rings (own column): u(L-2), u(L-1); T(L-2); z1(L-3), z1(L-2).  Edge waves: u(L-2, ie),
+    // u(L-1, ie), z1(L-2, ie).
+    double2 uP = z, uC = z, Tm = z, z1a = z, z1b = z;
+    double2 euP = z, euC = z, ez1b = z;
+    // row L-1's shifted diagonal and the reciprocal of its |.|^2 (cdiv's one division), handed
+    // to the second sweep of the next step, whose row it is
+    double2 Dbm = make_double2(1.0, 0.0);
+    double invm = 1.0;
+    int buf = 0;
+    for (int L0 = rb - 2; L0 <= re + 1; ++L0) {
+      int L = L0;
+      asm volatile("" : "+s"(L), "+s"(kz));
+      const double2 uN = unew(L, ic);
+      double2 euN = z, eo = z;
+      if (ew || ee) {  // (wave-uniform)
+        const auto pr = unew2(L, ie, L - 1, io);
+        euN = csel(ehas, pr.a, z);
+        eo = csel(ohas, pr.b, z);
+      }
+      urow[buf][1 + t] = csel(act, uC, z);
+      zrow[buf][1 + t] = csel(act, z1b, z);
+      if (ew && lane == 0) {
+        urow[buf][0] = euC;
+        zrow[buf][0] = ez1b;
+      }
+      if (ee && lane == kWave - 1) {
+        urow[buf][kT + 1] = euC;
+        zrow[buf][kT + 1] = ez1b;
+      }
+      __syncthreads();
+      const double2 uW = urow[buf][t], uE = urow[buf][t + 2];
+      const double2 zW = zrow[buf][t], zE = zrow[buf][t + 2];
+      const bool v1 = on_grid(L - 1);  // row L-1 on the grid
+      // T and z1 on row L-1 (own column)
+      const double ic1 = icv_at(L - 1, ic);
+      const Co c1 = coefs(L - 1, ic, ic1);
+      double2 Au = cmul(c1.S, uP);
+      Au = cfma(c1.W, uW, Au);
+      Au = cfma(c1.D, uC, Au);
+      Au = cfma(c1.E, uE, Au);
+      Au = cfma(c1.N, uN, Au);
+      const double2 T1 = csel(act && v1, cscale(Au, sin), z);
+      const double inv1 = 1.0 / fma(c1.Db.x, c1.Db.x, c1.Db.y * c1.Db.y);
+      auto cdivr = [](double2 x, double2 b, double inv) {  // cdiv with the reciprocal given
+        return make_double2(fma(x.x, b.x, x.y * b.y) * inv, fma(x.y, b.x, -x.x * b.y) * inv);
+      };
+      const double2 z1c = csel(act && v1, cscale(cdivr(T1, c1.Db, inv1), damp), z);
+      // the same at the edge column (edge waves; broadcast values)
+      double2 ez1c = z;
+      if (ew || ee) {
+        const double2 uin = urow[buf][islot];
+        const double2 eW = ew ? eo : uin, eE = ew ? uin : eo;
+        const Co ce = coefs(L - 1, ie, icv_at(L - 1, ie));
+        double2 Ae = cmul(ce.S, euP);
+        Ae = cfma(ce.W, eW, Ae);
+        Ae = cfma(ce.D, euC, Ae);
+        Ae = cfma(ce.E, eE, Ae);
+        Ae = cfma(ce.N, euN, Ae);
+        const double2 eT = cscale(Ae, sin);
+        ez1c = csel(ehas && v1, cscale(cdiv(eT, ce.Db), damp), z);
+      }
+      // w on row r = L-2: the second sweep (A_beta on z1)
+      const int r = L - 2;
+      if (r >= rb && r < re) {  // (block-uniform)
+        const size_t p = (size_t)r * n + ic;
+        // row r's W, E, S, N (no mass term: its D_beta and reciprocal come from the last step)
+        const double* q = reinterpret_cast<const double*>(a.tab_j) + 8 * (size_t)r;
+        const double2 R2 = make_double2(q[0], q[1]), BS = make_double2(q[2], q[3]);
+        const double2 BN = make_double2(q[4], q[5]);
+        const double2 AW = a.tab_i[ic], AE = a.tab_i[n + ic], R1 = a.tab_i[2 * n + ic];
+        const double2 W2 = cmul(AW, R2), E2 = cmul(AE, R2), S2 = cmul(BS, R1), N2 = cmul(BN, R1);
+        double2 Az = cmul(S2, z1a);
+        Az = cfma(W2, zW, Az);
+        Az = cfma(Dbm, z1b, Az);
+        Az = cfma(E2, zE, Az);
+        Az = cfma(N2, z1c, Az);
+        const double2 w = csel(act, cadd(z1b, cscale(cdivr(csub(Tm, Az), Dbm, invm), damp)), z);
+        if (act) {
+          a.wout[p] = w;
+          a.uout[p] = uP;
+        }
+        const double2 uo = csel(act, uP, z);
+        nu = fma(uo.x, uo.x, fma(uo.y, uo.y, nu));
+        nw = fma(w.x, w.x, fma(w.y, w.y, nw));
+#pragma unroll
+        for (int k0 = 0; k0 < K; k0 += 8) {
+          double2 v[8];
+#pragma unroll
+          for (int q2 = 0; q2 < 8; ++q2) v[q2] = a.V[(size_t)min(k0 + q2, K - 1) * a.ldv + p];
+#pragma unroll
+          for (int q2 = 0; q2 < 8; ++q2)
+            if (k0 + q2 < K) acc[k0 + q2] = cfma_conj(v[q2], w, acc[k0 + q2]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        acc[K] = cfma_conj(uo, w, acc[K]);
+      }
+      uP = uC;
+      uC = uN;
+      Tm = T1;
+      z1a = z1b;
+      z1b = z1c;
+      euP = euC;
+      euC = euN;
+      ez1b = ez1c;
+      Dbm = c1.Db;
+      invm = inv1;
+      buf ^= 1;
+    }
+  }
+  double v[2 * (K + 1) + 2];
+#pragma unroll
+  for (int k = 0; k <= K; ++k) {
+    v[2 * k] = acc[k].x;
+    v[2 * k + 1] = acc[k].y;
+  }
+  v[2 * (K + 1)] = nw;
+  v[2 * (K + 1) + 1] = nu;
+  block_reduce_vec<2 * (K + 1) + 2>(v, a.partials, 2 * (K + 1) + 2);
+}
+
+// ----------------------------------------------------------------- edge rows (across ranks)
+// u_K on rows [r0, r0 + c0) and [r1, r1 + c1) of the rank-local vectors (a.V, a.win at the
+// rank's first row), written to a.uout: the rows the neighbouring ranks' passes read as their
+// halo.  The pass's own k-order arithmetic (csub(w, cmul(c_k, u_k)), explicit fmas): the value
+// a rank stores for its boundary row and the value its neighbour reads are the same bits.
+template <int K>
+__global__ __launch_bounds__(kT) void fused_edge_kernel(const FusedArgs a, int r0, int c0, int r1) {
+  if (a.stop && *a.stop) return;
+  __shared__ double2 coef[K];
+  load_coef<K>(a, coef);
+  __syncthreads();
+  const int tiles_x = (a.n + kT - 1) / kT;
+  const int row_i = blockIdx.x / tiles_x;
+  const int i = (blockIdx.x % tiles_x) * kT + threadIdx.x;
+  if (i >= a.n) return;
+  const int r = row_i < c0 ? r0 + row_i : r1 + (row_i - c0);
+  const size_t p = (size_t)r * a.n + i;
+  double2 w = a.win[p];
+#pragma unroll
+  for (int k = 0; k < K; ++k) w = csub(w, cmul(coef[k], a.V[(size_t)k * a.ldv + p]));
+  a.uout[p] = w;
+}
+
+// basis vectors whose re-read comes from the LDS copy (HH_FUSED_KEEP = 0 turns the copy off;
+// read per launch so one process can A/B it)
+int fused_keep() {
+  const char* e = std::getenv("HH_FUSED_KEEP");
+  return e ? std::atoi(e) : kFusedKeepDefault;
+}
+template <int K>
+void fused_launch(const FusedArgs& a, int blocks, hipStream_t s) {
+  if (a.sl) {
+    if (a.invc2)
+      hipLaunchKernelGGL((fused_sl_iter_kernel<K, false>), dim3(blocks), dim3(kT), 0, s, a);
+    else
+      hipLaunchKernelGGL((fused_sl_iter_kernel<K, true>), dim3(blocks), dim3(kT), 0, s, a);
+    return;
+  }
+  if (fused_keep() > 0) {
+    if (a.invc2)
+      hipLaunchKernelGGL((fused_iter_kernel<K, false, kFusedKeepDefault>), dim3(blocks), dim3(kT),
+                         0, s, a);
+    else
+      hipLaunchKernelGGL((fused_iter_kernel<K, true, kFusedKeepDefault>), dim3(blocks), dim3(kT),
+                         0, s, a);
+  } else {
+    if (a.invc2)
+      hipLaunchKernelGGL((fused_iter_kernel<K, false, 0>), dim3(blocks), dim3(kT), 0, s, a);
+    else
+      hipLaunchKernelGGL((fused_iter_kernel<K, true, 0>), dim3(blocks), dim3(kT), 0, s, a);
+  }
+}
+template <int K>
+void edge_launch(const FusedArgs& a, int r0, int c0, int r1, int c1, hipStream_t s) {
+  const int tiles_x = (a.n + kT - 1) / kT;
+  hipLaunchKernelGGL((fused_edge_kernel<K>), dim3(tiles_x * (c0 + c1)), dim3(kT), 0, s, a, r0,
+                     c0, r1);
+}
+template <int... Ks>
+struct FTable {
+  using FN = void (*)(const FusedArgs&, int, hipStream_t);
+  using EN = void (*)(const FusedArgs&, int, int, int, int, hipStream_t);
+  static constexpr FN f[] = {fused_launch<Ks>...};
+  static constexpr EN e[] = {edge_launch<Ks>...};
+};
+using FusedTable = FTable<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20>;
+static_assert(kFusedMaxK == 20, "table covers 1..kFusedMaxK");
+
+}  // namespace
+
+// Band height: 8 rows at 1024^2, 32 from 4096^2 (profiles/r03t/r03s_ab_rows*); HH_FUSED_ROWS
+// overrides.  The partial rows (one per block) stay within kMaxStreamBlocks.
+int fused_iter_rows(int n, int rows) {
+  static const int env = [] {
+    const char* e = std::getenv("HH_FUSED_ROWS");
+    return e ? std::atoi(e) : 0;
+  }();
+  const long tiles_x = (n + kT - 1) / kT;
+  int R = env > 0 ? env : (int)std::min<long>(32, std::max<long>(8, tiles_x * n / 1024));
+  while ((long)tiles_x * ((rows + R - 1) / R) > kMaxStreamBlocks) R *= 2;
+  return R;
+}
+int fused_iter_blocks(int n, int bands) {
+  const int T = (n + kT - 1) / kT * bands;
+  return (T + 7) / 8 * 8;
+}
+void launch_fused_iter(int K, const FusedArgs& a, int blocks, hipStream_t stream) {
+  FusedTable::f[K - 1](a, blocks, stream);
+}
+void launch_fused_edge(int K, const FusedArgs& a, int r0, int c0, int r1, int c1,
+                       hipStream_t stream) {
+  if (c0 + c1 > 0) FusedTable::e[K - 1](a, r0, c0, r1, c1, stream);
+}
+
+}  // namespace hh

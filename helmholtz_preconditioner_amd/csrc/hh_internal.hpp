@@ -200,40 +200,61 @@ struct GivensState {
   int* ctrl;          // [0] stop flag of the queued cycle, [1] last column executed
   int restart;
 };
-// One pass over the Krylov basis per lagged GMRES inner iteration (krylov.hip
-// fused_iter_kernel; single rank and slab, 5-point operator, M = none or Jacobi): the update of
-// iteration K-1, u_K = w_{K-1} - sum_{k<K} c_k u_k (c_k = d_k s_k^2 from the raw dots and the
-// basis scales, as update_kernel), written to V + K ldv; then w_K = M A (s_K u_K) into wout;
-// per block ONE partial row (width 2 (K + 1) + 2): <u_k, w_K> for k <= K and |w_K|^2 --
+// One pass over the Krylov basis per lagged GMRES inner iteration (fused.hip
+// fused_iter_kernel; 5-point operator, M = none, Jacobi or the two-sweep shifted Laplace): the
+// update of iteration K-1, u_K = w_{K-1} - sum_{k<K} c_k u_k (c_k = d_k s_k^2 from the raw dots
+// and the basis scales, as update_kernel), written to V + K ldv; then w_K = M A (s_K u_K) into
+// wout; per block ONE partial row (width 2 (K + 1) + 2): <u_k, w_K> for k <= K and |w_K|^2 --
 // multidot_kernel's quantities -- then |u_K|^2.  Every basis vector is read from HBM once per
-// iteration instead of twice.
+// iteration instead of twice.  One launch covers rows [row_begin, row_end) of one slab; the
+// rows just outside the slab (u_K of rows -H .. -1 and nl .. nl+H-1, H = 1, or 2 for the
+// shifted Laplace) come from `lo_mode` / `hi_mode`.
+enum FusedRow : int {
+  FROW_ZERO = 0,  // off the grid: u_K = 0 (homogeneous Dirichlet)
+  FROW_MEM = 1,   // a neighbouring slab of the same rank, contiguous in memory: formed in place
+  FROW_HALO = 2,  // a neighbouring rank's rows of u_K, received into halo_lo / halo_hi
+};
 struct FusedArgs {
-  const double2* V;
+  const double2* V;        // basis, at the slab's first row (negative row offsets: FROW_MEM)
   size_t ldv;
-  const double2* win;      // w_{K-1}
+  const double2* win;      // w_{K-1}, at the slab's first row
   double2* wout;           // w_K
   double2* uout;           // u_K (= V + K ldv)
   const double* raw;       // raw dots d_k (2 K doubles) of w_{K-1}
   const double* vscale;    // s_k, k < K
   const double* sin;       // s_K, the scale of the SpMV input (gmres_lag_kernel's estimate)
   const double2* tab_i;
-  const double2* tab_j;
-  const double* invc2;     // or nullptr (constant medium)
+  const double2* tab_j;    // the slab's rows (shifted Laplace: rows -2 .. nl+1 valid)
+  const double* invc2;     // the slab's [nl][n], or nullptr (constant medium)
   double invc2_const;
-  int n;
-  int rows;                // rows per band (grid: fused_iter_blocks)
+  const double* invc2_halo;  // shifted Laplace: 1/c^2 of rows -2, -1, nl, nl+1 (Slab)
+  int n;                   // row length
+  int nl;                  // rows of the slab
+  int row_begin, row_end;  // rows of this launch
+  int rows;                // rows per band
+  int row_step;            // first-row distance of consecutive bands (0: rows)
+  int bands;               // bands of this launch (grid: fused_iter_blocks)
+  int lo_mode, hi_mode;    // FusedRow of the rows below / above the slab
+  const double2* halo_lo;  // FROW_HALO: u_K of rows -H .. -1, [H][n]
+  const double2* halo_hi;  //            u_K of rows nl .. nl+H-1
   int jac;                 // 1: Jacobi M
   int sl;                  // 1: the two-sweep shifted-Laplace M (fused_sl_iter_kernel)
   double2 mshift;          // SL: mass-term multiplier of A_beta
   double damping;          // SL: damped-Jacobi weight
-  double* partials;
+  double* partials;        // this launch's partial rows
   const int* stop;
 };
 constexpr int kFusedMaxK = 20;  // K <= this (restart <= kFusedMaxK + 1)
-constexpr int kFusedKeepDefault = 8;  // basis re-reads served from LDS (HH_FUSED_KEEP: 0, 4, 8)
-int fused_iter_rows(int n);
-int fused_iter_blocks(int n, int rows);
+// basis vectors whose projection re-read is served from the pass's own LDS copy (HH_FUSED_KEEP:
+// 0 = every re-read from the memory system, for A/B)
+constexpr int kFusedKeepDefault = 17;
+int fused_iter_rows(int n, int rows);  // band height for a slab of `rows` rows
+int fused_iter_blocks(int n, int bands);
 void launch_fused_iter(int K, const FusedArgs& a, int blocks, hipStream_t stream);
+// u_K on rows [r0, r0 + c0) and [r1, r1 + c1) of a.V / a.win (rank-local), written to a.uout:
+// the rows a neighbouring rank's pass reads as its halo (fused_iter_kernel's arithmetic)
+void launch_fused_edge(int K, const FusedArgs& a, int r0, int c0, int r1, int c1,
+                       hipStream_t stream);
 
 // After multidot+update reductions: column `col` of H from raw dots (red_dots, 2*(col+1)
 // doubles + |w|^2 at [2*(col+1)]) and |w_new|^2 (red_norm[0]).  Then scipy's inner-loop

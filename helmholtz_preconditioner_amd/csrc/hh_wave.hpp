@@ -37,4 +37,37 @@ __device__ __forceinline__ double wave_sum_to_63(double v) {
   return v;
 }
 
+// Block-reduce NV doubles held per thread (a 256-thread block); the block's results land in
+// partials[blockIdx.x * width + k].  SC1: stored write-through at device scope (agent-scope
+// relaxed atomic stores), for a last block that reads them in the same launch
+// (MI355X_MICROARCH.md's hand-off form: sc1 stores, drained, then one lane's agent-scope
+// ticket; no L2-writeback fence).
+template <int NV, bool SC1 = false>
+__device__ __forceinline__ void block_reduce_vec(double (&v)[NV], double* partials, int width) {
+  constexpr int kBT = 256;
+  __shared__ double red[NV][kBT / 64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x / 64;
+  // wave sums by DPP lane moves (VALU only; the xor butterfly took 12 dependent ds_bpermute per
+  // value: ~500 LDS permutes per wave for the 41 values of a 20-vector multidot)
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const double x = wave_sum_to_63(v[k]);
+    if (lane == 63) red[k][wave] = x;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < NV; k += kBT) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < kBT / 64; ++w) s += red[k][w];
+    if constexpr (SC1)
+      __hip_atomic_store(
+          (__attribute__((address_space(1))) unsigned long long*)(partials +
+                                                                  (size_t)blockIdx.x * width + k),
+          (unsigned long long)__double_as_longlong(s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      partials[(size_t)blockIdx.x * width + k] = s;
+  }
+}
+
 }  // namespace hh

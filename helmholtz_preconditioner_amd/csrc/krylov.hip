@@ -34,36 +34,6 @@ __device__ __forceinline__ double2 ldnt(const double2* p) {
 using gu64k = __attribute__((address_space(1))) unsigned long long;
 using gu32k = __attribute__((address_space(1))) unsigned;
 
-// Block-reduce NV doubles held per thread; lane results land in partials[blk*width + k].
-// SC1: stored write-through at device scope (agent-scope relaxed atomic stores), for a last
-// block that reads them in the same launch (MI355X_MICROARCH.md's hand-off form: sc1 stores,
-// drained, then one lane's agent-scope ticket; no L2-writeback fence).
-template <int NV, bool SC1 = false>
-__device__ __forceinline__ void block_reduce_vec(double (&v)[NV], double* partials, int width) {
-  __shared__ double red[NV][kT / kWave];
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wave = threadIdx.x / kWave;
-  // wave sums by DPP lane moves (VALU only; the xor butterfly took 12 dependent ds_bpermute per
-  // value: ~500 LDS permutes per wave for the 41 values of a 20-vector multidot)
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const double x = wave_sum_to_63(v[k]);
-    if (lane == kWave - 1) red[k][wave] = x;
-  }
-  __syncthreads();
-  for (int k = threadIdx.x; k < NV; k += kT) {
-    double s = 0.0;
-#pragma unroll
-    for (int w = 0; w < kT / kWave; ++w) s += red[k][w];
-    if constexpr (SC1)
-      __hip_atomic_store((gu64k*)(partials + (size_t)blockIdx.x * width + k),
-                         (unsigned long long)__double_as_longlong(s), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    else
-      partials[(size_t)blockIdx.x * width + k] = s;
-  }
-}
-
 
 template <bool SC1 = false>
 __device__ double wave_reduce_like_block(const double* partials, int count, int width);
@@ -584,450 +554,6 @@ bool krylov_rev() {
   return rev;
 }
 
-// One-pass lagged GMRES iteration (FusedArgs, hh_internal.hpp).  A 256-thread block owns a
-// 256-column strip of a band of `rows` grid rows and marches it: per row r it forms u_K on row
-// r + 1 (w_{K-1} and the K basis vectors of that row: the iteration's only HBM read of them),
-// applies the stencil (+ Jacobi) to row r from a three-row register ring (W/E neighbours through
-// a double-buffered LDS row; the strip's two edge columns' u_K formed by the edge waves from
-// broadcast loads), stores u_K and w_K of row r and adds row r's <u_k, w_K> -- the u_k re-read
-// one row after the first read: the first KEEP of them from a two-row LDS copy each thread made
-// of its own column (no barrier: the same lane writes and reads), the rest from the memory
-// system (at 8192^2 the re-reads miss the L2: PMC FETCH ~2x the algorithmic reads,
-// profiles/r03zc/).  The band's two halo rows of u_K are formed, never
-// stored (each is a neighbouring band's own row): (rows + 2) / rows of the basis rows are read.
-// Tiles are dealt to XCDs in contiguous runs (block b -> XCD b % 8), so a band's halo rows are
-// mostly read on the XCD that owns them.  Arithmetic per point: update_kernel's coefficient
-// and term order, stencil.hip's operator (bit-identical to the three launches it replaces,
-// except the inner products' summation order).
-struct double2x2 {
-  double2 a, b;
-};
-__device__ __forceinline__ double2x2 make_double2x2(double2 a, double2 b) { return {a, b}; }
-
-// by-value select (a select of lvalues would become a select of addresses)
-__device__ __forceinline__ double2 csel(bool c, double2 a, double2 b) {
-  return make_double2(c ? a.x : b.x, c ? a.y : b.y);
-}
-
-template <int K, bool CONSTC, int KEEP>
-__global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
-  if (a.stop && *a.stop) return;
-  constexpr int KL = KEEP < K ? KEEP : K;  // (<= the update's batch of 8: its first batch)
-  static_assert(KL <= 8, "kept vectors come from the update's first batch");
-  __shared__ double2 coef[K];
-  __shared__ double2 urow[2][kT + 2];
-  __shared__ double2 vkeep[KL > 0 ? 2 : 1][KL > 0 ? KL : 1][kT];  // [row & 1][k][lane]
-  const int n = a.n, R = a.rows;
-  const int tiles_x = (n + kT - 1) / kT, bands = (n + R - 1) / R, T = tiles_x * bands;
-  const int per_xcd = (T + 7) / 8;
-  const int tile = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
-  const bool live = tile < T;
-  const int tx = live ? tile % tiles_x : 0, ty = live ? tile / tiles_x : 0;
-  const int t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
-  const int i0 = tx * kT, i = i0 + t;
-  const bool act = i < n;
-  const int ic = min(i, n - 1);
-  const int rb = ty * R, re = min(rb + R, n);
-  // the strip's edge columns: wave 0 forms u_K at i0 - 1, the last wave at i0 + kT
-  const bool ew = wv == 0, ee = wv == kT / kWave - 1;
-  const int ie = min(max(ew ? i0 - 1 : i0 + kT, 0), n - 1);
-  const bool ehas = (ew && i0 > 0) || (ee && i0 + kT < n);
-  if (t < K) {
-    const double sk = a.vscale[t];
-    const double2 hk = cscale(make_double2(a.raw[2 * t], a.raw[2 * t + 1]), sk);
-    coef[t] = cscale(hk, sk);
-  }
-  __syncthreads();
-  const double sin = *a.sin;
-  const double2 z = make_double2(0.0, 0.0);
-  // u_K at (r, col); rows off the grid are zero (loads from clamped rows, selected by value).
-  // kz: an opaque zero redefined every row, so neither the coefficients' LDS reads nor the
-  // per-vector addresses become loop-invariant / strength-reduced registers (4 + 2-6 VGPRs per
-  // basis vector otherwise, i.e. one wave per SIMD at K >= 11)
-  int kz = 0;
-  auto unew = [&](int r, int col, bool keep) {
-    __builtin_amdgcn_sched_barrier(0);  // (calls and batches do not interleave: registers)
-    const size_t p = (size_t)min(max(r, 0), n - 1) * n + col;
-    double2 w = a.win[p];
-    constexpr int kB = 8;
-    // a runtime loop over batches (an unrolled one kept ~16 VGPRs per basis vector live:
-    // one wave per SIMD from K = 11)
-#pragma unroll 1
-    for (int k0 = 0; k0 < K; k0 += kB) {
-      double2 v[kB];
-#pragma unroll
-      for (int q = 0; q < kB; ++q) v[q] = a.V[(size_t)min(k0 + q, K - 1) * a.ldv + p];
-      if (KL > 0 && keep && k0 == 0) {
-#pragma unroll
-        for (int q = 0; q < KL; ++q) vkeep[r & 1][q][threadIdx.x] = v[q];
-      }
-#pragma unroll
-      for (int q = 0; q < kB; ++q)
-        if (k0 + q < K) w = csub(w, cmul(coef[k0 + q + kz], v[q]));
-    }
-    return csel(r >= 0 && r < n, w, z);
-  };
-  // u_K at one point, lane-parallel (the edge waves: lane k of each half takes the term
-  // c_k u_k, summed by shuffles -- one load round trip instead of ceil(K / 8) batches)
-  auto unew1 = [&](int r, int c) {
-    const int k = lane & 31;
-    const size_t p = (size_t)min(max(r, 0), n - 1) * n + c;
-    const double2 wv = a.win[p];
-    const double2 vk = a.V[(size_t)min(k, K - 1) * a.ldv + p];
-    double2 tk = csel(k < K, cmul(coef[min(k, K - 1)], vk), z);
-#pragma unroll
-    for (int off = 16; off > 0; off >>= 1) {
-      tk.x += __shfl_xor(tk.x, off);
-      tk.y += __shfl_xor(tk.y, off);
-    }
-    return csel(r >= 0 && r < n, csub(wv, tk), z);
-  };
-  const double2 AW = a.tab_i[ic], AE = a.tab_i[n + ic], R1 = a.tab_i[2 * n + ic];
-  double2 acc[K + 1];
-#pragma unroll
-  for (int k = 0; k <= K; ++k) acc[k] = z;
-  double nw = 0.0, nu = 0.0;
-  if (live) {
-    double2 uS = unew(rb - 1, ic, false), uC = unew(rb, ic, true);
-    int buf = 0;
-    for (int r0 = rb; r0 < re; ++r0) {
-      int r = r0;
-      asm volatile("" : "+s"(r), "+s"(kz));
-      const double2 uN = unew(r + 1, ic, true);
-      double2 ue = z;
-      if (ew || ee) ue = unew1(r, ie);  // (wave-uniform: the two edge waves only)
-      urow[buf][1 + t] = csel(act, uC, z);
-      if (ew && lane == 0) urow[buf][0] = csel(ehas, ue, z);
-      if (ee && lane == kWave - 1) urow[buf][kT + 1] = csel(ehas, ue, z);
-      __syncthreads();
-      const double2 uW = urow[buf][t], uE = urow[buf][t + 2];
-      const double* q = reinterpret_cast<const double*>(a.tab_j) + 8 * (size_t)r;
-      const double2 R2 = make_double2(q[0], q[1]), BS = make_double2(q[2], q[3]);
-      const double2 BN = make_double2(q[4], q[5]), OM = make_double2(q[6], q[7]);
-      const size_t p = (size_t)r * n + ic;
-      const double icv = CONSTC ? a.invc2_const : a.invc2[p];
-      const double2 W = cmul(AW, R2);
-      const double2 E = cmul(AE, R2);
-      const double2 S = cmul(BS, R1);
-      const double2 N = cmul(BN, R1);
-      const double2 M = cscale(cmul(OM, R1), icv);
-      const double2 sum4 = cadd(cadd(cadd(W, E), S), N);
-      const double2 D = csub(M, sum4);
-      double2 Au = cmul(S, uS);
-      Au = cfma(W, uW, Au);
-      Au = cfma(D, uC, Au);
-      Au = cfma(E, uE, Au);
-      Au = cfma(N, uN, Au);
-      const double2 w = csel(act, a.jac ? cscale(cdiv(Au, D), sin) : cscale(Au, sin), z);
-      if (act) {
-        a.wout[p] = w;
-        a.uout[p] = uC;
-      }
-      const double2 uo = csel(act, uC, z);
-      nu = fma(uo.x, uo.x, fma(uo.y, uo.y, nu));
-      nw = fma(w.x, w.x, fma(w.y, w.y, nw));
-      // (batches of 8 re-reads in flight: all K at once would hold 4 K more VGPRs)
-#pragma unroll
-      for (int k0 = 0; k0 < K; k0 += 8) {
-        double2 v[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-          v[q] = k0 + q < KL ? vkeep[r & 1][k0 + q][t]
-                             : a.V[(size_t)min(k0 + q, K - 1) * a.ldv + p];
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (k0 + q < K) acc[k0 + q] = cfma_conj(v[q], w, acc[k0 + q]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      acc[K] = cfma_conj(uo, w, acc[K]);
-      uS = uC;
-      uC = uN;
-      buf ^= 1;
-    }
-  }
-  // one partial row: the K + 1 dots, |w_K|^2, then |u_K|^2 -- one reduce launch lands the last
-  // exactly where gmres_lag_kernel reads sigma_K^2 (red + 16 + 2 (K + 1) + 1)
-  double v[2 * (K + 1) + 2];
-#pragma unroll
-  for (int k = 0; k <= K; ++k) {
-    v[2 * k] = acc[k].x;
-    v[2 * k + 1] = acc[k].y;
-  }
-  v[2 * (K + 1)] = nw;
-  v[2 * (K + 1) + 1] = nu;
-  block_reduce_vec<2 * (K + 1) + 2>(v, a.partials, 2 * (K + 1) + 2);
-}
-
-// The same pass with M = the two-sweep shifted-Laplace smoother (stencil.hip EPI_SL_FIRST then
-// EPI_SL_SWEEP): T = s A u, z1 = damp T / D_beta, w = z1 + damp (T - A_beta z1) / D_beta.
-// Output row r needs z1 on rows r-1 .. r+1, i.e. u_K on rows r-2 .. r+2 and on two columns
-// beyond the strip on each side: per step L the block forms u_K on row L (own columns; the
-// edge waves also on the edge column and, one row behind, the outer column), T and z1 on row
-// L-1 (own columns; the edge waves on the edge column) and w on row L-2 -- rings of three u,
-// two T and three z1 rows, W/E neighbours of u (row L-1) and z1 (row L-2) through two
-// double-buffered LDS rows.  Rows and columns off the grid are zero for u, T and z1 alike
-// (the two-launch path's Dirichlet neighbours).
-template <int K, bool CONSTC>
-__global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
-  if (a.stop && *a.stop) return;
-  __shared__ double2 coef[K];
-  __shared__ double2 urow[2][kT + 2], zrow[2][kT + 2];
-  const int n = a.n, R = a.rows;
-  const int tiles_x = (n + kT - 1) / kT, bands = (n + R - 1) / R, T_ = tiles_x * bands;
-  const int per_xcd = (T_ + 7) / 8;
-  const int tile = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
-  const bool live = tile < T_;
-  const int tx = live ? tile % tiles_x : 0, ty = live ? tile / tiles_x : 0;
-  const int t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
-  const int i0 = tx * kT, i = i0 + t;
-  const bool act = i < n;
-  const int ic = min(i, n - 1);
-  const int rb = ty * R, re = min(rb + R, n);
-  // edge waves: wave 0 the W edge column i0-1 (outer i0-2, inner i0 = LDS slot 1), the last
-  // wave the E edge column i0+kT (outer i0+kT+1, inner i0+kT-1 = LDS slot kT)
-  const bool ew = wv == 0, ee = wv == kT / kWave - 1;
-  const int ie_raw = ew ? i0 - 1 : i0 + kT, io_raw = ew ? i0 - 2 : i0 + kT + 1;
-  const bool ehas = (ew || ee) && ie_raw >= 0 && ie_raw < n;
-  const bool ohas = (ew || ee) && io_raw >= 0 && io_raw < n;
-  const int ie = min(max(ie_raw, 0), n - 1), io = min(max(io_raw, 0), n - 1);
-  const int islot = ew ? 1 : kT;  // LDS slot of the edge column's inner neighbour
-  if (t < K) {
-    const double sk = a.vscale[t];
-    const double2 hk = cscale(make_double2(a.raw[2 * t], a.raw[2 * t + 1]), sk);
-    coef[t] = cscale(hk, sk);
-  }
-  __syncthreads();
-  const double sin = *a.sin;
-  const double damp = a.damping;
-  const double2 mshift = a.mshift;
-  const double2 z = make_double2(0.0, 0.0);
-  int kz = 0;
-  auto unew = [&](int r, int col) {
-    __builtin_amdgcn_sched_barrier(0);
-    const size_t p = (size_t)min(max(r, 0), n - 1) * n + col;
-    double2 w = a.win[p];
-    constexpr int kB = 8;
-#pragma unroll 1
-    for (int k0 = 0; k0 < K; k0 += kB) {
-      double2 v[kB];
-#pragma unroll
-      for (int q = 0; q < kB; ++q) v[q] = a.V[(size_t)min(k0 + q, K - 1) * a.ldv + p];
-#pragma unroll
-      for (int q = 0; q < kB; ++q)
-        if (k0 + q < K) w = csub(w, cmul(coef[k0 + q + kz], v[q]));
-    }
-    return csel(r >= 0 && r < n, w, z);
-  };
-  // u_K at two points at once, lane-parallel (the edge waves): half h of the wave takes point
-  // h, lane k of the half the term c_k u_k, the 32 terms summed by shuffles -- one load round
-  // trip instead of two chains of ceil(K / 8) batches (terms in a tree order: the strip that
-  // owns the column forms it in k order, so halo values agree to rounding)
-  auto unew2 = [&](int r1, int c1, int r2, int c2) {
-    const int h = lane >> 5, k = lane & 31;
-    const int r = h ? r2 : r1, c = h ? c2 : c1;
-    const size_t p = (size_t)min(max(r, 0), n - 1) * n + c;
-    const double2 wv = a.win[p];
-    const double2 vk = a.V[(size_t)min(k, K - 1) * a.ldv + p];
-    double2 tk = csel(k < K, cmul(coef[min(k, K - 1)], vk), z);
-#pragma unroll
-    for (int off = 16; off > 0; off >>= 1) {
-      tk.x += __shfl_xor(tk.x, off);
-      tk.y += __shfl_xor(tk.y, off);
-    }
-    const double2 u = csel(r >= 0 && r < n, csub(wv, tk), z);
-    const double2 ua = make_double2(__shfl(u.x, 0), __shfl(u.y, 0));
-    const double2 ub = make_double2(__shfl(u.x, 32), __shfl(u.y, 32));
-    return make_double2x2(ua, ub);
-  };
-  // the operator's coefficients at (row r, column c): W, E, S, N, D, D_beta (stencil.hip order)
-  struct Co {
-    double2 W, E, S, N, D, Db;
-  };
-  auto coefs = [&](int r, int c, double icv) {
-    const double* q = reinterpret_cast<const double*>(a.tab_j) + 8 * (size_t)min(max(r, 0), n - 1);
-    const double2 R2 = make_double2(q[0], q[1]), BS = make_double2(q[2], q[3]);
-    const double2 BN = make_double2(q[4], q[5]), OM = make_double2(q[6], q[7]);
-    const double2 AW = a.tab_i[c], AE = a.tab_i[n + c], R1 = a.tab_i[2 * n + c];
-    Co o;
-    o.W = cmul(AW, R2);
-    o.E = cmul(AE, R2);
-    o.S = cmul(BS, R1);
-    o.N = cmul(BN, R1);
-    const double2 M = cscale(cmul(OM, R1), icv);
-    const double2 sum4 = cadd(cadd(cadd(o.W, o.E), o.S), o.N);
-    o.D = csub(M, sum4);
-    o.Db = csub(cmul(M, mshift), sum4);
-    return o;
-  };
-  auto icv_at = [&](int r, int c) {
-    return CONSTC ? a.invc2_const : a.invc2[(size_t)min(max(r, 0), n - 1) * n + c];
-  };
-  double2 acc[K + 1];
-#pragma unroll
-  for (int k = 0; k <= K; ++k) acc[k] = z;
-  double nw = 0.0, nu = 0.0;
-  if (live) {
-    // rings (own column): u(L-2), u(L-1); T(L-2); z1(L-3), z1(L-2).  Edge waves: u(L-2, ie),
-    // u(L-1, ie), z1(L-2, ie).
-    double2 uP = z, uC = z, Tm = z, z1a = z, z1b = z;
-    double2 euP = z, euC = z, ez1b = z;
-    // row L-1's shifted diagonal and the reciprocal of its |.|^2 (cdiv's one division), handed
-    // to the second sweep of the next step, whose row it is
-    double2 Dbm = make_double2(1.0, 0.0);
-    double invm = 1.0;
-    int buf = 0;
-    for (int L0 = rb - 2; L0 <= re + 1; ++L0) {
-      int L = L0;
-      asm volatile("" : "+s"(L), "+s"(kz));
-      const double2 uN = unew(L, ic);
-      double2 euN = z, eo = z;
-      if (ew || ee) {  // (wave-uniform)
-        const auto pr = unew2(L, ie, L - 1, io);
-        euN = csel(ehas, pr.a, z);
-        eo = csel(ohas, pr.b, z);
-      }
-      urow[buf][1 + t] = csel(act, uC, z);
-      zrow[buf][1 + t] = csel(act, z1b, z);
-      if (ew && lane == 0) {
-        urow[buf][0] = euC;
-        zrow[buf][0] = ez1b;
-      }
-      if (ee && lane == kWave - 1) {
-        urow[buf][kT + 1] = euC;
-        zrow[buf][kT + 1] = ez1b;
-      }
-      __syncthreads();
-      const double2 uW = urow[buf][t], uE = urow[buf][t + 2];
-      const double2 zW = zrow[buf][t], zE = zrow[buf][t + 2];
-      const bool v1 = L - 1 >= 0 && L - 1 < n;  // row L-1 on the grid
-      // T and z1 on row L-1 (own column)
-      const double ic1 = icv_at(L - 1, ic);
-      const Co c1 = coefs(L - 1, ic, ic1);
-      double2 Au = cmul(c1.S, uP);
-      Au = cfma(c1.W, uW, Au);
-      Au = cfma(c1.D, uC, Au);
-      Au = cfma(c1.E, uE, Au);
-      Au = cfma(c1.N, uN, Au);
-      const double2 T1 = csel(act && v1, cscale(Au, sin), z);
-      const double inv1 = 1.0 / fma(c1.Db.x, c1.Db.x, c1.Db.y * c1.Db.y);
-      auto cdivr = [](double2 x, double2 b, double inv) {  // cdiv with the reciprocal given
-        return make_double2(fma(x.x, b.x, x.y * b.y) * inv, fma(x.y, b.x, -x.x * b.y) * inv);
-      };
-      const double2 z1c = csel(act && v1, cscale(cdivr(T1, c1.Db, inv1), damp), z);
-      // the same at the edge column (edge waves; broadcast values)
-      double2 ez1c = z;
-      if (ew || ee) {
-        const double2 uin = urow[buf][islot];
-        const double2 eW = ew ? eo : uin, eE = ew ? uin : eo;
-        const Co ce = coefs(L - 1, ie, icv_at(L - 1, ie));
-        double2 Ae = cmul(ce.S, euP);
-        Ae = cfma(ce.W, eW, Ae);
-        Ae = cfma(ce.D, euC, Ae);
-        Ae = cfma(ce.E, eE, Ae);
-        Ae = cfma(ce.N, euN, Ae);
-        const double2 eT = cscale(Ae, sin);
-        ez1c = csel(ehas && v1, cscale(cdiv(eT, ce.Db), damp), z);
-      }
-      // w on row r = L-2: the second sweep (A_beta on z1)
-      const int r = L - 2;
-      if (r >= rb && r < re) {  // (block-uniform)
-        const size_t p = (size_t)r * n + ic;
-        // row r's W, E, S, N (no mass term: its D_beta and reciprocal come from the last step)
-        const double* q = reinterpret_cast<const double*>(a.tab_j) + 8 * (size_t)r;
-        const double2 R2 = make_double2(q[0], q[1]), BS = make_double2(q[2], q[3]);
-        const double2 BN = make_double2(q[4], q[5]);
-        const double2 AW = a.tab_i[ic], AE = a.tab_i[n + ic], R1 = a.tab_i[2 * n + ic];
-        const double2 W2 = cmul(AW, R2), E2 = cmul(AE, R2), S2 = cmul(BS, R1), N2 = cmul(BN, R1);
-        double2 Az = cmul(S2, z1a);
-        Az = cfma(W2, zW, Az);
-        Az = cfma(Dbm, z1b, Az);
-        Az = cfma(E2, zE, Az);
-        Az = cfma(N2, z1c, Az);
-        const double2 w = csel(act, cadd(z1b, cscale(cdivr(csub(Tm, Az), Dbm, invm), damp)), z);
-        if (act) {
-          a.wout[p] = w;
-          a.uout[p] = uP;
-        }
-        const double2 uo = csel(act, uP, z);
-        nu = fma(uo.x, uo.x, fma(uo.y, uo.y, nu));
-        nw = fma(w.x, w.x, fma(w.y, w.y, nw));
-#pragma unroll
-        for (int k0 = 0; k0 < K; k0 += 8) {
-          double2 v[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] = a.V[(size_t)min(k0 + q, K - 1) * a.ldv + p];
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            if (k0 + q < K) acc[k0 + q] = cfma_conj(v[q], w, acc[k0 + q]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        acc[K] = cfma_conj(uo, w, acc[K]);
-      }
-      uP = uC;
-      uC = uN;
-      Tm = T1;
-      z1a = z1b;
-      z1b = z1c;
-      euP = euC;
-      euC = euN;
-      ez1b = ez1c;
-      Dbm = c1.Db;
-      invm = inv1;
-      buf ^= 1;
-    }
-  }
-  double v[2 * (K + 1) + 2];
-#pragma unroll
-  for (int k = 0; k <= K; ++k) {
-    v[2 * k] = acc[k].x;
-    v[2 * k + 1] = acc[k].y;
-  }
-  v[2 * (K + 1)] = nw;
-  v[2 * (K + 1) + 1] = nu;
-  block_reduce_vec<2 * (K + 1) + 2>(v, a.partials, 2 * (K + 1) + 2);
-}
-
-// basis vectors whose re-read comes from the LDS copy (HH_FUSED_KEEP: 0, 4 or 8; read per
-// launch so one process can A/B it)
-int fused_keep() {
-  const char* e = std::getenv("HH_FUSED_KEEP");
-  return e ? std::atoi(e) : kFusedKeepDefault;
-}
-template <int K>
-void fused_launch(const FusedArgs& a, int blocks, hipStream_t s) {
-  if (a.sl) {
-    if (a.invc2)
-      hipLaunchKernelGGL((fused_sl_iter_kernel<K, false>), dim3(blocks), dim3(kT), 0, s, a);
-    else
-      hipLaunchKernelGGL((fused_sl_iter_kernel<K, true>), dim3(blocks), dim3(kT), 0, s, a);
-    return;
-  }
-  const int keep = fused_keep();
-  if (keep >= 8) {
-    if (a.invc2)
-      hipLaunchKernelGGL((fused_iter_kernel<K, false, 8>), dim3(blocks), dim3(kT), 0, s, a);
-    else
-      hipLaunchKernelGGL((fused_iter_kernel<K, true, 8>), dim3(blocks), dim3(kT), 0, s, a);
-  } else if (keep >= 4) {
-    if (a.invc2)
-      hipLaunchKernelGGL((fused_iter_kernel<K, false, 4>), dim3(blocks), dim3(kT), 0, s, a);
-    else
-      hipLaunchKernelGGL((fused_iter_kernel<K, true, 4>), dim3(blocks), dim3(kT), 0, s, a);
-  } else {
-    if (a.invc2)
-      hipLaunchKernelGGL((fused_iter_kernel<K, false, 0>), dim3(blocks), dim3(kT), 0, s, a);
-    else
-      hipLaunchKernelGGL((fused_iter_kernel<K, true, 0>), dim3(blocks), dim3(kT), 0, s, a);
-  }
-}
-template <int... Ks>
-struct FTable {
-  using FN = void (*)(const FusedArgs&, int, hipStream_t);
-  static constexpr FN f[] = {fused_launch<Ks>...};
-};
-using FusedTable = FTable<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20>;
-static_assert(kFusedMaxK == 20, "table covers 1..kFusedMaxK");
-
 template <int K>
 void md_launch(const double2* V, size_t ldv, const double2* w, size_t len, double* part,
                int blocks, hipStream_t s, const int* stop, double* out, int cols,
@@ -1095,25 +621,6 @@ using Table = KTable<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 
 static_assert(kMaxProj == 32, "table covers 1..kMaxProj");
 
 }  // namespace
-
-int fused_iter_rows(int n) {
-  static const int env = [] {
-    const char* e = std::getenv("HH_FUSED_ROWS");
-    return e ? std::atoi(e) : 0;
-  }();
-  const long tiles_x = (n + kT - 1) / kT;
-  int R = env > 0 ? env : (int)std::min<long>(32, std::max<long>(8, tiles_x * n / 1024));
-  // the partial rows (one per block) fit kMaxStreamBlocks
-  while ((long)tiles_x * ((n + R - 1) / R) > kMaxStreamBlocks) R *= 2;
-  return R;
-}
-int fused_iter_blocks(int n, int rows) {
-  const int T = (n + kT - 1) / kT * ((n + rows - 1) / rows);
-  return (T + 7) / 8 * 8;
-}
-void launch_fused_iter(int K, const FusedArgs& a, int blocks, hipStream_t stream) {
-  FusedTable::f[K - 1](a, blocks, stream);
-}
 
 void tune_krylov(int nt, int blocks) {
   g_krylov_nt = nt < 0 ? -1 : (nt != 0);

@@ -755,10 +755,6 @@ void read_dev(hh_op* op, const double* dsrc, double* hdst, int count) {
   std::memcpy(hdst, op->status_h, count * sizeof(double));
 }
 
-// The persistent sweep chain (sweep_dense.hip) bounds its grid-wide waits and reports a
-// timeout in red[kRedTimeout] instead of hanging; its output is then garbage.  Every path that
-// ran a chained sweep apply checks the word here (one synchronising read; nothing for the other
-// preconditioners) and clears it only after the check, so no timeout is lost or reported twice.
 // the one-pass iteration where it applies, unless HH_FUSED_ITER=0
 bool fused_default() {
   static const bool on = [] {
@@ -768,6 +764,125 @@ bool fused_default() {
   return on;
 }
 
+// One pass of the one-pass GMRES iteration (fused.hip) over the rank's slabs: u_K = w_{K-1} -
+// sum_k c_k u_k into V[K], w_K = M A (s_K u_K) into wout, and the partial rows of the next
+// projections (width 2 (K + 1) + 2).  Slabs of one rank read each other's rows in place
+// (FROW_MEM).  Across ranks the rows next to a rank boundary need the neighbour's u_K, which
+// does not exist before the pass: the rank's own edge rows of it (H = 1, or 2 for the
+// shifted Laplace) are formed first by a small launch, exchanged on the halo stream while the
+// interior rows run on the compute stream, and the H boundary rows run behind the exchange on
+// the halo stream (run_stencil's overlap).  Returns the number of partial rows written.
+int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double* raw,
+              const double* sin) {
+  hh_ctx* c = op->ctx;
+  const int n = op->n;
+  const int S = (int)op->slabs.size();
+  const bool sl = op->pkind == HH_PREC_SHIFTED_LAPLACE;
+  const int H = sl ? 2 : 1;
+  const bool lo_x = c->world > 1 && c->rank > 0;
+  const bool hi_x = c->world > 1 && c->rank < c->world - 1;
+  const size_t ldv = op->nloc;
+  double2* uout = op->V + (size_t)K * ldv;
+  const int width = 2 * (K + 1) + 2;
+  const int rows_rank = op->je - op->jb;
+  const int R = fused_iter_rows(n, rows_rank);
+  FusedArgs base{};
+  base.ldv = ldv;
+  base.raw = raw;
+  base.vscale = op->gs.vscale;
+  base.sin = sin;
+  base.tab_i = op->tab_i;
+  base.invc2_const = op->invc2_const;
+  base.n = n;
+  base.jac = op->pkind == HH_PREC_JACOBI ? 1 : 0;
+  base.sl = sl ? 1 : 0;
+  base.mshift = op->mshift;
+  base.damping = op->damping;
+  base.stop = op->stop_flag;
+  int nparts = 0;
+  auto launch = [&](int si, int r0, int r1, int rows, int step, hipStream_t st) {
+    if (r1 <= r0) return;
+    const Slab& s = op->slabs[si];
+    FusedArgs a = base;
+    a.V = op->V + s.off;
+    a.win = win + s.off;
+    a.wout = wout + s.off;
+    a.uout = uout + s.off;
+    a.tab_j = s.tab_j;
+    a.invc2 = op->const_c ? nullptr : s.invc2;
+    a.invc2_halo = s.invc2_halo;
+    a.nl = s.nl;
+    a.lo_mode = si > 0 ? FROW_MEM : (lo_x ? FROW_HALO : FROW_ZERO);
+    a.hi_mode = si < S - 1 ? FROW_MEM : (hi_x ? FROW_HALO : FROW_ZERO);
+    a.halo_lo = sl ? s.halo2_lo : s.halo_lo_buf;
+    a.halo_hi = sl ? s.halo2_hi : s.halo_hi_buf;
+    a.row_begin = r0;
+    a.row_end = r1;
+    a.rows = rows;
+    a.row_step = step;
+    a.bands = step > 0 ? (r1 - r0 - 1) / step + 1 : (r1 - r0 + rows - 1) / rows;
+    a.partials = op->partials + (size_t)nparts * width;
+    const int blocks = fused_iter_blocks(n, a.bands);
+    REQUIRE((size_t)(nparts + blocks) * width <= op->partials_cap,
+            "partials workspace too small for the one-pass iteration (%d blocks)", nparts + blocks);
+    launch_fused_iter(K, a, blocks, st);
+    nparts += blocks;
+  };
+  hipEvent_t t_halo = nullptr;
+  if (lo_x || hi_x) {
+    FusedArgs e = base;  // (rank-local rows)
+    e.V = op->V;
+    e.win = win;
+    e.uout = uout;
+    if (rows_rank <= 2 * H)
+      launch_fused_edge(K, e, 0, rows_rank, 0, 0, c->stream);
+    else
+      launch_fused_edge(K, e, 0, lo_x ? H : 0, rows_rank - H, hi_x ? H : 0, c->stream);
+    const Slab& s0 = op->slabs[0];
+    const Slab& sL = op->slabs[S - 1];
+    hipEvent_t t_ready = tmark(op, c->stream);
+    c->comm->halo(lo_x ? uout : nullptr, lo_x ? (sl ? s0.halo2_lo : s0.halo_lo_buf) : nullptr,
+                  hi_x ? uout + (size_t)(rows_rank - H) * n : nullptr,
+                  hi_x ? (sl ? sL.halo2_hi : sL.halo_hi_buf) : nullptr,
+                  (size_t)H * n * sizeof(double2), c->stream, c->cstream, c->ev_in);
+    t_halo = tmark(op, c->cstream);
+    tspan(op, HH_SPAN_HALO, t_ready, t_halo);
+  }
+  hipEvent_t t_int0 = tmark(op, c->stream);
+  for (int si = 0; si < S; ++si) {
+    const Slab& s = op->slabs[si];
+    const int r0 = (si == 0 && lo_x) ? H : 0;
+    const int r1 = (si == S - 1 && hi_x) ? s.nl - H : s.nl;
+    launch(si, r0, r1, R, 0, c->stream);
+  }
+  hipEvent_t t_int1 = tmark(op, c->stream);
+  tspan(op, HH_SPAN_INTERIOR, t_int0, t_int1);
+  if (lo_x || hi_x) {
+    hipStream_t hs = c->cstream;
+    const Slab& s0 = op->slabs[0];
+    const Slab& sL = op->slabs[S - 1];
+    if (S == 1 && lo_x && hi_x) {
+      if (s0.nl <= 2 * H) launch(0, 0, s0.nl, s0.nl, 0, hs);  // (no interior rows)
+      else launch(0, 0, s0.nl, H, s0.nl - H, hs);             // rows [0, H) and [nl - H, nl)
+    } else {
+      if (lo_x) launch(0, 0, std::min(H, s0.nl), H, 0, hs);
+      if (hi_x) launch(S - 1, std::max(0, sL.nl - H), sL.nl, H, 0, hs);
+    }
+    hipEvent_t t_bnd = tmark(op, hs);
+    tspan(op, HH_SPAN_BOUNDARY, t_halo, t_bnd);
+    tspan(op, HH_SPAN_HALO_WAIT, t_int1, t_bnd, true);
+    HIPC(hipEventRecord(c->ev_halo, hs));
+    HIPC(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+  }
+  HIPC(hipGetLastError());
+  op->stats.spmv_count++;
+  return nparts;
+}
+
+// The persistent sweep chain (sweep_dense.hip) bounds its grid-wide waits and reports a
+// timeout in red[kRedTimeout] instead of hanging; its output is then garbage.  Every path that
+// ran a chained sweep apply checks the word here (one synchronising read; nothing for the other
+// preconditioners) and clears it only after the check, so no timeout is lost or reported twice.
 void check_sweep_chain(hh_op* op) {
   const bool grid = op->sw_chain || (!op->sw_T && op->sweep.chunks > 0 && op->sweep.G > 1);
   if (!grid || !is_sweep(op->pkind)) return;
@@ -2019,12 +2134,14 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
   bool legacy = legacy_maxiter != 0;
   // collectives per inner iteration: one (lagged normalisation) by default across ranks, two on
   // one rank (no collective there; the exact-norm path keeps round 1's bit-for-bit results)
-  // one pass over the basis per inner iteration (krylov.hip fused_iter_kernel): the lagged
+  // one pass over the basis per inner iteration (fused.hip fused_iter_kernel): the lagged
   // iteration with the update, the next M A and the next projection in one streaming kernel;
-  // single rank and slab, 5-point, M none / Jacobi (mode 3, or by default where it applies)
-  const bool fused_ok = !reorth && c->world == 1 && op->slabs.size() == 1 && op->points == 5 &&
+  // any slabs and ranks (run_fused: one halo exchange and one allreduce per inner iteration),
+  // 5-point, M none / Jacobi / two-sweep shifted Laplace (mode 3, or by default where it applies)
+  const bool fused_ok = !reorth && op->points == 5 &&
                         (op->pkind == HH_PREC_NONE || op->pkind == HH_PREC_JACOBI ||
-                         (op->pkind == HH_PREC_SHIFTED_LAPLACE && op->sweeps == 2)) &&
+                         (op->pkind == HH_PREC_SHIFTED_LAPLACE && op->sweeps == 2 &&
+                          op->sl_ext_ok)) &&
                         restart <= kFusedMaxK + 1;
   // (by default from n = 1024: smaller grids give the pass too few tiles to stream at speed --
   // n = 300: 16-25k it/s against 29-30k for the regular cycle, profiles/r03q)
@@ -2250,45 +2367,30 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       apply_MA(op, V, g.sscale, Wb[0]);  // w_0 = M A (s_0 u_0)
       launch_multidot(V, ldv, 1, Wb[0], L, op->partials, blocks, s, stp);
       launch_reduce(op->partials, blocks, 4, 3, op->red + 16, s, stp);
+      allreduce_sum_dev(op, op->red + 16, 3);
       launch_gmres_lag(g, 0, op->red + 16, op->red + 16 + 3, false, eps, ptol, stop_col, s);
-      const int frows = fused_iter_rows(op->n);
-      const int fblocks = fused_iter_blocks(op->n, frows);
       for (int c2 = 0; c2 < stop_col; ++c2) {
         const int K = c2 + 1, K2 = K + 1;
-        FusedArgs fa{};
-        fa.V = V;
-        fa.ldv = ldv;
-        fa.win = Wb[c2 & 1];
-        fa.wout = Wb[(c2 + 1) & 1];
-        fa.uout = V + (size_t)K * ldv;
-        fa.raw = op->red + 16;
-        fa.vscale = g.vscale;
-        fa.sin = g.sscale + K;
-        fa.tab_i = op->tab_i;
-        fa.tab_j = op->slabs[0].tab_j;
-        fa.invc2 = op->const_c ? nullptr : op->slabs[0].invc2;
-        fa.invc2_const = op->invc2_const;
-        fa.n = op->n;
-        fa.rows = frows;
-        fa.jac = op->pkind == HH_PREC_JACOBI ? 1 : 0;
-        fa.sl = op->pkind == HH_PREC_SHIFTED_LAPLACE ? 1 : 0;
-        fa.mshift = op->mshift;
-        fa.damping = op->damping;
-        fa.partials = op->partials;
-        fa.stop = stp;
-        launch_fused_iter(K, fa, fblocks, s);
-        op->stats.spmv_count++;
-        // (dots, |w|^2 and |u|^2 in one partial row: one reduce)
-        launch_reduce(op->partials, fblocks, 2 * K2 + 2, 2 * K2 + 2, op->red + 16, s, stp);
+        const int np = run_fused(op, K, Wb[c2 & 1], Wb[(c2 + 1) & 1], op->red + 16, g.sscale + K);
+        // (dots, |w|^2 and |u|^2 in one partial row: one reduce, one allreduce)
+        hipEvent_t k0 = tmark(op, s);
+        launch_reduce(op->partials, np, 2 * K2 + 2, 2 * K2 + 2, op->red + 16, s, stp);
+        tspan(op, HH_SPAN_MULTIDOT, k0, tmark(op, s));
+        allreduce_sum_dev(op, op->red + 16, 2 * K2 + 2);
+        hipEvent_t k1 = tmark(op, s);
         launch_gmres_lag(g, c2 + 1, op->red + 16, op->red + 16 + 2 * K2 + 1, false, eps, ptol,
                          stop_col, s);
+        tspan(op, HH_SPAN_COLUMN, k1, tmark(op, s));
         HIPC(hipGetLastError());
       }
       {  // the last column's update and the norm that completes it
         const int K = stop_col + 1;
+        hipEvent_t k0 = tmark(op, s);
         launch_update(V, ldv, K, op->red + 16, g.vscale, Wb[stop_col & 1],
                       V + (size_t)(stop_col + 1) * ldv, L, op->npart, blocks, s, stp);
+        tspan(op, HH_SPAN_UPDATE, k0, tmark(op, s));
         launch_reduce(op->npart, blocks, kMaxNorms, 1, op->red + 8, s, stp);
+        allreduce_sum_dev(op, op->red + 8, 1);
         launch_gmres_lag(g, stop_col + 1, nullptr, op->red + 8, true, eps, ptol, stop_col, s);
         HIPC(hipGetLastError());
       }

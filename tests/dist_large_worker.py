@@ -64,7 +64,7 @@ def main():
                              return_history=True)
     xref = np.load(os.path.join(a.ref_dir, "x.npy"), mmap_mode="r")[j0 * n:j1 * n]
     out.update(info=info, hist=hist, dx2=float(np.sum(np.abs(xs - xref) ** 2)),
-               x2=float(np.sum(np.abs(xref) ** 2)))
+               x2=float(np.sum(np.abs(xref) ** 2)), path=A.last_solve_path())
     np.savez(a.out, **out)
     ctx.barrier()
 

@@ -28,8 +28,10 @@ class SlabOperator:
         self.n, self.j0, self.j1 = n, j0, j1
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
         self.jacobi = jacobi
+        self.halo_calls = 0  # halo exchanges so far (gmres_dist_onepass counts them per pass)
 
     def _halo(self, X):
+        self.halo_calls += 1
         n = self.n
         lo, hi = np.zeros(n, complex), np.zeros(n, complex)
         reqs = []
@@ -276,3 +278,119 @@ def gmres_dist_lagged(op, b, rtol, restart, maxiter):
         ptol_f = max(eps, 0.25 * ptol_f) if presid <= ptol else min(1.0, 1.5 * ptol_f)
         ptol = presid * min(ptol_f, atol / rn)
     return x, (0 if rn <= atol else maxiter), np.array(hist), cycle_reduces / inner
+
+
+def gmres_dist_onepass(op, b, rtol, restart, maxiter):
+    """The one-pass inner iteration across ranks (csrc/runtime.cpp run_fused + hh_gmres, DESIGN
+    3g), restated in the runtime's order: a cycle starts with w_0 = M A (s_0 u_0) and its
+    projection (one allreduce); then every pass K forms u_K = w_{K-1} - sum_k c_k u_k on the
+    rank's own rows, exchanges ONLY u_K's edge rows (fused_edge_kernel + the halo exchange: the
+    neighbours' passes read them as their halo rows), forms w_K = M A (s_K u_K) from the own rows
+    and the received ones, and reduces <u_k, w_K> (k <= K), |w_K|^2 and |u_K|^2 in ONE allreduce;
+    the cycle's last update adds one allreduce (its norm).  Same Hessenberg arithmetic as
+    gmres_dist_lagged.  Returns (x, info, history, allreduces per pass, halo exchanges per pass):
+    each pass is one inner iteration's update + M A + projection."""
+    lartg = get_lapack_funcs('lartg', dtype=np.complex128)
+    eps = np.finfo(float).eps
+    x = np.zeros_like(b)
+    bn = gnorm(b)
+    atol = rtol * bn
+    Mb = gnorm(op.psolve(b))
+    ptol_f = 1.0
+    ptol = Mb * min(ptol_f, atol / bn)
+    U = np.empty((restart + 1, b.size), complex)
+    vs = np.zeros(restart + 1)
+    ss = np.zeros(restart + 1)
+    H = np.zeros((restart, restart + 1), complex)
+    G = np.zeros((restart, 2), complex)
+    hist, inner, reduces, halos, passes = [], 0, 0, 0, 0
+    r = b.copy()
+    presid = 0.0
+    for _ in range(maxiter):
+        U[0] = op.psolve(r)
+        t = gnorm(U[0])
+        vs[0] = ss[0] = 1 / t
+        S = np.zeros(restart + 1, complex)
+        S[0] = t
+        brk = False
+        h0 = {}
+        stop_col = min(restart - 1, maxiter - inner - 1)
+
+        def finish(col, h1):
+            nonlocal brk, presid
+            H[col, col + 1] = h1
+            if h1 <= eps * h0[col]:
+                H[col, col + 1] = 0
+                brk = True
+            for k in range(col):
+                c, s = G[k]
+                n0, n1 = H[col, [k, k + 1]]
+                H[col, [k, k + 1]] = [c * n0 + s * n1, -s.conj() * n0 + c * n1]
+            c, s, mag = lartg(H[col, col], H[col, col + 1])
+            G[col] = [c, s]
+            H[col, [col, col + 1]] = mag, 0
+            tmp = -np.conj(s) * S[col]
+            S[[col, col + 1]] = [c * S[col], tmp]
+            presid = abs(tmp)
+            hist.append(presid / bn)
+            return presid <= ptol or brk or col >= stop_col
+
+        def start(j, d, w2):  # column j from the raw dots; the next SpMV input's scale
+            f = vs[j] / ss[j]
+            H[j, :j + 1] = d * vs[:j + 1] * f
+            h0[j] = np.sqrt(w2) * f
+            ss[j + 1] = 1 / np.sqrt(max(w2 - np.sum(np.abs(d) ** 2 * vs[:j + 1] ** 2),
+                                        max(w2 * 1e-28, 1e-300)))
+
+        # the cycle's head: w_0 and its projection
+        w = ss[0] * op.psolve(op.apply(U[0]))
+        raw = counted_allreduce([np.vdot(U[0], w).real, np.vdot(U[0], w).imag,
+                                 np.vdot(w, w).real])
+        d = np.array([raw[0] + 1j * raw[1]])
+        start(0, d, raw[2])
+        col, done = -1, False
+        for K in range(1, stop_col + 1):  # pass K: update K-1, M A and projection of K
+            U[K] = w - (d * vs[:K] ** 2) @ U[:K]
+            passes += 1
+            h_before = op.halo_calls
+            w = ss[K] * op.psolve(op.apply(U[K]))  # (exchanges exactly u_K's edge rows)
+            halos += op.halo_calls - h_before
+            vals = sum(([c.real, c.imag] for c in (U[:K + 1].conj() @ w)), [])
+            raw = counted_allreduce(vals + [np.vdot(w, w).real, np.vdot(U[K], U[K]).real])
+            reduces += 1
+            d = raw[0:2 * (K + 1):2] + 1j * raw[1:2 * (K + 1):2]
+            sj = np.sqrt(raw[2 * (K + 1) + 1])
+            vs[K] = 1 / sj
+            col = K - 1
+            if finish(col, sj * vs[K - 1] / ss[K - 1]):
+                done = True
+                break
+            start(K, d, raw[2 * (K + 1)])
+        if not done:  # the last update and its norm (one more reduction per cycle)
+            U[stop_col + 1] = w - (d * vs[:stop_col + 1] ** 2) @ U[:stop_col + 1]
+            sl = np.sqrt(counted_allreduce([np.vdot(U[stop_col + 1], U[stop_col + 1]).real])[0])
+            col = stop_col
+            vs[stop_col + 1] = 1 / sl
+            finish(col, sl * vs[col] / ss[col])
+        inner += col + 1
+        if H[col, col] == 0:
+            S[col] = 0
+        y = S[:col + 1].copy()
+        for k in range(col, 0, -1):
+            if y[k] != 0:
+                y[k] /= H[k, k]
+                y[:k] -= y[k] * H[k, :k]
+        if y[0] != 0:
+            y[0] /= H[0, 0]
+        x += (y * vs[:col + 1]) @ U[:col + 1]
+        r = b - op.apply(x)
+        rn = gnorm(r)
+        per = max(passes, 1)
+        if inner == maxiter:
+            return x, (0 if rn <= atol else maxiter), np.array(hist), reduces / per, halos / per
+        if rn <= atol or brk:
+            break
+        ptol_f = max(eps, 0.25 * ptol_f) if presid <= ptol else min(1.0, 1.5 * ptol_f)
+        ptol = presid * min(ptol_f, atol / rn)
+    per = max(passes, 1)
+    return x, (0 if rn <= atol else maxiter), np.array(hist), reduces / per, halos / per

@@ -33,6 +33,7 @@ def main():
     p.add_argument("--stencil", type=int, default=5)
     p.add_argument("--apply-only", action="store_true")
     p.add_argument("--transport", default="shm", choices=["shm", "rccl"])
+    p.add_argument("--krylov", default="auto", help="krylov mode of the solves (auto, one, fused)")
     p.add_argument("--default-limits", action="store_true",
                    help="also solve with scipy's default restart / maxiter (global-N based)")
     a = p.parse_args()
@@ -51,6 +52,7 @@ def main():
     om, h, eta = H.problem_params(n, 12, 6.0, 2.0)
     cm = H.init_c1_mat(.5, .5, n)
     A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, context=ctx, stencil=a.stencil)
+    A.krylov_mode(a.krylov)
     j0, j1 = A.row_begin, A.row_end
     rng = np.random.default_rng(5)
     xg = (rng.standard_normal(n * n) + 1j * rng.standard_normal(n * n)).reshape(n, n)
@@ -67,6 +69,7 @@ def main():
                                 callback=lambda r: None, callback_type="legacy",
                                 return_history=True)
         out[f"x_{name}"], out[f"info_{name}"], out[f"hist_{name}"] = x, info, hist
+        out[f"path_{name}"] = A.last_solve_path()
     if a.default_limits:
         x, info = H.gmres(A, f, rtol=1e-3, M="jacobi")
         out["x_default"], out["info_default"] = x, info

@@ -52,6 +52,8 @@ def test_file_rendezvous_two_processes():
 
 
 def _gloo_worker(rank, world, port, case, out, lagged=False):
+    """lagged: False (two allreduces per iteration), True (one), or "onepass" (the one-pass
+    iteration's order: one halo exchange of u_K's edge rows and one allreduce per pass)"""
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -68,23 +70,31 @@ def _gloo_worker(rank, world, port, case, out, lagged=False):
                          medium(str(z["medium"]), n), j0, j1,
                          jacobi=str(z["precond"]) == "jacobi")
     f = O.init_f1_mat(.5, .125, om, n)[j0:j1].ravel()
-    if lagged:
+    halo_it = 1.0
+    if lagged == "onepass":
+        x, info, hist, per_it, halo_it = DM.gmres_dist_onepass(op, f, 1e-3, 20, int(z["K"]))
+    elif lagged:
         x, info, hist, per_it = DM.gmres_dist_lagged(op, f, 1e-3, 20, int(z["K"]))
     else:
         x, info, hist = DM.gmres_dist(op, f, 1e-3, 20, int(z["K"]))
         per_it = 2.0
-    np.savez(out, x=x, info=info, hist=hist, j0=j0, j1=j1, per_it=per_it)
+    np.savez(out, x=x, info=info, hist=hist, j0=j0, j1=j1, per_it=per_it, halo_it=halo_it)
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("case,world,lagged", [("gmres_n64_c1_none.npz", 2, False),
                                                ("gmres_n128_jacobi.npz", 3, False),
                                                ("gmres_n64_c1_none.npz", 2, True),
-                                               ("gmres_n128_jacobi.npz", 3, True)])
+                                               ("gmres_n128_jacobi.npz", 3, True),
+                                               ("gmres_n64_c1_none.npz", 2, "onepass"),
+                                               ("gmres_n128_jacobi.npz", 3, "onepass"),
+                                               ("gmres_n128_none.npz", 4, "onepass")])
 def test_distributed_gmres_mirror_matches_reference(case, world, lagged):
-    """lagged: the one-allreduce iteration (the runtime's default across ranks) -- the golden
-    histories to 1e-9, with ONE allreduce per inner iteration inside the restart cycles (plus
-    one per cycle for the last column's norm)."""
+    """lagged: the one-allreduce iteration (the runtime's lagged path across ranks) -- the
+    golden histories to 1e-9, with ONE allreduce per inner iteration inside the restart cycles
+    (plus one per cycle for the last column's norm).  "onepass": the one-pass iteration's order
+    (runtime.cpp run_fused, the default across ranks from n = 1024) -- ONE allreduce and ONE halo
+    exchange (u_K's edge rows) per pass."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -107,6 +117,8 @@ def test_distributed_gmres_mirror_matches_reference(case, world, lagged):
             assert np.max(np.abs(p["hist"] - z["history"]) / z["history"]) < 1e-9
             if lagged:  # one allreduce per inner iteration inside the cycles
                 assert float(p["per_it"]) == 1.0
+            if lagged == "onepass":  # and one halo exchange, of u_K's edge rows
+                assert float(p["halo_it"]) == 1.0
         assert np.linalg.norm(x - z["x"]) / np.linalg.norm(z["x"]) < 1e-9
 
 

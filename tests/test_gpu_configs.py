@@ -100,9 +100,9 @@ from test_gpu_dist import rccl_rank_env  # noqa: E402  (one NCCL host id per ran
 
 
 def _single_domain_solve(ctx, d, n, wn, K, with_apply, K_oracle=None):
-    """Single-domain (hash-filled) apply and Jacobi GMRES(20) of K iterations in the ranks'
-    krylov mode (one allreduce per iteration: like with like), x saved for the ranks; with
-    K_oracle also the default-mode solve of K_oracle iterations, saved for the oracle."""
+    """Single-domain (hash-filled) apply and Jacobi GMRES(20) of K iterations in the default
+    krylov mode -- the one-pass iteration, which the ranks run too (like with like) --, x saved
+    for the ranks; with K_oracle also a solve of K_oracle iterations, saved for the oracle."""
     om, h, eta = H.problem_params(n, B, wn, ALPHA)
     A = H.build_A_matrix(B, C, eta, om, h, n, np.broadcast_to(1.0, (n + 2, n + 2)), context=ctx)
     xh = yh = None
@@ -115,15 +115,15 @@ def _single_domain_solve(ctx, d, n, wn, K, with_apply, K_oracle=None):
         y.close()
         np.save(d / "y.npy", yh)
     f = H.init_f1_mat(.5, .125, om, n).ravel()
-    A.krylov_mode("one")
+    A.krylov_mode("auto")
     xs, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=K, M="jacobi",
                              callback=lambda r: None, callback_type="legacy",
                              return_history=True)
+    assert A.last_solve_path() == "one-pass"
     np.save(d / "x.npy", xs)
     del xs
     ko = None
     if K_oracle:
-        A.krylov_mode("auto")  # (the single-rank default: two reductions per iteration)
         xo, info_o, hist_o = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=K_oracle, M="jacobi",
                                      callback=lambda r: None, callback_type="legacy",
                                      return_history=True)
@@ -213,6 +213,7 @@ def _run_large_ranks(tmp_path, d, world, transport, n, wn, K, apply_check=True):
 
 def _assert_ranks_match(parts, info, hist):
     for p in parts:
+        assert str(p["path"]) == "one-pass"  # (the default across ranks from n = 1024)
         assert int(p["info"]) == info and len(p["hist"]) == len(hist)
         assert np.max(np.abs(p["hist"] - hist) / hist) < 1e-8
     dx = np.sqrt(sum(float(p["dx2"]) for p in parts) / sum(float(p["x2"]) for p in parts))

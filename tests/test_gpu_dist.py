@@ -59,12 +59,14 @@ def _run_workers(tmp_path, world, n, extra=(), transport="shm", timeout=240):
     return [np.load(o) for _, o in procs]
 
 
-def _single_domain(n, stencil=5, default_limits=False):
+def _single_domain(n, stencil=5, default_limits=False, krylov="one"):
     ctx = H.Context(device=0)
     om, h, eta = H.problem_params(n, 12, 6.0, 2.0)
     A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.init_c1_mat(.5, .5, n), context=ctx,
                          stencil=stencil)
-    A.krylov_mode("one")  # the ranks' default (one allreduce per iteration): like with like
+    # like with like: the ranks' mode ("one": the lagged iteration, their default below n = 1024;
+    # "fused": the one-pass iteration)
+    A.krylov_mode(krylov)
     rng = np.random.default_rng(5)
     xg = rng.standard_normal(n * n) + 1j * rng.standard_normal(n * n)
     res = dict(y=A @ xg)
@@ -78,6 +80,7 @@ def _single_domain(n, stencil=5, default_limits=False):
                                 callback=lambda r: None, callback_type="legacy",
                                 return_history=True)
         res[f"x_{name}"], res[f"info_{name}"], res[f"hist_{name}"] = x, info, hist
+        res[f"path_{name}"] = A.last_solve_path()
     if default_limits:
         res["x_default"], res["info_default"] = H.gmres(A, f, rtol=1e-3, M="jacobi")
     return res
@@ -128,6 +131,26 @@ def test_uneven_slabs_default_limits(tmp_path):
     n = 151
     _check_against_single_domain(_run_workers(tmp_path, 3, n, ["--default-limits"]),
                                  _single_domain(n, default_limits=True), 3, n)
+
+
+@pytest.mark.parametrize("world,slabs,transport", [(2, 1, "shm"), (3, 2, "shm"), (4, 1, "shm"),
+                                                  (2, 1, "rccl"), (3, 1, "rccl"),
+                                                  (4, 2, "rccl")])
+def test_fused_pass_ranks_match_single_domain(tmp_path, world, slabs, transport):
+    """The one-pass iteration across ranks (runtime.cpp run_fused: u_K's edge rows formed
+    first, exchanged on the halo stream while the interior rows run, the boundary rows behind
+    the exchange; one allreduce per pass) for none / Jacobi / the two-sweep shifted Laplace
+    (two edge rows), over both transports, with and without virtual slabs inside the ranks:
+    every rank reports the one-pass path, and matches the single domain's one-pass solve to
+    1e-8."""
+    n = 150
+    parts = _run_workers(tmp_path, world, n, ["--slabs", str(slabs), "--krylov", "fused"],
+                         transport=transport, timeout=240)
+    ref = _single_domain(n, krylov="fused")
+    for name in ("none", "jacobi", "sl"):
+        assert ref[f"path_{name}"] == "one-pass"
+        assert all(str(p[f"path_{name}"]) == "one-pass" for p in parts), name
+    _check_against_single_domain(parts, ref, world, n)
 
 
 @pytest.mark.parametrize("world", [2, 3])

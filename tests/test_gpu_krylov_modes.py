@@ -217,17 +217,17 @@ def test_fused_pass_is_the_single_rank_default(ctx):
 
 @pytest.mark.parametrize("n,kind", [(300, "c1"), (1100, "marmousi")])
 def test_fused_pass_lds_kept_basis_is_bit_identical(ctx, n, kind, monkeypatch):
-    """HH_FUSED_KEEP (read per launch): the projections' re-read of the first 0 / 4 / 8 basis
-    vectors from the pass's own LDS copy instead of the memory system reads the same values in
-    the same order -- histories and fields bit-identical (K up to 20: the kept and re-read
-    vectors mixed in one pass)"""
+    """HH_FUSED_KEEP (read per launch): the projections' re-read of the first 17 basis vectors
+    from the pass's own one-row LDS copy (the default) instead of the memory system (0) reads
+    the same values in the same order -- histories and fields bit-identical (K up to 20: the
+    kept and re-read vectors mixed in one pass)"""
     om, h, eta = O.problem_params(n, 12, n / 40.0, 2.0)
     cm = medium(kind, n) if kind != "marmousi" else H.marmousi_like_c_mat(n)
     A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, context=ctx)
     f = O.init_f1_mat(.5, .125, om, n).ravel()
     A.krylov_mode("fused")
     out = []
-    for keep in ("0", "4", "8"):
+    for keep in ("0", "17"):
         monkeypatch.setenv("HH_FUSED_KEEP", keep)
         hist = []
         x, info = H.gmres(A, f, rtol=1e-12, restart=21, maxiter=25, M="jacobi",
@@ -238,3 +238,38 @@ def test_fused_pass_lds_kept_basis_is_bit_identical(ctx, n, kind, monkeypatch):
     for x, hh in out[1:]:
         assert np.array_equal(hh, out[0][1])
         assert np.array_equal(x, out[0][0])
+
+
+@pytest.mark.parametrize("n,slabs", [(150, 2), (300, 3), (613, 4)])
+@pytest.mark.parametrize("precond", [None, "jacobi", "sl"])
+def test_fused_pass_virtual_slabs_match_single_slab(ctx, n, slabs, precond):
+    """The one-pass iteration over several slabs of one rank (runtime.cpp run_fused: one launch
+    per slab, the rows next to a slab boundary formed in place from the neighbouring slab,
+    FROW_MEM -- two rows for the shifted Laplace) against the single slab: u and w are formed
+    by the same arithmetic, only the projections' partial rows add in another order -- history
+    and field (the dist tests' problem; restart 12, 26 iterations: three cycles)"""
+    om, h, eta = H.problem_params(n, 12, 6.0, 2.0)
+    cm = H.init_c1_mat(.5, .5, n)
+    f = H.init_f1_mat(.5, .125, om, n).ravel()
+    vctx = H.Context(device=0, virtual_slabs=slabs)
+    out = []
+    for c in (ctx, vctx):
+        A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, context=c)
+        A.krylov_mode("fused")
+        A.small_cycle("off")  # (n = 150, restart 12 would take the whole-cycle kernel)
+        M = H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7) if precond == "sl" else precond
+        x, info, hist = H.gmres(A, f, rtol=1e-3, restart=12, maxiter=26, M=M,
+                                callback=lambda r: None, callback_type="legacy",
+                                return_history=True)
+        assert A.last_solve_path() == "one-pass"
+        out.append((x, info, np.asarray(hist)))
+        A.close()
+    vctx.close()
+    (x1, i1, h1), (x2, i2, h2) = out
+    assert i1 == i2 and len(h1) == len(h2)
+    # the first iterations to rounding (the reordered sums' last bits); later iterations
+    # amplify that rounding (DESIGN 6 'Where history parity is defined at all'): the whole
+    # history and the field within the parity contract
+    assert np.max(np.abs(h1[:5] - h2[:5]) / h1[:5]) < 1e-10
+    assert np.max(np.abs(h1 - h2) / h1) < TOL
+    assert relerr(x2, x1) < TOL
