@@ -108,6 +108,10 @@ template <int K, bool CONSTC, int KEEP>
 __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
   if (a.stop && *a.stop) return;
   constexpr int KL = KEEP < K ? KEEP : K;  // kept (LDS-served) projection re-reads
+  // the next KR vectors' re-reads served from registers: their row r + 1 (loaded for the
+  // update) and row r (the previous step's) both held -- 8 VGPRs each (K = 18, 19: every
+  // re-read on chip within two waves per SIMD)
+  constexpr int KR = KL > 0 ? (K - KL < 2 ? K - KL : 2) : 0;
   constexpr int kB = KL > 0 ? 4 : 8;       // batch of the remaining vectors' loads
   __shared__ double2 coef[K];
   __shared__ double2 urow[2][kT + 2];
@@ -137,6 +141,7 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
   // basis row r + 1 of the first KL vectors, held from the update's load until row r's
   // projections are done, then copied to vkeep for row r + 1's projections
   double2 hold[KL > 0 ? KL : 1];
+  double2 rnext[KR > 0 ? KR : 1], rcur[KR > 0 ? KR : 1];  // rows r + 1 and r, k in [KL, KL + KR)
   // u_K at (r, col): w_{K-1} - sum_k c_k u_k in k order; the first KL loads issued together
   // (one memory round trip), the rest in batches of kB in a runtime loop (a fully unrolled
   // loop keeps ~16 VGPRs per vector live)
@@ -167,11 +172,18 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    if constexpr (KR > 0) {
+#pragma unroll
+      for (int q = 0; q < KR; ++q) rnext[q] = ld_at(vrow + (size_t)(KL + q) * a.ldv, bo);
+#pragma unroll
+      for (int q = 0; q < KR; ++q) w = csub(w, cmul(coef[KL + q + kz], rnext[q]));
+    }
 #pragma unroll 1
-    for (int k0 = KL; k0 < K; k0 += kB) {
+    for (int k0 = KL + KR; k0 < K; k0 += kB) {
       double2 v[kB];
 #pragma unroll
-      for (int q = 0; q < kB; ++q) v[q] = ld_at(vrow + (size_t)min(k0 + q, K - 1) * a.ldv, bo);
+      for (int q = 0; q < kB; ++q)
+        v[q] = ld_at(vrow + (size_t)min(k0 + q, K - 1) * a.ldv, bo);
 #pragma unroll
       for (int q = 0; q < kB; ++q)
         if (k0 + q < K) w = csub(w, cmul(coef[k0 + q + kz], v[q]));
@@ -182,20 +194,30 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
     return row_value<1>(a, rlo, rhi, r, col, w);
   };
   // u_K at one point, lane-parallel (the edge waves: lane k of each half takes the term
-  // c_k u_k, summed by shuffles -- one load round trip instead of ceil(K / kB) batches)
-  auto unew1 = [&](int r, int c) {
+  // c_k u_k, summed by shuffles -- one load round trip instead of ceil(K / kB) batches).  Its
+  // two loads are issued before the strip's own row (unew), so that both round trips overlap:
+  // the edge waves otherwise waited on a second one every row, and the block's barrier with them
+  struct EdgeLd {
+    double2 wv, vk;
+  };
+  auto unew1_issue = [&](int r, int c) {
     const int k = lane & 31;
     const int rc = min(max(r, rlo), rhi - 1);
     const ptrdiff_t p = (ptrdiff_t)rc * n + c;
-    const double2 wv = a.win[p];
-    const double2 vk = (a.V + p)[(size_t)min(k, K - 1) * a.ldv];
-    double2 tk = csel(k < K, cmul(coef[min(k, K - 1)], vk), z);
+    EdgeLd e;
+    e.wv = a.win[p];
+    e.vk = (a.V + p)[(size_t)min(k, K - 1) * a.ldv];
+    return e;
+  };
+  auto unew1_finish = [&](int r, int c, const EdgeLd& e) {
+    const int k = lane & 31;
+    double2 tk = csel(k < K, cmul(coef[min(k, K - 1)], e.vk), z);
 #pragma unroll
     for (int off = 16; off > 0; off >>= 1) {
       tk.x += __shfl_xor(tk.x, off);
       tk.y += __shfl_xor(tk.y, off);
     }
-    return row_value<1>(a, rlo, rhi, r, c, csub(wv, tk));
+    return row_value<1>(a, rlo, rhi, r, c, csub(e.wv, tk));
   };
   const double2 AW = a.tab_i[ic], AE = a.tab_i[n + ic], R1 = a.tab_i[2 * n + ic];
   double2 acc[K + 1];
@@ -209,13 +231,17 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
 #pragma unroll
       for (int q = 0; q < KL; ++q) vkeep[q][t] = hold[q];
     }
+#pragma unroll
+    for (int q = 0; q < KR; ++q) rcur[q] = rnext[q];
     int buf = 0;
     for (int r0 = rb; r0 < re; ++r0) {
       int r = r0;
       asm volatile("" : "+s"(r), "+s"(kz));
+      EdgeLd el{z, z};
+      if (ew || ee) el = unew1_issue(r, ie);  // (wave-uniform: the two edge waves only)
       const double2 uN = unew(r + 1, (unsigned)ic);
       double2 ue = z;
-      if (ew || ee) ue = unew1(r, ie);  // (wave-uniform: the two edge waves only)
+      if (ew || ee) ue = unew1_finish(r, ie, el);
       urow[buf][1 + t] = csel(act, uC, z);
       if (ew && lane == 0) urow[buf][0] = csel(ehas, ue, z);
       if (ee && lane == kWave - 1) urow[buf][kT + 1] = csel(ehas, ue, z);
@@ -260,11 +286,13 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+#pragma unroll
+      for (int q2 = 0; q2 < KR; ++q2) acc[KL + q2] = cfma_conj(rcur[q2], w, acc[KL + q2]);
       // the remaining re-reads from the memory system, kB in flight
       gd2* vr = gptr(a.V + (size_t)r * n);
       asm volatile("" : "+s"(vr));
 #pragma unroll
-      for (int k0 = KL; k0 < K; k0 += kB) {
+      for (int k0 = KL + KR; k0 < K; k0 += kB) {
         double2 v[kB];
 #pragma unroll
         for (int q2 = 0; q2 < kB; ++q2)
@@ -279,6 +307,8 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
 #pragma unroll
         for (int q2 = 0; q2 < KL; ++q2) vkeep[q2][t] = hold[q2];
       }
+#pragma unroll
+      for (int q2 = 0; q2 < KR; ++q2) rcur[q2] = rnext[q2];
       uS = uC;
       uC = uN;
       buf ^= 1;
@@ -610,15 +640,19 @@ static_assert(kFusedMaxK == 20, "table covers 1..kFusedMaxK");
 
 }  // namespace
 
-// Band height: 8 rows at 1024^2, 32 from 4096^2 (profiles/r03t/r03s_ab_rows*); HH_FUSED_ROWS
-// overrides.  The partial rows (one per block) stay within kMaxStreamBlocks.
+// Band height: 8 rows at 1024^2, 32 at 4096^2 (profiles/r03t/r03s_ab_rows*), 64 from 8192^2;
+// HH_FUSED_ROWS overrides.  The partial rows (one per block) stay within kMaxStreamBlocks.
 int fused_iter_rows(int n, int rows) {
   static const int env = [] {
     const char* e = std::getenv("HH_FUSED_ROWS");
     return e ? std::atoi(e) : 0;
   }();
   const long tiles_x = (n + kT - 1) / kT;
-  int R = env > 0 ? env : (int)std::min<long>(32, std::max<long>(8, tiles_x * n / 1024));
+  // (64 rows from n = 8192: 3 % fewer halo-row re-formations, +1.5 % at 8192^2,
+  // profiles/r04/r04g_ab_rows_8192.log; at 4096^2 64-row bands leave too few tiles per CU)
+  int R = env > 0 ? env
+                  : (n >= 8192 ? 64
+                               : (int)std::min<long>(32, std::max<long>(8, tiles_x * n / 1024)));
   while ((long)tiles_x * ((rows + R - 1) / R) > kMaxStreamBlocks) R *= 2;
   return R;
 }

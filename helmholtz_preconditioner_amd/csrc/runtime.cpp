@@ -186,6 +186,7 @@ struct hh_op {
   // GMRES workspace
   double2* V = nullptr;
   int V_cols = 0;
+  size_t ldv = 0;  // distance between consecutive basis vectors (nloc + basis_pad())
   double2* gbuf = nullptr;
   GivensState gs{};
   double* status_h = nullptr;
@@ -781,7 +782,7 @@ int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double*
   const int H = sl ? 2 : 1;
   const bool lo_x = c->world > 1 && c->rank > 0;
   const bool hi_x = c->world > 1 && c->rank < c->world - 1;
-  const size_t ldv = op->nloc;
+  const size_t ldv = op->ldv;
   double2* uout = op->V + (size_t)K * ldv;
   const int width = 2 * (K + 1) + 2;
   const int rows_rank = op->je - op->jb;
@@ -899,12 +900,26 @@ void check_sweep_chain(hh_op* op) {
   }
 }
 
+// Padding between consecutive basis vectors, in complex elements (HH_BASIS_PAD overrides).
+// Unpadded, the K vectors a Krylov pass streams together sit exactly nloc * 16 B apart (1 GiB
+// at 8192^2): 4 KiB + 256 B between them measured +3 % for the one-pass iteration at 8192^2
+// (316.6 -> 326.0 it/s; 256 B +1.5 %, 2.3 / 8.3 / 64.3 KiB +1.5-2.5 %,
+// profiles/r04/r04h_ab_pad_c4.log, r04i_ab_nt_c4.log)
+size_t basis_pad() {
+  static const size_t pad = [] {
+    const char* e = std::getenv("HH_BASIS_PAD");
+    return e ? (size_t)std::atol(e) : (size_t)272;
+  }();
+  return pad;
+}
+
 void ensure_gmres(hh_op* op, int restart) {
   REQUIRE(restart >= 1 && restart <= kMaxProj - 1, "restart must be in [1, %d]", kMaxProj - 1);
   if (op->V && op->V_cols >= restart + 1) return;
   dfree(op->V);
+  op->ldv = op->nloc + basis_pad();
   dfree(op->gbuf);
-  op->V = dalloc<double2>(op->nloc * (size_t)(restart + 1));
+  op->V = dalloc<double2>(op->ldv * (size_t)(restart + 1));
   op->V_cols = restart + 1;
   const int R1 = restart + 1;
   const size_t nH = (size_t)restart * R1, nG = 2 * (size_t)restart, nS = R1, nY = restart;
@@ -2066,7 +2081,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
   if (restart > (long)op->n * op->n) restart = (int)((long)op->n * op->n);
   ensure_gmres(op, restart);
   const size_t L = op->nloc;
-  const size_t ldv = L;
+  const size_t ldv = op->ldv;
   double2* V = op->V;
   const double2* b = bv->d;
   double2* x = xv->d;
