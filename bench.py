@@ -331,10 +331,11 @@ def gmres_path_bytes(args, its, bpp, N, path):
     unknown: the one-pass iteration moves, at iteration j of a cycle, j = 0: the
     cycle's first M A (bpp) + its projection (u_0, w_0: 32 B); j >= 1: ONE pass, w_{j-1} and
     the j basis vectors read, u_j and w_j written -- 16 (j + 3) B, + 8 B of 1/c^2 for a
-    non-constant medium (the operator's bpp is 32 + 8 then) --; the cycle's last update adds
-    16 (R + 1) B.  The regular and lagged cycles move the CGS bytes of gmres_bytes (the SpMV,
-    then the basis twice).  Per-cycle extras (x update, residual) are left out of both, as in
-    gmres_bytes.  (PMC counters cannot run inside the timed solve: the pass's measured
+    non-constant medium (the operator's bpp is 32 + 8 then) --; the end of the cycle, in which
+    the last update's norm and the x update share one pass (fused.hip cycle_end_kernel: R basis
+    vectors, w and x read, x and V b written; then x += y V b), adds 16 (R + 4 + 3) B.  The
+    regular and lagged cycles move the CGS bytes of gmres_bytes (the SpMV, then the basis
+    twice; their x update is left out, as is every cycle's residual).  (PMC counters cannot run inside the timed solve: the pass's measured
     traffic per K is in profiles/r04_pmc_fused.json.)"""
     if path != "one-pass":
         return gmres_bytes(args, its, bpp, N)[0]
@@ -345,7 +346,7 @@ def gmres_path_bytes(args, its, bpp, N, path):
         j = i % R
         total += (bpp + 32) * N if j == 0 else (16 * (j + 3) + ic) * N
         if j == R - 1:
-            total += 16 * (R + 1) * N
+            total += 16 * (R + 7) * N
     return total
 
 

@@ -593,6 +593,129 @@ __global__ __launch_bounds__(kT) void fused_edge_kernel(const FusedArgs a, int r
   a.uout[p] = w;
 }
 
+// ------------------------------------------------------------ the end of a full cycle
+// A one-pass cycle that reaches its last column (col = stop_col) still owes: the last update
+// u_{col+1} = w_col - sum_k c_k u_k, whose norm is the Hessenberg subdiagonal h1 of column col;
+// then the triangular solve for y and x += sum_k y_k v_k (scipy iterative.py:817-824) -- two
+// more passes over the K = col + 1 basis vectors (update_kernel, then xupdate_kernel).  y
+// depends on h1 only through its last entry: with the rotations of columns < col known, the
+// back-substitution is affine in y_col, y = a + y_col b (a: y_col = 0, b: the response to
+// y_col = 1).  So ONE pass forms |u_{col+1}|^2 and, from the same loads, x + sum a_k v_k
+// (in place) and vb = sum b_k v_k (into V[K], the vector u_{col+1} would have occupied); once
+// the last column is finished, x += y_col vb.  K + 2 vector reads and 2 writes, then 2 + 1,
+// instead of 2 K + 2 and 2.
+
+// a, b of y = a + y_col b, scaled by the basis scales (x += sum (a_k + y_col b_k) v_k / sigma_k):
+// ab[k] = a_k vscale_k, ab[kMaxProj + k] = b_k vscale_k, k <= col.  Column col as started by
+// gmres_lag_kernel (unrotated); the previous columns final.  One thread (once per cycle).
+__global__ void cycle_coef_kernel(GivensState g, int col, double2* ab) {
+  if (threadIdx.x != 0 || g.ctrl[0]) return;  // (the cycle stopped before its last column)
+  const int R1 = g.restart + 1;
+  auto H = [&](int c, int k) { return g.H[(size_t)c * R1 + k]; };
+  // column col's rows < col after the previous rotations (gmres_finish_column's chain)
+  double2 hc[kMaxProj];
+  double2 n0 = H(col, 0);
+  for (int k = 0; k < col; ++k) {
+    const double c = g.G[2 * k].x;
+    const double2 sk = g.G[2 * k + 1], n1 = H(col, k + 1);
+    hc[k] = cadd(cscale(n0, c), cmul(sk, n1));
+    n0 = cadd(cmul(make_double2(-sk.x, sk.y), n0), cscale(n1, c));
+  }
+  double2 ya[kMaxProj], yb[kMaxProj];
+  ya[col] = make_double2(0.0, 0.0);
+  yb[col] = make_double2(1.0, 0.0);
+  for (int k = col - 1; k >= 0; --k) {
+    double2 sa = g.S[k], sb = cneg(hc[k]);
+    for (int m = k + 1; m < col; ++m) {
+      const double2 hmk = H(m, k);
+      sa = csub(sa, cmul(ya[m], hmk));
+      sb = csub(sb, cmul(yb[m], hmk));
+    }
+    ya[k] = cdiv_smith(sa, H(k, k));
+    yb[k] = cdiv_smith(sb, H(k, k));
+  }
+  for (int k = 0; k <= col; ++k) {
+    ab[k] = cscale(ya[k], g.vscale[k]);
+    ab[kMaxProj + k] = cscale(yb[k], g.vscale[k]);
+  }
+}
+
+// |w - sum_k c_k V_k|^2 block partials (update_kernel's coefficients and term order), x += sum
+// a_k V_k in place, vb = sum b_k V_k.  Coefficients in LDS (3 K complex: registers would not
+// hold them), the K loads in batches of 8.
+template <int K>
+__global__ __launch_bounds__(kT) void cycle_end_kernel(const double2* __restrict__ V, size_t ldv,
+                                                       const double* __restrict__ raw,
+                                                       const double* __restrict__ vscale,
+                                                       const double2* __restrict__ ab,
+                                                       const double2* w, double2* x, double2* vb,
+                                                       size_t len, double* partials,
+                                                       const int* stop) {
+  if (stop && *stop) return;
+  __shared__ double2 cu[K], ca[K], cb[K];
+  const int t = threadIdx.x;
+  if (t < K) {
+    const double sk = vscale[t];
+    cu[t] = cscale(cscale(make_double2(raw[2 * t], raw[2 * t + 1]), sk), sk);
+    ca[t] = ab[t];
+    cb[t] = ab[kMaxProj + t];
+  }
+  __syncthreads();
+  double nrm = 0.0;
+  const size_t stride = (size_t)gridDim.x * kT;
+  for (size_t p = (size_t)blockIdx.x * kT + t; p < len; p += stride) {
+    double2 u = w[p], xa = x[p], b = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int k0 = 0; k0 < K; k0 += 8) {
+      double2 v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = V[(size_t)min(k0 + q, K - 1) * ldv + p];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (k0 + q < K) {
+          u = csub(u, cmul(cu[k0 + q], v[q]));
+          xa = cfma(ca[k0 + q], v[q], xa);
+          b = cfma(cb[k0 + q], v[q], b);
+        }
+    }
+    nrm = fma(u.x, u.x, fma(u.y, u.y, nrm));
+    x[p] = xa;
+    vb[p] = b;
+  }
+  double v1[1] = {nrm};
+  block_reduce_vec<1>(v1, partials, kMaxNorms);
+}
+
+// x += y_col vb once column col is finished: y_col = S[col] / H[col][col] (scipy's rule: S[col]
+// = 0 when H[col][col] == 0, iterative.py:815-816)
+__global__ __launch_bounds__(kT) void cycle_finish_kernel(GivensState g, int col,
+                                                          const double2* vb, double2* x,
+                                                          size_t len) {
+  const int R1 = g.restart + 1;
+  const double2 hcc = g.H[(size_t)col * R1 + col];
+  const double2 sc = g.S[col];
+  const double2 y = (hcc.x == 0.0 && hcc.y == 0.0) ? make_double2(0.0, 0.0) : cdiv_smith(sc, hcc);
+  const size_t stride = (size_t)gridDim.x * kT;
+  for (size_t p = (size_t)blockIdx.x * kT + threadIdx.x; p < len; p += stride)
+    x[p] = cfma(y, vb[p], x[p]);
+}
+
+template <int K>
+void cycle_end_launch(const double2* V, size_t ldv, const double* raw, const double* vscale,
+                      const double2* ab, const double2* w, double2* x, double2* vb, size_t len,
+                      double* partials, int blocks, hipStream_t s, const int* stop) {
+  hipLaunchKernelGGL((cycle_end_kernel<K>), dim3(blocks), dim3(kT), 0, s, V, ldv, raw, vscale,
+                     ab, w, x, vb, len, partials, stop);
+}
+template <int... Ks>
+struct CTable {
+  using FN = void (*)(const double2*, size_t, const double*, const double*, const double2*,
+                      const double2*, double2*, double2*, size_t, double*, int, hipStream_t,
+                      const int*);
+  static constexpr FN f[] = {cycle_end_launch<Ks>...};
+};
+using CycleTable = CTable<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21>;
+
 // basis vectors whose re-read comes from the LDS copy (HH_FUSED_KEEP = 0 turns the copy off;
 // read per launch so one process can A/B it)
 int fused_keep() {
@@ -666,6 +789,18 @@ void launch_fused_iter(int K, const FusedArgs& a, int blocks, hipStream_t stream
 void launch_fused_edge(int K, const FusedArgs& a, int r0, int c0, int r1, int c1,
                        hipStream_t stream) {
   if (c0 + c1 > 0) FusedTable::e[K - 1](a, r0, c0, r1, c1, stream);
+}
+void launch_cycle_coef(const GivensState& g, int col, double2* ab, hipStream_t stream) {
+  hipLaunchKernelGGL(cycle_coef_kernel, dim3(1), dim3(kWave), 0, stream, g, col, ab);
+}
+void launch_cycle_end(int K, const double2* V, size_t ldv, const double* raw, const double* vscale,
+                      const double2* ab, const double2* w, double2* x, double2* vb, size_t len,
+                      double* partials, int blocks, hipStream_t stream, const int* stop) {
+  CycleTable::f[K - 1](V, ldv, raw, vscale, ab, w, x, vb, len, partials, blocks, stream, stop);
+}
+void launch_cycle_finish(const GivensState& g, int col, const double2* vb, double2* x, size_t len,
+                         int blocks, hipStream_t stream) {
+  hipLaunchKernelGGL(cycle_finish_kernel, dim3(blocks), dim3(kT), 0, stream, g, col, vb, x, len);
 }
 
 }  // namespace hh

@@ -256,6 +256,18 @@ void launch_fused_iter(int K, const FusedArgs& a, int blocks, hipStream_t stream
 void launch_fused_edge(int K, const FusedArgs& a, int r0, int c0, int r1, int c1,
                        hipStream_t stream);
 
+// The end of a one-pass cycle that reaches its last column col (fused.hip): cycle_coef writes
+// ab[k] = a_k s_k, ab[kMaxProj + k] = b_k s_k (y = a + y_col b, k <= col; a no-op once the
+// stop flag is up); cycle_end forms the last update's |u|^2 partials (partials[blk][kMaxNorms])
+// and, from the same loads, x += sum a_k s_k V_k in place and vb = sum b_k s_k V_k over K =
+// col + 1 vectors; after the last column is finished, cycle_finish does x += y_col vb.
+void launch_cycle_coef(const GivensState& g, int col, double2* ab, hipStream_t stream);
+void launch_cycle_end(int K, const double2* V, size_t ldv, const double* raw, const double* vscale,
+                      const double2* ab, const double2* w, double2* x, double2* vb, size_t len,
+                      double* partials, int blocks, hipStream_t stream, const int* stop);
+void launch_cycle_finish(const GivensState& g, int col, const double2* vb, double2* x, size_t len,
+                         int blocks, hipStream_t stream);
+
 // After multidot+update reductions: column `col` of H from raw dots (red_dots, 2*(col+1)
 // doubles + |w|^2 at [2*(col+1)]) and |w_new|^2 (red_norm[0]).  Then scipy's inner-loop
 // exit test (iterative.py:792-795) on the device: presid <= ptol, breakdown, or

@@ -228,6 +228,7 @@ struct hh_op {
   unsigned long long* sw_prof = nullptr;  // diagnostic phase ticks (hh_op_sweep_profile)
   unsigned long long* sw_chain = nullptr;  // granules of the persistent apply chain, or null
   double2* fw = nullptr;        // one-pass GMRES iteration: the w_j ping-pong pair [2][nloc]
+  double2* cab = nullptr;       // its cycle end: y = a + y_col b coefficients [2][kMaxProj]
   unsigned sw_seq = 0;                     // its launch sequence number
   double2* sw_u = nullptr;      // dense apply scratch (n^2)
   double2* sw_in = nullptr;     // dense apply: fixed input / output the captured graphs use
@@ -1297,6 +1298,7 @@ static void op_release(hh_op* op) {
   dfree(op->gbuf);
   dfree(op->npart);
   dfree(op->fw);
+  dfree(op->cab);
   dfree(op->small_scr);
   dfree(op->small_ticks);
   dfree(op->kcount);
@@ -2187,6 +2189,15 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
   }
 
   if (fused && !op->fw) op->fw = dalloc<double2>(2 * L);
+  if (fused && !op->cab) op->cab = dalloc<double2>(2 * kMaxProj);
+  // the end of a full one-pass cycle in one pass over the basis (fused.hip cycle_end_kernel:
+  // the last update's norm, x += V a and V b together; HH_CYCLE_MERGE=0: update, then the
+  // triangular solve and xupdate)
+  static const bool merge_env = [] {
+    const char* e = std::getenv("HH_CYCLE_MERGE");
+    return !(e && e[0] == '0');
+  }();
+  const bool merge_end = fused && merge_env;
   double r0 = bnrm2;  // (x0 = 0: r = b)
   if (x_any) {
     residual(op, b, x, V, 4);  // V[0] = M (b - A x0); red[4..5]
@@ -2401,8 +2412,14 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       {  // the last column's update and the norm that completes it
         const int K = stop_col + 1;
         hipEvent_t k0 = tmark(op, s);
-        launch_update(V, ldv, K, op->red + 16, g.vscale, Wb[stop_col & 1],
-                      V + (size_t)(stop_col + 1) * ldv, L, op->npart, blocks, s, stp);
+        if (merge_end) {  // (with x += V a, V b: see cycle_coef_kernel)
+          launch_cycle_coef(g, stop_col, op->cab, s);
+          launch_cycle_end(K, V, ldv, op->red + 16, g.vscale, op->cab, Wb[stop_col & 1], x,
+                           V + (size_t)K * ldv, L, op->npart, blocks, s, stp);
+        } else {
+          launch_update(V, ldv, K, op->red + 16, g.vscale, Wb[stop_col & 1],
+                        V + (size_t)K * ldv, L, op->npart, blocks, s, stp);
+        }
         tspan(op, HH_SPAN_UPDATE, k0, tmark(op, s));
         launch_reduce(op->npart, blocks, kMaxNorms, 1, op->red + 8, s, stp);
         allreduce_sum_dev(op, op->red + 8, 1);
@@ -2529,8 +2546,13 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     presid = sth[4 * col];
     breakdown = sth[4 * col + 1] != 0.0;
     op->stats.restarts++;
-    launch_gmres_solve(g, col, s);
-    launch_xupdate(V, ldv, col + 1, g.ycoef, x, L, blocks, s);
+    if (merge_end && col == stop_col) {
+      // (the cycle reached its last column, so cycle_end ran: x already holds x + V a)
+      launch_cycle_finish(g, col, V + (size_t)(col + 1) * ldv, x, L, blocks, s);
+    } else {
+      launch_gmres_solve(g, col, s);
+      launch_xupdate(V, ldv, col + 1, g.ycoef, x, L, blocks, s);
+    }
     residual(op, b, x, V, 4);  // r = b - A x; V[0] = M r for the next cycle
     read_dev(op, op->red + 4, st, 1);
     check_sweep_chain(op);  // (the M r of the last cycle is never read by a cycle report)
