@@ -2232,6 +2232,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     }
   };
   bool small_refused = false;
+  long cycles_done = 0;  // restart cycles the small-grid kernel completed before a refusal
   op->last_path = small ? 1 : (fused ? 3 : 0);
   if (small) {
     // Small grids: whole-cycle launches (gmres_small.hip), each running up to kSmallBatch restart
@@ -2256,7 +2257,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     HIPC(hipMemcpyAsync(outer, outer_h, kOuterDoubles * sizeof(double), hipMemcpyHostToDevice, s));
     const int cap = op->cycle_cb ? 1 : kSmallBatch;
     const Slab& sl = op->slabs[0];
-    long iteration = 0;
+    long iteration = 0, launches = 0;
     bool done = false;
     while (!done && iteration < maxiter) {
       // (legacy: maxiter caps inner iterations, so no more cycles than those left can run)
@@ -2296,11 +2297,18 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         sa.obuf = sa.mbuf + 4 * (size_t)op->n * op->n;
         sa.gate_decide = sa.obuf + 8;
         sa.gate_arrive = reinterpret_cast<unsigned*>(sa.gate_decide + 1);
-        static const bool force_abort = [] {  // test hook: the gate refuses the grid
+        // test hooks: the gate refuses every launch (HH_SMALL_COOP_REFUSE=1), or only the
+        // solve's launch number HH_SMALL_REFUSE_AT (1-based: 2 = the second batch)
+        static const bool force_abort = [] {
           const char* e = std::getenv("HH_SMALL_COOP_REFUSE");
           return e && e[0] == '1';
         }();
-        sa.gate_force_abort = force_abort ? 1 : 0;
+        static const long refuse_at = [] {
+          const char* e = std::getenv("HH_SMALL_REFUSE_AT");
+          return e ? std::atol(e) : 0L;
+        }();
+        ++launches;
+        sa.gate_force_abort = (force_abort || launches == refuse_at) ? 1 : 0;
         // P consecutive sequence numbers, none 0 (tag 0 is the zeroed scratch)
         if (((op->small_seq + (unsigned)P) & 0xffffffu) < (unsigned)P) op->small_seq = 0;
         sa.seq = (op->small_seq + 1) & 0xffffffu;
@@ -2311,13 +2319,8 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         sa.outer = outer;
         const hipError_t le = launch_small_cycle(sa, op->const_c, op->pkind == HH_PREC_JACOBI, s);
         if (le != hipSuccess) {
-          // refused before anything of the cycle ran (cooperative launch: e.g. the grid cannot
-          // be co-resident): the first launch of the solve falls back to the regular cycle, which
-          // starts from the same state (V[0] = M r, red[4..5]); a later refusal cannot, as cycles
-          // already changed x
-          REQUIRE(iteration == 0,
-                  "small-grid GMRES: cooperative launch refused after %ld cycles (%s)", iteration,
-                  hipGetErrorString(le));
+          // refused before anything of the batch ran (cooperative launch: e.g. the grid cannot
+          // be co-resident): the regular cycle takes over below, at this restart boundary
           small_refused = true;
         }
       }
@@ -2325,9 +2328,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       HIPC(hipStreamSynchronize(s));
       if (reinterpret_cast<const int*>(op->status_h + kRedDoubles + kRedCtrl)[0] == 3) {
         // the kernel's co-residency gate refused the grid before any workgroup touched state
-        REQUIRE(iteration == 0,
-                "small-grid GMRES: workgroups not co-resident after %ld cycles (the GPU is "
-                "shared?); hh_op_set_small_cycle(op, 0) selects the regular cycle", iteration);
+        // (the GPU shared with another process?): the regular cycle takes over below
         small_refused = true;
         break;
       }
@@ -2370,10 +2371,23 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       finish(inner, rnorm <= atol ? 0 : (int)std::min<long>(maxiter, 0x7fffffff), rnorm);
       return HH_OK;
     }
-    op->last_path = 2;  // refused: the regular cycle below runs the whole solve
+    // Refused: the regular cycle below runs the rest of the solve.  A batch starts at a restart
+    // boundary and a refusal leaves the cycle state untouched, so it resumes from exactly where
+    // the last completed cycle left it: x, V[0] = M r and red[4..5] (|r|^2, |M r|^2) of the
+    // current x -- each cycle's tail computes them for the next --, and scipy's restart-loop
+    // state the kernel carried on the device (ptol, ptol_max_factor; `inner` and the cycle
+    // count are the host's own, from the replayed reports).
+    op->last_path = 2;
+    cycles_done = iteration;
+    if (iteration > 0) {
+      double o[kOuterDoubles];
+      read_dev(op, outer, o, kOuterDoubles);
+      ptol = o[0];
+      ptol_max_factor = o[1];
+    }
   }
 
-  for (long iteration = 0; iteration < maxiter; ++iteration) {
+  for (long iteration = cycles_done; iteration < maxiter; ++iteration) {
     // v[0] = psolve(r) / ||psolve(r)||, S[0] = ||psolve(r)|| (lazy scale); clears the stop flag
     launch_gmres_start(g, op->red, 4, mnorm_slot(op, 4), s);
     // The whole cycle is queued at once: the column kernel evaluates scipy's inner exit test

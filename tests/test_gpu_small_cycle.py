@@ -8,6 +8,7 @@ maxiter ending inside a cycle, restart 1 and 7, ragged n (block sizes not a mult
 wave, one-row grids), both media kinds.
 """
 import os
+import tempfile
 
 import numpy as np
 import pytest
@@ -242,3 +243,46 @@ print("ok")
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
                        text=True, timeout=240)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_small_cycle_refusal_after_cycles_hands_over():
+    """A refusal after cycles have run (simulated: HH_SMALL_REFUSE_AT=2 makes the gate refuse the
+    solve's second launch, after the first batch of 16 restart cycles) hands the solve to the
+    regular cycle at that restart boundary -- x, V[0] = M r, |r|^2, |M r|^2 and the device's
+    ptol state as the last completed cycle left them -- instead of failing: same info and
+    history (1e-9) as the uninterrupted small-cycle solve.  Child processes: the knob is read
+    once per process."""
+    import subprocess
+    import sys
+    code = r'''
+import numpy as np, sys
+sys.path.insert(0, ".")
+sys.path.insert(0, "tests")
+import helmholtz_preconditioner_amd as H
+from conftest import medium
+from oracle import helmholtz_oracle as O
+n, b, C, wn = 37, 6, 61.0, 3.0
+om, h, eta = O.problem_params(n, b, wn, 2.0)
+A = H.build_A_matrix(b, C, eta, om, h, n, medium("c1", n))
+f = O.init_f1_mat(.5, .125, om, n).ravel()
+A.small_cycle("on")
+x, info, hist = H.gmres(A, f, rtol=1e-3, restart=2, maxiter=40, callback=lambda r: None,
+                        callback_type="legacy", return_history=True)
+np.savez(sys.argv[1], x=x, info=info, hist=hist, path=A.last_solve_path())
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    with tempfile.TemporaryDirectory() as td:
+        for at in ("0", "2"):
+            out = os.path.join(td, f"r{at}.npz")
+            env = dict(os.environ, HH_SMALL_REFUSE_AT=at)
+            r = subprocess.run([sys.executable, "-c", code, out], cwd=root, env=env,
+                               capture_output=True, text=True, timeout=240)
+            assert r.returncode == 0, r.stdout + r.stderr
+            res.append(np.load(out))
+    a, b = res
+    assert str(a["path"]) == "small-cycle" and str(b["path"]) == "small-cycle refused -> regular"
+    assert int(a["info"]) == int(b["info"]) and len(a["hist"]) == len(b["hist"]) == 40
+    assert np.array_equal(a["hist"][:32], b["hist"][:32])  # (the 16 cycles before the refusal)
+    assert np.all(np.abs(a["hist"] - b["hist"]) <= 1e-9 * np.abs(a["hist"]) + 1e-15)
+    assert np.linalg.norm(a["x"] - b["x"]) <= 1e-9 * np.linalg.norm(a["x"])
