@@ -20,6 +20,33 @@ if not os.path.exists(LIB_PATH):
 
 lib = ctypes.CDLL(LIB_PATH)
 
+# Every live handle (vectors, operators, contexts) is released by an atexit hook, vectors first:
+# an object a garbage collector never finalises would otherwise still own device memory, streams
+# and an RCCL communicator when the HIP runtime's own exit handlers run -- after a profiler
+# (rocprofv3) has finalised its hooks, which is where such late releases crashed
+# (profiles/r03i: SIGSEGV inside exit()).  Python atexit hooks run before the C runtime's.
+import atexit  # noqa: E402
+import weakref  # noqa: E402
+
+_LIVE = (weakref.WeakSet(), weakref.WeakSet(), weakref.WeakSet())  # vectors, operators, contexts
+
+
+def track(obj, rank: int) -> None:
+    """register a handle owner for release at exit (rank 0 vector, 1 operator, 2 context)"""
+    _LIVE[rank].add(obj)
+
+
+def release_all() -> None:
+    for live in _LIVE:
+        for obj in list(live):
+            try:
+                obj.close()
+            except Exception:  # pragma: no cover - best effort at interpreter exit
+                pass
+
+
+atexit.register(release_all)
+
 c_int, c_long, c_double, c_void_p = ctypes.c_int, ctypes.c_long, ctypes.c_double, ctypes.c_void_p
 c_dp = ctypes.POINTER(ctypes.c_double)
 c_ip = ctypes.POINTER(ctypes.c_int)

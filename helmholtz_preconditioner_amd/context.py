@@ -37,6 +37,7 @@ class Context:
         check(lib.hh_ctx_create_ex(device, rank, world, idbuf, virtual_slabs, kinds[transport],
                                    ctypes.byref(h)))
         self._h = h
+        _ffi.track(self, 2)
 
     @property
     def handle(self):

@@ -21,6 +21,8 @@
 // launches).  Solve shape: see bt_solve.
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
+#include <cstdlib>
+
 #include "sweep.hpp"
 #include "hh_error.hpp"
 
@@ -1058,9 +1060,10 @@ void launch_part(const void* fn, const SweepArgs& a, double2* u, double2* uF, hi
   if (e == hipSuccess) {
     SweepArgs arg = a;
     void* params[] = {&arg, &u, &uF};
-    e = a.G > 1 ? hipLaunchCooperativeKernel(fn, dim3(a.G), dim3(kPartThreads), params,
-                                             (unsigned)lds, st)
-                : hipLaunchKernel(fn, dim3(1), dim3(kPartThreads), params, lds, st);
+    e = a.G > 1 && sweep_coop_launch()
+            ? hipLaunchCooperativeKernel(fn, dim3(a.G), dim3(kPartThreads), params,
+                                         (unsigned)lds, st)
+            : hipLaunchKernel(fn, dim3(a.G), dim3(kPartThreads), params, lds, st);
   }
   if (e != hipSuccess) {
     (void)hipGetLastError();
@@ -1129,6 +1132,14 @@ bool sweep_part_ys_lds(int B, int G, int n) {
        : B == 12 ? part_ys_lds<12>(G, n) : part_ys_lds<16>(G, n);
 }
 size_t sweep_part_granules(int G) { return (size_t)2 * 2 * G * kSweepGranStride; }
+
+bool sweep_coop_launch() {
+  static const bool coop = [] {
+    const char* e = std::getenv("HH_SWEEP_COOP");
+    return !(e && e[0] == '0');
+  }();
+  return coop;
+}
 
 int sweep_block(int b) { return b <= 4 ? 4 : (b <= 8 ? 8 : (b <= 12 ? 12 : (b <= 16 ? 16 : 0))); }
 

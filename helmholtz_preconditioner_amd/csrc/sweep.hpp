@@ -50,6 +50,14 @@ template <int B>
 __host__ __device__ constexpr int pidx(int j, int c) {
   return (c % (B / 2)) * 2 * B + (c / (B / 2)) * B + j;
 }
+// Grid-wide sweeps (the partitioned block-Thomas solves over G > 1 workgroups, the dense
+// form's persistent chain) are cooperative launches, so a grid that cannot be co-resident fails
+// at launch; HH_SWEEP_COOP=0 launches them as plain kernels, whose grid-wide waits are bounded
+// anyway (a timeout word the host checks).  (ROCm 7.2 + rocprofv3: a process that made ANY
+// cooperative launch dies with SIGSEGV inside exit() -- libamdhip64's exit handler tearing down
+// an HSA queue after rocprofiler-sdk finalised, tools/exit_probe.py; profiling runs
+// of the sweep set HH_SWEEP_COOP=0.)
+bool sweep_coop_launch();
 int sweep_block(int b);
 size_t sweep_scratch_per_wave(int n);  // padded block size B (4, 8, 12, 16) or 0 if b > 16
 // what: 0 factor (one wave per system), 1 forward sweep, 2 middle sweep, 3 backward sweep,

@@ -492,11 +492,14 @@ void launch_chain_t(const ChainArgs& c, hipStream_t st) {
   void* params[] = {&arg};
   const dim3 grid((c.n + kChainRows - 1) / kChainRows), block(kChainThreads);
   // cooperative: the launch fails instead of hanging if the grid cannot be co-resident
-  const hipError_t e = hipLaunchCooperativeKernel(
-      reinterpret_cast<const void*>(&sweep_chain_kernel<J>), grid, block, params, (unsigned)lds, st);
+  // (HH_SWEEP_COOP=0: a plain launch; the chain's waits are bounded either way)
+  const void* fn = reinterpret_cast<const void*>(&sweep_chain_kernel<J>);
+  const hipError_t e = sweep_coop_launch()
+                           ? hipLaunchCooperativeKernel(fn, grid, block, params, (unsigned)lds, st)
+                           : hipLaunchKernel(fn, grid, block, params, lds, st);
   if (e != hipSuccess) {
     (void)hipGetLastError();
-    fail(HH_ERR_HIP, "sweep chain: cooperative launch of %u workgroups failed (%s)", grid.x,
+    fail(HH_ERR_HIP, "sweep chain: launch of %u workgroups failed (%s)", grid.x,
          hipGetErrorString(e));
   }
 }

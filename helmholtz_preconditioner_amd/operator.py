@@ -71,6 +71,7 @@ class DeviceVector:
         h = ctypes.c_void_p()
         check(lib.hh_vec_create(op.handle, ctypes.byref(h)))
         self._h = h
+        _ffi.track(self, 0)
         if data is not None:
             self.upload(data)
 
@@ -125,6 +126,7 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
                                None if host is None else _ffi.dptr(host), float(c_const),
                                mass.real, mass.imag, ctypes.byref(hnd)))
         self._h = hnd
+        _ffi.track(self, 1)
         jb, je = ctypes.c_int(), ctypes.c_int()
         check(lib.hh_op_local_rows(hnd, ctypes.byref(jb), ctypes.byref(je)))
         self.row_begin, self.row_end = jb.value, je.value

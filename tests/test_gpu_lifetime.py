@@ -4,11 +4,13 @@ Releasing a handle never frees an object that another live object still uses: a 
 outlives its operators and an operator its vectors, whatever order the caller (or a
 garbage collector) releases them in -- and no stale HIP error leaks into a later call.
 """
+import os
+
 import numpy as np
 import pytest
 
 import helmholtz_preconditioner_amd as H
-from conftest import rand_complex
+from conftest import ROOT, rand_complex
 
 pytestmark = pytest.mark.gpu
 
@@ -47,3 +49,55 @@ def test_no_stale_error_after_out_of_order_teardown():
     B = _op(c2, 33)
     xb = rand_complex(B.local_size, 1)
     assert np.all(np.isfinite(B @ xb))
+
+
+_LIVE_AT_EXIT = r'''
+import gc, sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+import helmholtz_preconditioner_amd as H
+ctx = H.Context(device=0)
+n = 160
+om, h, eta = H.problem_params(n, 12, 6.0, 2.0)
+A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.init_c1_mat(.5, .5, n), context=ctx)
+M = H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7)
+x, y = A.vector(np.ones(n * n, complex)), A.vector()
+A.apply_device(x, y)
+u, info = H.gmres(A, H.init_f1_mat(.5, .125, om, n).ravel(), rtol=1e-3, restart=20, maxiter=5,
+                  M=M, callback=lambda r: None, callback_type="legacy")
+Ms = H.Sweeping(A, form="thomas", workgroups=4)  # (a grid-wide, partitioned sweep)
+Ms.configure()
+A.apply_device(x, y, 2)  # (HH_APPLY_PREC)
+assert Ms.partitioned and Ms.workgroups == 4, (Ms.partitioned, Ms.workgroups)
+cycle = [A, M, Ms, x, y, ctx]
+cycle.append(cycle)  # (a reference cycle: no refcount ever reaches zero before exit)
+gc.disable()
+print("exiting with live handles", flush=True)
+'''
+
+
+@pytest.mark.parametrize("profiled", [False, True])
+def test_exit_with_live_handles(tmp_path, profiled):
+    """A fresh process that exits with a live context, operator, shifted-Laplace and sweeping
+    preconditioners and device vectors -- held in a reference cycle with the collector off, so
+    no __del__ runs -- ends with status 0: the package's atexit hook releases vectors, then
+    operators, then contexts, before the HIP runtime's exit handlers (and a profiler's
+    finalisation) run.  Also under rocprofv3 --kernel-trace, where round 3 saw a SIGSEGV inside
+    exit() (profiles/r03i): that one is ROCm's own teardown after any cooperative launch
+    (tools/exit_probe.py, DESIGN 3b), so the profiled run takes the grid-wide sweep as a plain
+    launch (HH_SWEEP_COOP=0)."""
+    import shutil
+    import subprocess
+    import sys
+    cmd = [sys.executable, "-c", _LIVE_AT_EXIT, ROOT]
+    env = dict(os.environ, TMPDIR=str(tmp_path))
+    if profiled:
+        env["HH_SWEEP_COOP"] = "0"
+        rp = shutil.which("rocprofv3")
+        if rp is None:
+            pytest.skip("rocprofv3 not on PATH")
+        cmd = [rp, "--kernel-trace", "--stats", "-d", str(tmp_path / "prof"), "-o", "run",
+               "--output-format", "csv", "--"] + cmd
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "exiting with live handles" in r.stdout

@@ -6,6 +6,8 @@ code.py:345-385) on the device (csrc/sweep.hip, block Thomas instead of SuperLU)
 * corrected (Alg. 2.4) against the oracle's SuperLU restatement: apply 1e-10, GMRES
   history / field 1e-6 (contract).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -269,3 +271,45 @@ def test_sweep_partitioned_workgroups_agree_with_dense(ctx):
         y = M @ x
         assert M.partitioned and M.workgroups == want
         assert relerr(y, yd) < 1e-10
+
+
+_PLAIN_LAUNCH = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import helmholtz_preconditioner_amd as H
+from helmholtz_preconditioner_amd import _ffi
+out = sys.argv[2]
+res = {}
+for n, form in ((300, "thomas"), (255, "dense")):
+    om, h, eta = H.problem_params(n, 12, n / 8 + 1, 2.0)
+    cm, f = H.init_c1_f1(om, n)
+    A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm)
+    M = H.Sweeping(A, form=form, workgroups=4 if form == "thomas" else 0)
+    M.configure()
+    x, y = A.vector(f.ravel()), A.vector()
+    A.apply_device(x, y, _ffi.HH_APPLY_PREC)
+    res[form] = y.download()
+    res[form + "_grid"] = np.array([M.partitioned or M.dense, M.workgroups])
+    x.close(); y.close(); A.close()
+np.savez(out, **res)
+'''
+
+
+def test_sweep_plain_launch_matches_cooperative(tmp_path):
+    """HH_SWEEP_COOP=0 (the grid-wide sweeps -- partitioned block-Thomas over 4 workgroups, the
+    dense form's persistent chain -- as plain launches; profiling runs use it, DESIGN 3b) gives
+    bit-identical applies: only the launch API differs, the kernels and their bounded grid
+    waits are the same.  Child processes: the switch is read once per process."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    outs = []
+    for coop in ("1", "0"):
+        out = tmp_path / f"c{coop}.npz"
+        subprocess.run([sys.executable, "-c", _PLAIN_LAUNCH, ROOT, str(out)], check=True,
+                       timeout=240, env=dict(os.environ, HH_SWEEP_COOP=coop))
+        outs.append(np.load(out))
+    a, b = outs
+    assert int(a["thomas_grid"][1]) == 4
+    for k in ("thomas", "dense"):
+        np.testing.assert_array_equal(a[k], b[k])

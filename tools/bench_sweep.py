@@ -61,6 +61,9 @@ for n in ns:
         gbs = f" ({alg / t_apply / 1e9:.0f} GB/s algorithmic, dense)"
     kind = "dense" if Msw.dense else (f"partitioned, {Msw.workgroups} workgroups" if Msw.partitioned
                                       else "sequential")
+    x.close()  # (every handle released explicitly, before the next grid and before exit)
+    y.close()
+    A.close()
     line = (f"n={n} b={b} wn={wn} form={form} ({kind}): setup {t_setup*1e3:.1f} ms, apply {t_apply*1e3:.2f} ms{gbs}, "
             f"corrected-sweep GMRES {len(hist)} its info={info} in {t_solve:.3f} s")
     if n <= 255 and os.path.isdir(os.path.join(ROOT, "oracle")):
@@ -74,3 +77,4 @@ for n in ns:
         line += f" | CPU SuperLU (1 core): setup {cpu_setup:.2f} s, apply {cpu_apply*1e3:.0f} ms"
     print(line, flush=True)
     del A, x, y
+H.default_context().close()  # (the last handle, before exit)
