@@ -108,6 +108,8 @@ def parse():
                    help="5 = the reference's operator; 9 = the 9-point operator (SURVEY row F4)")
     p.add_argument("--gmres-iters", type=int, default=40, help="timed inner GMRES iterations")
     p.add_argument("--restart", type=int, default=20)
+    p.add_argument("--krylov", default="auto", choices=["auto", "two", "one", "fused"],
+                   help="GMRES inner-iteration form (hh_op_set_krylov_mode; A/B studies)")
     p.add_argument("--no-gmres", action="store_true")
     p.add_argument("--const-steps", type=int, default=200,
                    help="timed applies of the same grid with a constant medium (reported as "
@@ -489,6 +491,7 @@ def main():
     assert (A.row_begin, A.row_end) == (j0, j1)
     if args.variant >= 0:
         A.tune(args.variant)
+    A.krylov_mode(args.krylov)
     bpp = A.bytes_per_point
 
     # ---------------- GMRES(restart): timed inner iterations ----------------

@@ -341,8 +341,15 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
 template <int K, bool CONSTC>
 __global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
   if (a.stop && *a.stop) return;
+  // the projections of row r run two steps after its basis row was loaded for the update (w on
+  // row r needs u_K two rows further): the first KS vectors' rows r .. r + 2 are kept in a
+  // three-row LDS ring (written from the update's first load batch, read by the same lane),
+  // the rest re-read from the memory system.  (KS = 5: 60 KB, the most that keeps two blocks
+  // per CU beside the exchange rows)
+  constexpr int KS = K < kSlKeep ? K : kSlKeep;
   __shared__ double2 coef[K];
   __shared__ double2 urow[2][kT + 2], zrow[2][kT + 2];
+  __shared__ double2 vkeep[3][KS][kT];
   const int n = a.n, nl = a.nl;
   const Band bd = band_of(a);
   const int t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
@@ -366,36 +373,61 @@ __global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
   const double2 mshift = a.mshift;
   const double2 z = make_double2(0.0, 0.0);
   int kz = 0;
-  auto unew = [&](int r, int col) {
+  // (scalar row pointers + the lane's 32-bit offset, coefficient reads in batches of 4, the
+  // update kept out of row_value's branch: fused_iter_kernel's register economies)
+  auto unew = [&](int r, unsigned col) {
     __builtin_amdgcn_sched_barrier(0);
     const int rc = min(max(r, rlo), rhi - 1);
-    const ptrdiff_t p = (ptrdiff_t)rc * n + col;
-    const double2* vp = a.V + p;
-    double2 w = a.win[p];
+    gd2* vrow = gptr(a.V + (ptrdiff_t)rc * n);
+    gd2* wrow = gptr(a.win + (ptrdiff_t)rc * n);
+    asm volatile("" : "+s"(vrow), "+s"(wrow));
+    const unsigned bo = col * (unsigned)sizeof(double2);
+    double2 w = ld_at(wrow, bo);
+    const int slot = (r % 3 + 3) % 3;
     constexpr int kB = 8;
 #pragma unroll 1
     for (int k0 = 0; k0 < K; k0 += kB) {
       double2 v[kB];
 #pragma unroll
-      for (int q = 0; q < kB; ++q) v[q] = vp[(size_t)min(k0 + q, K - 1) * a.ldv];
+      for (int q = 0; q < kB; ++q) v[q] = ld_at(vrow + (size_t)min(k0 + q, K - 1) * a.ldv, bo);
+      if (k0 == 0) {
 #pragma unroll
-      for (int q = 0; q < kB; ++q)
-        if (k0 + q < K) w = csub(w, cmul(coef[k0 + q + kz], v[q]));
+        for (int q = 0; q < KS; ++q) vkeep[slot][q][threadIdx.x] = v[q];
+      }
+#pragma unroll
+      for (int q0 = 0; q0 < kB; q0 += 4) {
+        double2 c[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c[q] = coef[min(k0 + q0 + q, K - 1) + kz];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (k0 + q0 + q < K) w = csub(w, cmul(c[q], v[q0 + q]));
+      }
     }
+    asm volatile("" : "+v"(w.x), "+v"(w.y));
     return row_value<2>(a, rlo, rhi, r, col, w);
   };
   // u_K at two points at once, lane-parallel (the edge waves): half h of the wave takes point
   // h, lane k of the half the term c_k u_k, the 32 terms summed by shuffles -- one load round
   // trip instead of two chains of ceil(K / 8) batches (terms in a tree order: the strip that
-  // owns the column forms it in k order, so halo values agree to rounding)
-  auto unew2 = [&](int r1, int c1, int r2, int c2) {
+  // owns the column forms it in k order, so halo values agree to rounding).  The two loads are
+  // issued before the strip's own row (so both round trips overlap), the sum after it.
+  struct EdgeLd {
+    double2 wv, vk;
+  };
+  auto unew2_issue = [&](int r1, int c1, int r2, int c2) {
     const int h = lane >> 5, k = lane & 31;
     const int r = h ? r2 : r1, c = h ? c2 : c1;
     const int rc = min(max(r, rlo), rhi - 1);
     const ptrdiff_t p = (ptrdiff_t)rc * n + c;
-    const double2 wv = a.win[p];
-    const double2 vk = (a.V + p)[(size_t)min(k, K - 1) * a.ldv];
-    double2 tk = csel(k < K, cmul(coef[min(k, K - 1)], vk), z);
+    EdgeLd e;
+    e.wv = a.win[p];
+    e.vk = (a.V + p)[(size_t)min(k, K - 1) * a.ldv];
+    return e;
+  };
+  auto unew2_finish = [&](int r1, int c1, int r2, int c2, const EdgeLd& e) {
+    const int k = lane & 31;
+    double2 tk = csel(k < K, cmul(coef[min(k, K - 1)], e.vk), z);
 #pragma unroll
     for (int off = 16; off > 0; off >>= 1) {
       tk.x += __shfl_xor(tk.x, off);
@@ -403,8 +435,8 @@ __global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
     }
     const double2 ua = make_double2(__shfl(tk.x, 0), __shfl(tk.y, 0));
     const double2 ub = make_double2(__shfl(tk.x, 32), __shfl(tk.y, 32));
-    const double2 wa = make_double2(__shfl(wv.x, 0), __shfl(wv.y, 0));
-    const double2 wb = make_double2(__shfl(wv.x, 32), __shfl(wv.y, 32));
+    const double2 wa = make_double2(__shfl(e.wv.x, 0), __shfl(e.wv.y, 0));
+    const double2 wb = make_double2(__shfl(e.wv.x, 32), __shfl(e.wv.y, 32));
     return make_double2x2(row_value<2>(a, rlo, rhi, r1, c1, csub(wa, ua)),
                           row_value<2>(a, rlo, rhi, r2, c2, csub(wb, ub)));
   };
@@ -462,10 +494,12 @@ __global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
     for (int L0 = rb - 2; L0 <= re + 1; ++L0) {
       int L = L0;
       asm volatile("" : "+s"(L), "+s"(kz));
-      const double2 uN = unew(L, ic);
+      EdgeLd el{z, z};
+      if (ew || ee) el = unew2_issue(L, ie, L - 1, io);  // (wave-uniform)
+      const double2 uN = unew(L, (unsigned)ic);
       double2 euN = z, eo = z;
-      if (ew || ee) {  // (wave-uniform)
-        const auto pr = unew2(L, ie, L - 1, io);
+      if (ew || ee) {
+        const auto pr = unew2_finish(L, ie, L - 1, io, el);
         euN = csel(ehas, pr.a, z);
         eo = csel(ohas, pr.b, z);
       }
@@ -534,11 +568,17 @@ __global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
         const double2 uo = csel(act, uP, z);
         nu = fma(uo.x, uo.x, fma(uo.y, uo.y, nu));
         nw = fma(w.x, w.x, fma(w.y, w.y, nw));
+        const int slot = r % 3;  // (r >= 0)
 #pragma unroll
-        for (int k0 = 0; k0 < K; k0 += 8) {
+        for (int k = 0; k < KS; ++k) acc[k] = cfma_conj(vkeep[slot][k][t], w, acc[k]);
+        gd2* vr = gptr(a.V + (size_t)r * n);
+        asm volatile("" : "+s"(vr));
+#pragma unroll
+        for (int k0 = KS; k0 < K; k0 += 8) {
           double2 v[8];
 #pragma unroll
-          for (int q2 = 0; q2 < 8; ++q2) v[q2] = a.V[(size_t)min(k0 + q2, K - 1) * a.ldv + p];
+          for (int q2 = 0; q2 < 8; ++q2)
+            v[q2] = ld_at(vr + (size_t)min(k0 + q2, K - 1) * a.ldv, (unsigned)ic * 16u);
 #pragma unroll
           for (int q2 = 0; q2 < 8; ++q2)
             if (k0 + q2 < K) acc[k0 + q2] = cfma_conj(v[q2], w, acc[k0 + q2]);
