@@ -248,7 +248,6 @@ constexpr int kFusedMaxK = 20;  // K <= this (restart <= kFusedMaxK + 1)
 // basis vectors whose projection re-read is served from the pass's own LDS copy (HH_FUSED_KEEP:
 // 0 = every re-read from the memory system, for A/B)
 constexpr int kFusedKeepDefault = 17;
-constexpr int kSlKeep = 5;  // shifted-Laplace pass: basis vectors kept in its 3-row LDS ring
 int fused_iter_rows(int n, int rows);  // band height for a slab of `rows` rows
 int fused_iter_blocks(int n, int bands);
 void launch_fused_iter(int K, const FusedArgs& a, int blocks, hipStream_t stream);

@@ -2161,12 +2161,11 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
                           op->sl_ext_ok)) &&
                         restart <= kFusedMaxK + 1;
   // (by default from n = 1024: smaller grids give the pass too few tiles to stream at speed --
-  // n = 300: 16-25k it/s against 29-30k for the regular cycle, profiles/r03q)
-  // (the shifted-Laplace pass is opt-in: 736 vs 755 it/s for the regular cycle at 4096^2,
-  // profiles/r03y -- two stencils and two complex divisions per point make it VALU-heavy)
+  // n = 300: 16-25k it/s against 29-30k for the regular cycle, profiles/r03q; the two-sweep
+  // shifted-Laplace pass too since round 4: 889-894 vs 769-774 it/s for the regular cycle at
+  // 4096^2, profiles/r04/r04q_ab_sl_fused_vs_regular_4096.log)
   const bool fused = fused_ok && (op->krylov_mode == 3 ||
-                                  (op->krylov_mode == 0 && fused_default() && op->n >= 1024 &&
-                                   op->pkind != HH_PREC_SHIFTED_LAPLACE));
+                                  (op->krylov_mode == 0 && fused_default() && op->n >= 1024));
   const bool lagged = !reorth && !fused &&
                       (op->krylov_mode == 2 || (op->krylov_mode == 0 && c->world > 1));
   // small single-rank grids: the whole cycle in one launch (gmres_small.hip) -- launch-bound

@@ -197,8 +197,8 @@ def test_fused_pass_matches_lagged(ctx, n, kind, precond, restart, K):
 
 def test_fused_pass_is_the_single_rank_default(ctx):
     """mode auto on one rank picks the one-pass iteration where it applies (n >= 1024, M none /
-    Jacobi, restart <= 21) and the regular cycle elsewhere (restart 30, shifted Laplace); mode
-    "fused" also runs the two-sweep shifted Laplace in one pass (not three sweeps)"""
+    Jacobi / the two-sweep shifted Laplace, restart <= 21) and the regular cycle elsewhere
+    (restart 30, three sweeps, n < 1024); mode "two" forces the regular cycle"""
     n = 1024
     om, h, eta = O.problem_params(n, 12, 64.0, 2.0)
     A = H.build_A_matrix(12, 81.0, eta, om, h, n, H.constant_c_mat(n), context=ctx)
@@ -208,13 +208,19 @@ def test_fused_pass_is_the_single_rank_default(ctx):
     H.gmres(A, f, rtol=1e-12, restart=30, maxiter=5, M="jacobi")
     assert A.last_solve_path() == "regular"
     H.gmres(A, f, rtol=1e-12, restart=20, maxiter=3, M=H.ShiftedLaplace(A))
-    assert A.last_solve_path() == "regular"  # (the shifted-Laplace pass is opt-in: mode 3)
-    A.krylov_mode("fused")
-    H.gmres(A, f, rtol=1e-12, restart=20, maxiter=3, M=H.ShiftedLaplace(A))
     assert A.last_solve_path() == "one-pass"
     H.gmres(A, f, rtol=1e-12, restart=20, maxiter=3, M=H.ShiftedLaplace(A, sweeps=3))
     assert A.last_solve_path() == "regular"
+    A.krylov_mode("two")
+    H.gmres(A, f, rtol=1e-12, restart=20, maxiter=3, M=H.ShiftedLaplace(A))
+    assert A.last_solve_path() == "regular"
     A.krylov_mode("auto")
+    n2 = 600
+    om, h, eta = O.problem_params(n2, 12, 30.0, 2.0)
+    B = H.build_A_matrix(12, 81.0, eta, om, h, n2, H.constant_c_mat(n2), context=ctx)
+    H.gmres(B, O.init_f1_mat(.5, .125, om, n2).ravel(), rtol=1e-12, restart=20, maxiter=3,
+            M=H.ShiftedLaplace(B))
+    assert B.last_solve_path() == "regular"
 
 
 @pytest.mark.parametrize("n,kind", [(300, "c1"), (1100, "marmousi")])
