@@ -27,7 +27,6 @@
 #include <algorithm>
 #include <cstddef>
 #include <cstdlib>
-#include <type_traits>
 
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
@@ -43,25 +42,11 @@ constexpr int kT = 256;  // threads per block = columns per strip
 #define HH_SL_KEEP 5
 #endif
 constexpr int kSlKeep = HH_SL_KEEP;
-// waves per SIMD the shifted-Laplace pass is compiled for (the register allocator's target)
-#ifndef HH_SL_WAVES
-#define HH_SL_WAVES 0
-#endif
-constexpr int sl_waves(int K) { return HH_SL_WAVES > 0 ? HH_SL_WAVES : (K > 0 ? 2 : 2); }
 
 struct double2x2 {
   double2 a, b;
 };
 __device__ __forceinline__ double2x2 make_double2x2(double2 a, double2 b) { return {a, b}; }
-
-// compile-time loop: f(integral_constant<int, i>) for i in [B, E)
-template <int B, int E, class F>
-__device__ __forceinline__ void sfor(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    sfor<B + 1, E>(f);
-  }
-}
 
 // by-value select (a select of lvalues would become a select of addresses)
 __device__ __forceinline__ double2 csel(bool c, double2 a, double2 b) {
@@ -360,8 +345,7 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
 // (the two-launch path's Dirichlet neighbours); the slab's tables hold rows -2 .. nl+1 and
 // invc2_halo the medium of rows -2, -1, nl, nl+1.
 template <int K, bool CONSTC>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(sl_waves(K))))
-void fused_sl_iter_kernel(const FusedArgs a) {
+__global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
   if (a.stop && *a.stop) return;
   // the projections of row r run two steps after its basis row was loaded for the update (w on
   // row r needs u_K two rows further): the first KS vectors' rows r .. r + 2 are kept in a
@@ -429,42 +413,6 @@ void fused_sl_iter_kernel(const FusedArgs a) {
     }
     asm volatile("" : "+v"(w.x), "+v"(w.y));
     return row_value<2>(a, rlo, rhi, r, col, w);
-  };
-  // Few basis vectors (K <= 4): a row's loads are too few to keep the memory system busy while
-  // the step's two stencils run, and the step waited a full round trip on them -- so the rows'
-  // loads run D steps ahead through a register ring (row L + d at index d), which costs
-  // 4 (K + 1) D VGPRs.  Same arithmetic as unew.
-  constexpr int D = K <= 2 ? 4 : (K <= 4 ? 2 : 0);
-  constexpr int DR = D > 0 ? D : 1;
-  double2 rw[DR], rv[DR][K];
-  auto issue = [&](auto dc, int r) {
-    constexpr int d = decltype(dc)::value;
-    const int rc = min(max(r, rlo), rhi - 1);
-    gd2* vrow = gptr(a.V + (ptrdiff_t)rc * n);
-    gd2* wrow = gptr(a.win + (ptrdiff_t)rc * n);
-    asm volatile("" : "+s"(vrow), "+s"(wrow));
-    const unsigned bo = (unsigned)ic * (unsigned)sizeof(double2);
-    rw[d] = ld_at(wrow, bo);
-#pragma unroll
-    for (int q = 0; q < K; ++q) rv[d][q] = ld_at(vrow + (size_t)q * a.ldv, bo);
-  };
-  auto unew_pf = [&](int r) {
-    const int slot = (r % 3 + 3) % 3;
-#pragma unroll
-    for (int q = 0; q < KS; ++q) vkeep[slot][q][threadIdx.x] = rv[0][q];
-    double2 w = rw[0];
-#pragma unroll
-    for (int q = 0; q < K; ++q) w = csub(w, cmul(coef[q + kz], rv[0][q]));
-    asm volatile("" : "+v"(w.x), "+v"(w.y));
-    // (the ring moves one row on; the row D steps ahead is requested)
-    sfor<0, (D > 0 ? D - 1 : 0)>([&](auto dc) {
-      constexpr int d = decltype(dc)::value;
-      rw[d] = rw[d + 1];
-#pragma unroll
-      for (int q = 0; q < K; ++q) rv[d][q] = rv[d + 1][q];
-    });
-    if constexpr (D > 0) issue(std::integral_constant<int, D - 1>{}, r + D);
-    return row_value<2>(a, rlo, rhi, r, (unsigned)ic, w);
   };
   // u_K at two points at once, lane-parallel (the edge waves): half h of the wave takes point
   // h, lane k of the half the term c_k u_k, the 32 terms summed by shuffles -- one load round
@@ -551,16 +499,12 @@ void fused_sl_iter_kernel(const FusedArgs a) {
     double invm = 1.0;
     double2 Wm = z, Em = z, Sm = z, Nm = z;
     int buf = 0;
-    if constexpr (D > 0)
-      sfor<0, D>([&](auto dc) { issue(dc, rb - 2 + (int)decltype(dc)::value); });
     for (int L0 = rb - 2; L0 <= re + 1; ++L0) {
       int L = L0;
       asm volatile("" : "+s"(L), "+s"(kz));
       EdgeLd el{z, z};
       if (ew || ee) el = unew2_issue(L, ie, L - 1, io);  // (wave-uniform)
-      double2 uN;
-      if constexpr (D > 0) uN = unew_pf(L);
-      else uN = unew(L, (unsigned)ic);
+      const double2 uN = unew(L, (unsigned)ic);
       double2 euN = z, eo = z;
       if (ew || ee) {
         const auto pr = unew2_finish(L, ie, L - 1, io, el);
