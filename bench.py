@@ -328,6 +328,23 @@ def gmres_bytes(args, its, bpp, N):
     return sum((bpp + pre) * N + 16 * (j + 2) * N + 16 * (j + 3) * N for j in js), fused
 
 
+FUSED_TRAFFIC_DB = "profiles/r04_pmc_fused.json"
+
+
+def fused_pass_traffic(n, medium, precond, world):
+    """Measured HBM traffic of the one-pass iteration's pass kernels over a restart cycle, as a
+    ratio to their algorithmic bytes (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes, separate
+    runs; tools/pmc_fused.py --merge): (ratio, per-K ratios, source), or Nones for a workload
+    without a record."""
+    path = os.path.join(ROOT, FUSED_TRAFFIC_DB)
+    if world != 1 or not os.path.exists(path):
+        return None, None, None
+    rec = json.load(open(path)).get(f"n{n}_{medium}_{precond}")
+    if not rec:
+        return None, None, None
+    return rec["ratio"], rec["per_K"], f"{FUSED_TRAFFIC_DB}: {rec['source']}"
+
+
 def gmres_path_bytes(args, its, bpp, N, path):
     """algorithmic bytes of `its` inner iterations on the path the solve actually ran, per
     unknown: the one-pass iteration moves, at iteration j of a cycle, j = 0: the
@@ -525,6 +542,12 @@ def main():
             # one pass over the basis (fused.hip fused_iter_kernel)
             "solve_path": A.last_solve_path(),
         }
+        if gmres_block["solve_path"] == "one-pass":
+            # the passes' measured HBM traffic per algorithmic byte over a cycle (PMC counters
+            # cannot run inside the timed solve: the committed record of the same workload)
+            ratio, per_k, src = fused_pass_traffic(n, args.medium, args.precond, world)
+            gmres_block["pass_traffic_vs_algorithmic"] = ratio
+            gmres_block["pass_traffic_source"] = src
 
     R = max(1, args.rotate)
     const_block = None

@@ -4,9 +4,13 @@ algorithmic bytes: reads (K + 1) 16 B per unknown (the K basis vectors v_0 .. v_
 writes 32 B (u_{j+1} into V[K], w_{j+1}); + 8 B read of 1/c^2 for a non-constant medium.
 FETCH_SIZE is doubled (gfx950 correction for 16-B/lane coalesced reads, MI355X_MICROARCH.md),
 as in tools/pmc_traffic.py.
-usage: python tools/pmc_fused.py FETCH_CSV WRITE_CSV --n N [--medium const|marmousi]"""
+usage: python tools/pmc_fused.py FETCH_CSV WRITE_CSV --n N [--medium const|marmousi]
+       [--merge DB.json --key KEY]  (records the cycle's ratio and the per-K ratios under KEY,
+       for bench.py's GMRES block)"""
 import argparse
 import csv
+import json
+import os
 import re
 from collections import defaultdict
 
@@ -26,10 +30,13 @@ def main():
     p.add_argument("write")
     p.add_argument("--n", type=int, required=True)
     p.add_argument("--medium", default="const")
+    p.add_argument("--merge")
+    p.add_argument("--key")
     a = p.parse_args()
     N = a.n * a.n
     fetch, write = load(a.fetch), load(a.write)
     tot_t = tot_a = 0.0
+    per_k = {}
     print(f"n={a.n} {a.medium}: per launch, MB (FETCH_SIZE x2 | WRITE_SIZE) vs algorithmic")
     for key in sorted(fetch):
         sl, K = key
@@ -39,12 +46,19 @@ def main():
         wr = 32 * N
         tot_t += (2 * f + w) * cnt
         tot_a += (rd + wr) * cnt
+        per_k[f"{'sl' if sl else ''}K{K}"] = round((2 * f + w) / (rd + wr), 4)
         print(f"{'sl ' if sl else ''}K={K:2d} x{cnt:3d}: read {2 * f / 1e6:9.1f} vs {rd / 1e6:9.1f} "
               f"({2 * f / rd:.3f}x, raw {f / rd:.3f}x) | write {w / 1e6:8.1f} vs {wr / 1e6:8.1f} "
               f"({w / wr:.3f}x) | total {(2 * f + w) / (rd + wr):.3f}x")
     if tot_a:
         print(f"all launches: {tot_t / 1e9:.2f} GB vs {tot_a / 1e9:.2f} GB algorithmic = "
               f"{tot_t / tot_a:.3f}x")
+        if a.merge and a.key:
+            db = json.load(open(a.merge)) if os.path.exists(a.merge) else {}
+            db[a.key] = {"ratio": round(tot_t / tot_a, 4), "per_K": per_k,
+                         "source": f"{os.path.basename(os.path.dirname(a.fetch))}, "
+                                   f"{os.path.basename(os.path.dirname(a.write))}"}
+            json.dump(db, open(a.merge, "w"), indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
