@@ -273,12 +273,12 @@ class DeviceOperator(scipy.sparse.linalg.LinearOperator):
     KRYLOV_MODES = {"auto": 0, "two": 1, "one": 2, "fused": 3}
 
     def krylov_mode(self, mode: str = "auto"):
-        """Global reductions per GMRES inner iteration: "two" (projections, then the updated
-        vector's norm -- exact normalisation), "one" (lagged normalisation: one allreduce per
-        iteration), "fused" ("one" with the update, the next M A and its projections in one
-        pass over the basis: single rank and slab, 5-point, M none / Jacobi, restart <= 21),
-        "auto" ("fused" where it applies, else one across ranks and two on a single rank).
-        Results agree to rounding."""
+        """GMRES inner-iteration form: "two" (projections, then the updated vector's norm --
+        exact normalisation), "one" (lagged normalisation: one allreduce per iteration), "fused"
+        ("one" with the update, the next M A and its projections in one pass over the basis,
+        csrc/fused.hip: any slabs and ranks, 5-point operator, M none / Jacobi / the two-sweep
+        shifted Laplace, restart <= 21), "auto" ("fused" where it applies and n >= 1024, else
+        "one" across ranks and "two" on a single rank).  Results agree to rounding."""
         if mode not in self.KRYLOV_MODES:
             raise ValueError(f"mode must be one of {sorted(self.KRYLOV_MODES)}")
         check(lib.hh_op_set_krylov_mode(self.handle, self.KRYLOV_MODES[mode]))
