@@ -223,6 +223,9 @@ struct hh_op {
   double2* sw_Pf = nullptr;     // chunk products of the partitioned solves, or null
   double2* sw_Pb = nullptr;
   double2* sw_Pw = nullptr;     // workgroup maps of the multi-workgroup partitioned solves
+  double2* sw_Tm = nullptr;     // their grid maps
+  double2* sw_Rw = nullptr;     // split-chain and suffix workgroup maps
+  double2* sw_Sw = nullptr;
   unsigned long long* sw_gran = nullptr;  // their grid-exchange granules
   int sw_wgs = 0;               // requested workgroups per partitioned solve (0: by n)
   unsigned long long* sw_prof = nullptr;  // diagnostic phase ticks (hh_op_sweep_profile)
@@ -1306,6 +1309,9 @@ static void op_release(hh_op* op) {
   dfree(op->sw_Pf);
   dfree(op->sw_Pb);
   dfree(op->sw_Pw);
+  dfree(op->sw_Tm);
+  dfree(op->sw_Rw);
+  dfree(op->sw_Sw);
   dfree(op->sw_gran);
   dfree(op->sw_prof);
   dfree(op->sw_y);
@@ -1403,7 +1409,7 @@ static void sweep_dense_configure(hh_op* op) {
 
 // Partitioned block-Thomas solves (sweep.hip bt_solve_chunked) for the forward / backward
 // sweeps when the block-Thomas form is in use: G workgroups of kSweepChunks chunks each share
-// every solve (G by n: ~4 columns per chunk, at most sweep_part_max_wgs(B) and the CU count;
+// every solve (G by n: 2 columns per chunk, at most sweep_part_max_wgs(B) and the CU count;
 // hh_op_sweep_workgroups overrides it).  The chunk products Psi_f / Psi_b (2 x the factors'
 // memory) and the workgroup maps are formed once here.  Mode 3, the dense form, n < 2 columns
 // per chunk or a lack of memory keep the sequential solves.
@@ -1411,13 +1417,16 @@ static void sweep_part_release(hh_op* op) {
   dfree(op->sw_Pf);
   dfree(op->sw_Pb);
   dfree(op->sw_Pw);
+  dfree(op->sw_Tm);
+  dfree(op->sw_Rw);
+  dfree(op->sw_Sw);
   dfree(op->sw_gran);
-  op->sw_Pf = op->sw_Pb = op->sw_Pw = nullptr;
+  op->sw_Pf = op->sw_Pb = op->sw_Pw = op->sw_Tm = op->sw_Rw = op->sw_Sw = nullptr;
   op->sw_gran = nullptr;
   SweepArgs& a = op->sweep;
   a.chunks = 0;
   a.G = 0;
-  a.Pf = a.Pb = a.Pw = nullptr;
+  a.Pf = a.Pb = a.Pw = a.Tm = a.Rw = a.Sw = nullptr;
   a.gran = nullptr;
 }
 
@@ -1425,7 +1434,9 @@ static int sweep_part_wgs(hh_op* op) {
   const int n = op->n, B = sweep_block(op->b);
   int cus = 0;
   HIPC(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, op->ctx->device));
-  int G = op->sw_wgs > 0 ? op->sw_wgs : n / (4 * kSweepChunks);
+  // by n: 2 columns per chunk (the chunk-local passes are per-CU latency / bandwidth bound, the
+  // grid step is one B x B step per half-wave whatever G: profiles/r04/r04sw3_*)
+  int G = op->sw_wgs > 0 ? op->sw_wgs : n / (2 * kSweepChunks);
   G = std::max(1, std::min({G, sweep_part_max_wgs(B), cus, n / (2 * kSweepChunks)}));
   if (op->sw_wgs == 0)  // by n: the largest G <= that whose B-vectors fit in LDS, if any
     for (int g2 = G; g2 >= 1; --g2)
@@ -1447,13 +1458,19 @@ static void sweep_chunk_configure(hh_op* op) {
   sweep_part_release(op);
   const size_t elems = (size_t)a.nsys * n * B * B;
   const size_t welems = (size_t)a.nsys * G * 2 * kSweepChunks * B * B;
+  const size_t telems = (size_t)a.nsys * 2 * sweep_grid_tri(G) * B * B;
   size_t free_b = 0, total_b = 0;
   HIPC(hipMemGetInfo(&free_b, &total_b));
-  if ((2 * elems + welems) * sizeof(double2) > free_b / 10 * 8) return;  // sequential solves
+  const size_t relems = welems / 2;  // Rw: 8 maps per (system, workgroup, direction); Sw: 16
+  if ((2 * elems + 2 * welems + relems + telems) * sizeof(double2) > free_b / 10 * 8)
+    return;  // sequential solves
   try {
     op->sw_Pf = dalloc<double2>(elems);
     op->sw_Pb = dalloc<double2>(elems);
     op->sw_Pw = dalloc<double2>(welems);
+    op->sw_Tm = dalloc<double2>(std::max<size_t>(telems, 1));
+    op->sw_Rw = dalloc<double2>(relems);
+    op->sw_Sw = dalloc<double2>(welems);
     op->sw_gran = dalloc<unsigned long long>(sweep_part_granules(G));
   } catch (...) {
     sweep_part_release(op);
@@ -1465,6 +1482,9 @@ static void sweep_chunk_configure(hh_op* op) {
   a.Pf = op->sw_Pf;
   a.Pb = op->sw_Pb;
   a.Pw = op->sw_Pw;
+  a.Tm = op->sw_Tm;
+  a.Rw = op->sw_Rw;
+  a.Sw = op->sw_Sw;
   a.gran = op->sw_gran;
   a.timeout = reinterpret_cast<unsigned*>(op->red + kRedTimeout);
   launch_sweep(a, 4, nullptr, nullptr, 0, op->ctx->stream);
@@ -1931,7 +1951,7 @@ HH_API int hh_op_sweep_profile(hh_op* op, int enable, double* phase_us, int cap)
   GUARD_BEGIN
   REQUIRE(op, "null op");
   HIPC(hipSetDevice(op->ctx->device));
-  const size_t slots = (size_t)32 * kSweepProfSlots;
+  const size_t slots = (size_t)kSweepMaxWgs * kSweepProfSlots;  // (one row per workgroup)
   if (phase_us && op->sw_prof) {
     std::vector<unsigned long long> t(slots);
     HIPC(hipMemcpy(t.data(), op->sw_prof, slots * sizeof(unsigned long long),

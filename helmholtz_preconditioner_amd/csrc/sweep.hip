@@ -398,15 +398,20 @@ __global__ __launch_bounds__(kSW) void sweep_chunk_setup_kernel(const SweepArgs 
   }
 }
 
-// Setup: the workgroup maps of one (system, workgroup) per wave (after the chunk products),
-// with F_k = Psi_f[end_k], B_k = Psi_b[lo_k] the chunk maps (end_k / lo_k: the chunk's last /
-// first column): forward Pw[..][0][q] = F_q .. F_0 (the map from the workgroup's carry to the
-// end of chunk q), backward Pw[..][1][q] = B_{15-q} .. B_15 (from the carry past the workgroup
-// to the start of chunk 15 - q); [15] is the whole workgroup's map Phi.
+// Setup: the workgroup maps of one (system, workgroup) per wave (after the chunk products).
+// With F_p the map of the chunk at chain position p (forward: chunk p, Psi_f at its last column;
+// backward: chunk 15 - p, Psi_b at its first column):
+//   Pw[..][dir][p] = F_p .. F_0, the map from the workgroup's carry to the end of position p
+//     ([15] is the whole workgroup's map Phi);
+//   Rw[..][dir][t] = F_{8+t} .. F_8 (t < 7), from the end of position 7 to the end of 8 + t
+//     (the second half of the split chunk chain);
+//   Sw[..][dir][p] = F_15 .. F_{p+1} (p < 15), from the end of position p to the workgroup's
+//     end (the suffix sum that publishes the workgroup's zero-carry vector).
 template <int B>
 __global__ __launch_bounds__(kSW) void sweep_wg_setup_kernel(const SweepArgs a) {
   constexpr int KG = B / kGroups;
   constexpr size_t PS = (size_t)B * B;
+  constexpr int KL = kSweepChunks;
   __shared__ double2 Q[2][B][B];
   const int n = a.n, G = a.G, K = a.chunks;
   const int s = blockIdx.x / G, wg = blockIdx.x % G;
@@ -416,65 +421,164 @@ __global__ __launch_bounds__(kSW) void sweep_wg_setup_kernel(const SweepArgs a) 
   const double2 z = make_double2(0.0, 0.0);
   for (int dir = 0; dir < 2; ++dir) {
     const double2* src = (dir == 0 ? a.Pf : a.Pb) + (size_t)s * n * PS;
-    double2* out = a.Pw + (((size_t)s * G + wg) * 2 + dir) * kSweepChunks * PS;
-    for (int q = 0; q < kSweepChunks; ++q) {  // forward: chunks in order; backward: from the last
-      const int k = kSweepChunks * wg + (dir == 0 ? q : kSweepChunks - 1 - q);
-      const int col = dir == 0 ? chunk_lo(n, K, k + 1) - 1 : chunk_lo(n, K, k);
-      double2 prow[B];
-      sfor<0, B>([&](auto mc) {
-        constexpr int m = decltype(mc)::value;
-        prow[m] = src[(size_t)col * PS + pidx<B>(jl, m)];
-      });
+    const size_t wsel = ((size_t)s * G + wg) * 2 + dir;
+    auto fmap = [&](int p) {  // F_p
+      const int k = KL * wg + (dir == 0 ? p : KL - 1 - p);
+      return src + (size_t)(dir == 0 ? chunk_lo(n, K, k + 1) - 1 : chunk_lo(n, K, k)) * PS;
+    };
+    auto put = [&](const double2 (&v)[KG], int t, double2* out) {
+      if (row) {
+        sfor<0, KG>([&](auto c2) {
+          constexpr int c = decltype(c2)::value;
+          Q[t & 1][j][g * KG + c] = v[c];
+          out[pidx<B>(j, g * KG + c)] = v[c];
+        });
+      }
+      wave_sync();
+    };
+    // left products F_{p1-1} .. F_{p0} into out[0 .. p1-p0)
+    auto left = [&](int p0, int p1, double2* out) {
+      for (int t = 0; t < p1 - p0; ++t) {
+        const double2* f = fmap(p0 + t);
+        double2 prow[B];
+        sfor<0, B>([&](auto mc) {
+          constexpr int m = decltype(mc)::value;
+          prow[m] = f[pidx<B>(jl, m)];
+        });
+        double2 v[KG];
+        sfor<0, KG>([&](auto c2) {
+          constexpr int c = decltype(c2)::value;
+          const int cx = g * KG + c;
+          double2 acc = z;
+          if (t == 0) {
+            sfor<0, B>([&](auto mc) {
+              constexpr int m = decltype(mc)::value;
+              acc = csel(m == cx, prow[m], acc);
+            });
+          } else {
+            sfor<0, B>([&](auto mc) {
+              constexpr int m = decltype(mc)::value;
+              acc = cfma(prow[m], Q[(t - 1) & 1][m][cx], acc);
+            });
+          }
+          v[c] = acc;
+        });
+        put(v, t, out + (size_t)t * PS);
+      }
+    };
+    left(0, KL, a.Pw + wsel * KL * PS);
+    left(KL / 2, KL - 1, a.Rw + wsel * (KL / 2) * PS);
+    // right products: Sw[p] = Sw[p+1] F_{p+1}, Sw[14] = F_15
+    double2* sw = a.Sw + wsel * KL * PS;
+    for (int t = 0; t < KL - 1; ++t) {
+      const int p = KL - 2 - t;
+      const double2* f = fmap(p + 1);
       double2 v[KG];
       sfor<0, KG>([&](auto c2) {
         constexpr int c = decltype(c2)::value;
         const int cx = g * KG + c;
         double2 acc = z;
-        if (q == 0) {
-          sfor<0, B>([&](auto mc) {
-            constexpr int m = decltype(mc)::value;
-            acc = csel(m == cx, prow[m], acc);
-          });
+        if (t == 0) {
+          acc = f[pidx<B>(jl, cx)];
         } else {
           sfor<0, B>([&](auto mc) {
             constexpr int m = decltype(mc)::value;
-            acc = cfma(prow[m], Q[(q - 1) & 1][m][cx], acc);
+            acc = cfma(Q[(t - 1) & 1][jl][m], f[pidx<B>(m, cx)], acc);
           });
         }
         v[c] = acc;
       });
-      if (row) {
-        sfor<0, KG>([&](auto c2) {
-          constexpr int c = decltype(c2)::value;
-          Q[q & 1][j][g * KG + c] = v[c];
-          out[(size_t)q * PS + pidx<B>(j, g * KG + c)] = v[c];
+      put(v, t, sw + (size_t)p * PS);
+    }
+  }
+}
+
+// Setup: the grid maps (SweepArgs::Tm), after the workgroup maps.  One wave per (system,
+// direction, upstream workgroup u) walks the downstream workgroups by left products:
+// T(u+2, u) = Phi_{u+1}, T(w+1, u) = Phi_w T(w, u) (backward mirrored: T(u-2, u) = Phi_{u-1},
+// T(w-1, u) = Phi_w T(w, u)), Phi_w = Pw[s][w][dir][15].  Same lane split as above.
+template <int B>
+__global__ __launch_bounds__(kSW) void sweep_grid_setup_kernel(const SweepArgs a) {
+  constexpr int KG = B / kGroups;
+  constexpr size_t PS = (size_t)B * B;
+  __shared__ double2 Q[2][B][B];
+  const int G = a.G;
+  const int s = blockIdx.x / (2 * G), dir = (blockIdx.x / G) & 1, u = blockIdx.x % G;
+  const int steps = dir == 0 ? G - 2 - u : u - 1;  // downstream workgroups at distance >= 2
+  const int lane = threadIdx.x, g = lane >> 4, j = lane & 15;
+  const bool row = j < B;
+  const int jl = row ? j : B - 1;
+  const double2 z = make_double2(0.0, 0.0);
+  double2* tbase = a.Tm + (size_t)(s * 2 + dir) * sweep_grid_tri(G) * PS;
+  for (int q = 0; q < steps; ++q) {
+    const int w = dir == 0 ? u + 1 + q : u - 1 - q;  // the new left factor's workgroup
+    const int cnt = dir == 0 ? w + 1 : G - w;          // upstream count of the map's workgroup
+    const double2* phi =
+        a.Pw + ((((size_t)s * a.G + w) * 2 + dir) * kSweepChunks + kSweepChunks - 1) * PS;
+    double2* out = tbase + (sweep_grid_tri(cnt) + (size_t)q) * PS;  // distance d = q + 2
+    double2 prow[B];
+    sfor<0, B>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+      prow[m] = phi[pidx<B>(jl, m)];
+    });
+    double2 v[KG];
+    sfor<0, KG>([&](auto c2) {
+      constexpr int c = decltype(c2)::value;
+      const int cx = g * KG + c;
+      double2 acc = z;
+      if (q == 0) {
+        sfor<0, B>([&](auto mc) {
+          constexpr int m = decltype(mc)::value;
+          acc = csel(m == cx, prow[m], acc);
+        });
+      } else {
+        sfor<0, B>([&](auto mc) {
+          constexpr int m = decltype(mc)::value;
+          acc = cfma(prow[m], Q[(q - 1) & 1][m][cx], acc);
         });
       }
-      wave_sync();
+      v[c] = acc;
+    });
+    if (row) {
+      sfor<0, KG>([&](auto c2) {
+        constexpr int c = decltype(c2)::value;
+        Q[q & 1][j][g * KG + c] = v[c];
+        out[pidx<B>(j, g * KG + c)] = v[c];
+      });
     }
+    wave_sync();
   }
 }
 
 template <int B>
 constexpr int chunk_ring() { return B <= 4 ? 4 : (B == 8 ? 3 : 2); }  // (no spills at 256 VGPRs)
 template <int B>
-constexpr int part_max_wgs() { return B <= 12 ? 32 : 12; }  // (LDS of the grid chain's maps)
+constexpr int part_max_wgs() { return kSweepMaxWgs; }  // (each half holds kSweepGridMaps maps)
 constexpr int kPartThreads = kSweepChunks / 2 * kSW;      // 8 waves, two chunks each
 constexpr unsigned kPartSpin = 1u << 20;                   // ~1 s of polling per wait
-// dynamic LDS of a partitioned solve: the chain maps [kSweepChunks + G - 1][B B], then the
+// dynamic LDS of a partitioned solve: the chunk chain's maps [kSweepChunks][B B], then the
 // other workgroups' published vectors [G][16]
 // the most columns one workgroup owns (n K < 2^31: chunk_lo exact) + 1
 __host__ __device__ inline int part_ys_cols(int n, int G) { return (n + G - 1) / G + 1; }
-// double2 of the fixed part (tl, bf, bb, gv, yvl of bt_solve_chunked)
-constexpr int kPartFixedLds = kSweepChunks * 2 * 16 + 2 * (kSweepChunks + 2) * 16 + 2 * 16 +
+// double2 of the fixed part (tl, bf, bb, yvl of bt_solve_chunked)
+constexpr int kPartFixedLds = kSweepChunks * 2 * 16 + 2 * (kSweepChunks + 2) * 16 +
                               kSweepChunks * 16;
 template <int B>
 size_t part_lds_bytes(int G, int n, bool ly) {
-  return ((size_t)kPartFixedLds + (size_t)(kSweepChunks + G - 1) * B * B + kSW + (size_t)G * 16 +
+  return ((size_t)kPartFixedLds + (size_t)kSweepChunks * B * B + kSW + (size_t)G * 16 +
           (ly ? (size_t)part_ys_cols(n, G) * B + kSW : 0)) * sizeof(double2);
 }
 constexpr size_t kPartStaticLds = 256;  // (anything the compiler adds beside the dynamic block)
 constexpr size_t kPartLdsBudget = 160 * 1024;
+
+// wait until at most N of this wave's vector-memory operations are outstanding (vmcnt only;
+// they complete in issue order).  After an LDS DMA and N later loads: waits for the DMA alone,
+// where the compiler's own wait before the next LDS access would take every load with it.
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
 
 // base[byte offset]: a scalar base plus a 32-bit lane offset in bytes is the form the
 // global_load/store saddr addressing takes (no 64-bit address pair per lane)
@@ -523,8 +627,11 @@ __device__ __forceinline__ void st_gran4(unsigned long long* p, unsigned tag, do
 //   2. the chain maps staged in LDS (chunk ends' Psi_f, earlier workgroups' Phi_f); wave 0:
 //      chunk boundaries from a zero workgroup carry, y_end_k = yL_end_k + Psi_f y_end_{k-1},
 //      the last one published as granules; waves 1..7 meanwhile poll the earlier workgroups'
-//   3. wave 0: the workgroup's carry y_in = chain of the earlier workgroups' vectors through
-//      their Phi_f (G = 1: step 2 alone)
+//   3. the workgroup's carry y_in = sum over the earlier workgroups u of T(wg, u) y_end_u (the
+//      grid maps, SweepArgs::Tm; identity for u = wg - 1): every half applies up to
+//      kSweepGridMaps of them (their rows requested before step 2, so they wait in registers),
+//      wave 0 sums the halves' partials in a fixed order -- one step after the last arrival
+//      instead of a chain of G - 1 (G = 1: step 2 alone)
 //   4. every half: its chunk's carry y_{lo-1} = the zero-carry chain's value + the workgroup's
 //      prefix map (Pw) applied to y_in; fix-up (rows independent): y_i = yL_i + Psi_f[i] y_{lo-1};
 //      then backward, chunk-local:
@@ -537,7 +644,8 @@ __device__ __forceinline__ void st_gran4(unsigned long long* p, unsigned tag, do
 // a.timeout set for the host).
 template <int B, bool SR, bool SO, bool LY>
 __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int round,
-                                                 const SolveIO& io, double2* ys, bool& ok,
+                                                 const SolveIO& io, const double2 R2,
+                                                 double2* ys, bool& ok,
                                                  unsigned long long (&tk)[kSweepProfSlots]) {
   constexpr int KG = B / 2;
   constexpr int D = chunk_ring<B>();
@@ -546,21 +654,21 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
   constexpr unsigned PSB = (unsigned)PS * 16u;  // bytes of one B x B matrix
   constexpr int NQ = 4 * B;                     // granules of one published vector
   // all LDS is carved from the dynamic block (one copy however many instantiations a kernel
-  // calls): the per-chunk step vectors tl, the chunk boundaries bf / bb ([KL]: workgroup carry,
-  // [KL + 1]: zeros), the grid chain's ping-pong gv, the chunk-end (forward) / chunk-start
-  // (backward) vectors yvl, then the chain maps, the grid vectors and (LY) the B-vectors
+  // calls): the per-chunk step vectors tl (in step 3 the halves' partial sums), the chunk
+  // boundaries bf / bb ([KL]: workgroup carry, [KL + 1]: zeros), the chunk-end (forward) /
+  // chunk-start (backward) vectors yvl, then the chain maps, the grid vectors and (LY) the
+  // B-vectors
   extern __shared__ double2 part_lds[];
   auto tl = reinterpret_cast<double2 (*)[2][16]>(part_lds);
   auto bf = reinterpret_cast<double2 (*)[16]>(part_lds + KL * 2 * 16);
   auto bb = bf + (KL + 2);
-  auto gv = bb + (KL + 2);
-  auto yvl = gv + 2;
+  auto yvl = bb + (KL + 2);
   const int tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, h = lane >> 5, g = (lane >> 4) & 1, j = lane & 15;
   const int n = a.n, G = a.G, wg = blockIdx.x, K = KL * G;
-  double2* mats = part_lds + kPartFixedLds;                 // [KL + G - 1][PS]
-  double2* gin = mats + (size_t)(KL + G - 1) * PS + kSW;     // [G][16] (after the DMA slack)
+  double2* mats = part_lds + kPartFixedLds;   // [KL][PS]
+  double2* gin = mats + (size_t)KL * PS + kSW;  // [G][16] (after the DMA slack)
   // LY: the workgroup's B-vectors (y, then x) in LDS, [column - c0w][B] + a junk slot per
   // lane: no global store in the dependent loops (a wait for a ring load would also wait for
   // every older store, and a store takes ~1 us to retire)
@@ -590,7 +698,6 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
   const double2* Pf = a.Pf + sbase;
   const double2* Pb = a.Pb + sbase;
   const double2 z = make_double2(0.0, 0.0);
-  const double2 R2 = csel(row, a.tab_k[4 * jl], z);
   const double2* AW = a.tab_i;
   const double2* AE = a.tab_i + n;
   const double2* R1 = a.tab_i + 2 * n;
@@ -617,75 +724,72 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
     });
     return make_double2(sum2(acc.x), sum2(acc.y));
   };
-  // the chain maps of direction dir into LDS: map k < KL is local chunk k's end map (forward:
-  // Psi_f at its last column; backward: Psi_b at its first), map KL + q the q-th other
-  // workgroup's Phi (forward: workgroups 0 .. wg-1; backward: wg+1 .. G-1).  By LDS DMA
-  // (global_load_lds: no registers, lane-linear 1 KB per wave instruction, per-lane sources),
-  // issued at the start of a chunk-local phase so its latency overlaps that phase's first ring
-  // loads; the barrier before the maps are read waits for it.  (The last instruction may write
-  // up to 63 entries past the maps: the region has that slack.)
+  // the chain maps of direction dir into LDS: map k is local chunk k's end map (forward:
+  // Psi_f at its last column; backward: Psi_b at its first).  By LDS DMA (global_load_lds: no
+  // registers, lane-linear 1 KB per wave instruction, per-lane sources), issued at the start
+  // of a chunk-local phase so its latency overlaps that phase's first ring loads; the barrier
+  // before the maps are read waits for it.  (The last instruction may write up to 63 entries
+  // past the maps: the region has that slack.)
   auto stage = [&](int dir) {
-    const int tot = (KL + (dir == 0 ? wg : G - 1 - wg)) * PS;
+    constexpr int tot = KL * PS;
+    constexpr int NI = (tot + kPartThreads - 1) / kPartThreads;  // (a fixed count: exact vmcnt)
     const double2* cp = dir == 0 ? Pf : Pb;
-    for (int e0 = w * kSW; e0 < tot; e0 += kPartThreads) {
+    sfor<0, NI>([&](auto ic) {
+      const int e0 = w * kSW + (int)decltype(ic)::value * kPartThreads;
       const int e = min(e0 + lane, tot - 1);
       const int mi = e / PS, off = e - mi * PS;
-      const double2* src;
-      if (mi < KL) {
-        const int k = KL * wg + mi;
-        src = cp + (size_t)(dir == 0 ? chunk_lo(n, K, k + 1) - 1 : chunk_lo(n, K, k)) * PS + off;
-      } else {
-        const int og = dir == 0 ? mi - KL : wg + 1 + (mi - KL);
-        src = a.Pw + ((((size_t)s * G + og) * 2 + dir) * KL + KL - 1) * PS + off;
-      }
+      const int k = KL * wg + mi;
+      const double2* src =
+          cp + (size_t)(dir == 0 ? chunk_lo(n, K, k + 1) - 1 : chunk_lo(n, K, k)) * PS + off;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(mats + e0), 16,
-                                       0, 0);
-    }
+                                       (__attribute__((address_space(3))) void*)(mats +
+                                                                                 min(e0, tot)),
+                                       16, 0, 0);
+    });
   };
-  // waves 1..7: wait for the vectors the grid chain needs (forward: workgroups 0 .. wg-1,
-  // backward: wg+1 .. G-1) and unpack them into gin
+  // waves 1..7: wait for the vectors the grid step needs (forward: workgroups 0 .. wg-1,
+  // backward: wg+1 .. G-1) and unpack them into gin (PQ granules per lane at a time)
   auto poll = [&](int dir) {
     const int first = dir == 0 ? 0 : wg + 1;
     const int nq = (dir == 0 ? wg : G - 1 - wg) * NQ;
-    const int q0 = tid - kSW;
-    if (q0 < 0 || q0 >= nq || !ok) return;
     constexpr int PQ = 4;
     constexpr int STEP = kPartThreads - kSW;
     const unsigned tg = part_tag(a.seq, round, dir);
     const unsigned long long* gb =
         a.gran + (size_t)(dir * 2 + (round & 1)) * G * kSweepGranStride;
-    unsigned long long v[PQ];
-    unsigned spins = 0;
-    for (;;) {
-      sfor<0, PQ>([&](auto pc) {
-        const int q = min(q0 + (int)decltype(pc)::value * STEP, nq - 1);
-        v[decltype(pc)::value] = __hip_atomic_load(
-            (gu64p)(gb + (size_t)(first + q / NQ) * kSweepGranStride + q % NQ), __ATOMIC_RELAXED,
-            __HIP_MEMORY_SCOPE_AGENT);
-      });
-      bool all = true;
+    for (int q0 = tid - kSW; q0 < nq && ok; q0 += PQ * STEP) {
+      unsigned long long v[PQ];
+      unsigned spins = 0;
+      for (;;) {
+        sfor<0, PQ>([&](auto pc) {
+          const int q = min(q0 + (int)decltype(pc)::value * STEP, nq - 1);
+          v[decltype(pc)::value] = __hip_atomic_load(
+              (gu64p)(gb + (size_t)(first + q / NQ) * kSweepGranStride + q % NQ), __ATOMIC_RELAXED,
+              __HIP_MEMORY_SCOPE_AGENT);
+        });
+        bool all = true;
+        sfor<0, PQ>([&](auto pc) {
+          const int q = q0 + (int)decltype(pc)::value * STEP;
+          all = all && (q >= nq || (unsigned)(v[decltype(pc)::value] >> 32) == tg);
+        });
+        if (all) break;
+        if (++spins > kPartSpin) {
+          ok = false;
+          __hip_atomic_store((__attribute__((address_space(1))) unsigned*)a.timeout, 1u,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      unsigned* g32 = reinterpret_cast<unsigned*>(gin);
       sfor<0, PQ>([&](auto pc) {
         const int q = q0 + (int)decltype(pc)::value * STEP;
-        all = all && (q >= nq || (unsigned)(v[decltype(pc)::value] >> 32) == tg);
+        if (q < nq) {  // granule r of a vector: row r / 4, part r % 4 = x hi, x lo, y hi, y lo
+          const int gi = q / NQ, r = q % NQ;
+          g32[(gi * 16 + (r >> 2)) * 4 + ((r & 3) ^ 1)] = (unsigned)v[decltype(pc)::value];
+        }
       });
-      if (all) break;
-      if (++spins > kPartSpin) {
-        ok = false;
-        __hip_atomic_store((__attribute__((address_space(1))) unsigned*)a.timeout, 1u,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
     }
-    unsigned* g32 = reinterpret_cast<unsigned*>(gin);
-    sfor<0, PQ>([&](auto pc) {
-      const int q = q0 + (int)decltype(pc)::value * STEP;
-      if (q < nq) {  // granule r of a vector: row r / 4, part r % 4 = x hi, x lo, y hi, y lo
-        const int gi = q / NQ, r = q % NQ;
-        g32[(gi * 16 + (r >> 2)) * 4 + ((r & 3) ^ 1)] = (unsigned)v[decltype(pc)::value];
-      }
-    });
   };
   // wave 0: chain over the local chunk boundaries, bv[k] = yv[k] + map_k bv[prev], prev = the
   // neighbour chunk (forward k - 1, backward k + 1) or `start` for the first step
@@ -711,28 +815,6 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
     });
     return v;
   };
-  // wave 0: the workgroup's carry from the other workgroups' vectors (gin) through their maps,
-  // into bv[KL] (forward: from workgroup 0 up; backward: from workgroup G-1 down)
-  auto gchain = [&](double2 (*bv)[16], int dir) {
-    const int cnt = dir == 0 ? wg : G - 1 - wg;
-    if (lane < 16) gv[0][lane] = z;
-    wave_sync();
-    int cur = 0;
-    double2 m[KG];
-    ldm(m, KL + (dir == 0 ? 0 : max(cnt - 1, 0)));
-    for (int q = 0; q < cnt; ++q) {
-      const int gi = dir == 0 ? q : cnt - 1 - q;
-      double2 mn[KG];  // the next step's map (clamped: valid LDS, unused on the last step)
-      ldm(mn, KL + (dir == 0 ? min(q + 1, cnt - 1) : max(cnt - 2 - q, 0)));
-      const double2 v = cadd(gin[gi * 16 + jl], rowdot(m, &gv[cur][0]));
-      if (lane < 16) gv[cur ^ 1][lane] = v;
-      wave_sync();
-      cur ^= 1;
-      sfor<0, KG>([&](auto cc) { m[decltype(cc)::value] = mn[decltype(cc)::value]; });
-    }
-    if (lane < 16) bv[KL][lane] = gv[cur][lane];
-    wave_sync();
-  };
   // phase timing (diagnostic): thread 0's wall clock at phase ends, into tk[slot]
   const bool prof = a.prof != nullptr && tid == 0;
   unsigned long long tmark = prof ? wall_clock64() : 0;
@@ -743,6 +825,8 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
       tmark = now;
     }
   };
+  // the workgroup-map selector of this (system, workgroup, direction)
+  auto wsel = [&](int dir) { return ((size_t)s * G + wg) * 2 + dir; };
   // steps 2-3 of one direction (after the chunk-local pass and its barrier)
   auto boundaries = [&](auto dirc, double2 (*bv)[16]) {
     constexpr int dir = decltype(dirc)::value;
@@ -764,7 +848,18 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
     if (G == 1) {
       if (w == 0) chain(fwdc, bv, KL + 1);
     } else {
-      const int cnt = fwd ? wg : G - 1 - wg;
+      const int cnt = fwd ? wg : G - 1 - wg;  // (block-uniform) upstream workgroups
+      // this half's grid maps, distances d = 2 + cl + KL t: the first TM requested now (used in
+      // step 3), any further ones (G > 2 + TM KL) loaded in step 3
+      constexpr int TM = B >= 16 ? 1 : kSweepGridMapsHeld;  // (B = 16: registers)
+      double2 tm[TM][KG];
+      const double2* Tb = a.Tm + ((size_t)(s * 2 + dir) * sweep_grid_tri(G) +
+                                  sweep_grid_tri(cnt)) * PS;
+      sfor<0, TM>([&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        const int d = 2 + cl + KL * t;
+        if (d <= cnt) ld_row(tm[t], Tb, d - 2);
+      });
       if (w == 0) {
         const double2 v = chain(fwdc, bv, KL + 1);
         const bool other = fwd ? wg + 1 < G : wg > 0;  // someone reads it
@@ -776,10 +871,39 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
       }
       ok = __syncthreads_and(ok);
       mark(fwd ? 2 : 6);  // zero-carry chain + publish | polls
-      if (w == 0 && cnt > 0) gchain(bv, dir);
+      if (cnt > 0) {
+        // 3. the halves' partials sum_t T(wg, u_d) y_end(u_d), u_d = wg -+ d (unused slots: a
+        // select, so both halves of a wave run one instruction stream), then wave 0 adds them
+        // to the nearest workgroup's vector (d = 1, identity map) in the halves' order
+        double2 acc = z;
+        sfor<0, TM>([&](auto tc) {
+          constexpr int t = decltype(tc)::value;
+          if (2 + KL * t <= cnt) {
+            const int d = 2 + cl + KL * t;
+            const int gi = fwd ? max(wg - d, 0) : min(d - 1, G - 1);  // (gin slot of u_d)
+            acc = csel(d <= cnt, cadd(acc, rowdot(tm[t], &gin[gi * 16])), acc);
+          }
+        });
+        for (int t = TM; 2 + KL * t <= cnt; ++t) {
+          const int d = 2 + cl + KL * t;
+          const int gi = fwd ? max(wg - d, 0) : min(d - 1, G - 1);
+          double2 m[KG];
+          ld_row(m, Tb, min(d, cnt) - 2);
+          acc = csel(d <= cnt, cadd(acc, rowdot(m, &gin[gi * 16])), acc);
+        }
+        if (g == 0) tl[cl][0][j] = acc;
+        __syncthreads();
+        if (tid < 16) {  // (every half wrote a partial, zero if it had no map)
+          double2 p[KL];
+          sfor<0, KL>([&](auto hc) { p[decltype(hc)::value] = tl[decltype(hc)::value][0][tid]; });
+          double2 v = gin[(fwd ? wg - 1 : 0) * 16 + tid];
+          sfor<0, KL>([&](auto hc) { v = cadd(v, p[decltype(hc)::value]); });
+          bv[KL][tid] = v;
+        }
+      }
     }
     __syncthreads();
-    mark(fwd ? 3 : 7);  // grid chain
+    mark(fwd ? 3 : 7);  // grid step
   };
   // the true carry into this half's chunk (forward: y at the end of chunk cl - 1; backward: x
   // at the start of chunk cl + 1) -- the zero-carry chain's value plus the workgroup carry
@@ -794,7 +918,7 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
     if (!has_in) return &bv[edge ? KL : nb][0];
     const int idx = dir == 0 ? max(cl - 1, 0) : max(KL - 2 - cl, 0);  // (edge: unused, clamped)
     double2 m[KG];
-    ld_row(m, a.Pw + (((size_t)s * G + wg) * 2 + dir) * KL * PS, idx);
+    ld_row(m, a.Pw + wsel(dir) * KL * PS, idx);
     const double2 v = cadd(bv[edge ? KL + 1 : nb][jl], rowdot(m, &bv[KL][0]));
     if (g == 0) tl[cl][0][j] = csel(edge, bv[KL][jl], v);
     wave_sync();
@@ -815,6 +939,7 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
       if constexpr (SR) sq[r] = R1[i];
     };
     sfor<0, D>([&](auto qc) { ld(qc, decltype(qc)::value); });
+    wait_vm<D * (KG + 2 + (SR ? 1 : 0))>();  // the maps' DMA (its LDS writes), not the ring
     double2 y = z;
     for (int q0 = 0; q0 < lenw; q0 += D) {  // steps past the half's last column: unstored
       sfor<0, D>([&](auto qc) {
@@ -844,9 +969,13 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
       ld_row(mq[r], Pf, i);
       yq[r] = yget(i);
     };
-    const double2* carry = carry_in(std::integral_constant<int, 0>{}, bf);
+    // the ring's first loads ahead of the carry's map row (B = 16: after it -- registers)
+    const double2* carry = nullptr;
+    if constexpr (B >= 16) carry = carry_in(std::integral_constant<int, 0>{}, bf);
     stage(1);  // the backward chain maps, overlapping this phase
     sfor<0, D>([&](auto qc) { ld(qc, decltype(qc)::value); });
+    if constexpr (B < 16) carry = carry_in(std::integral_constant<int, 0>{}, bf);
+    else wait_vm<D * (KG + (LY ? 0 : 1))>();  // the DMA, not the ring
     for (int q0 = 0; q0 < lenw; q0 += D) {
       sfor<0, D>([&](auto qc) {
         constexpr int r = decltype(qc)::value;
@@ -897,8 +1026,10 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
       oq[r] = at(io.out, (unsigned)i * 16u + ooff);
       if constexpr (SO) sq[r] = R1[i];
     };
-    const double2* carry = carry_in(std::integral_constant<int, 1>{}, bb);
+    const double2* carry = nullptr;
+    if constexpr (B >= 16) carry = carry_in(std::integral_constant<int, 1>{}, bb);
     sfor<0, D>([&](auto qc) { ld(qc, decltype(qc)::value); });
+    if constexpr (B < 16) carry = carry_in(std::integral_constant<int, 1>{}, bb);
     for (int q0 = 0; q0 < lenw; q0 += D) {
       sfor<0, D>([&](auto qc) {
         constexpr int r = decltype(qc)::value;
@@ -932,14 +1063,23 @@ __device__ __forceinline__ SolveIO solve_io(const double2* rhs, int rhs_first, d
   return io;
 }
 
+// this lane's local-layer 1/s2 in a partitioned solve (row j = lane mod 16 of the block; 0 on
+// padding rows), loaded once per launch: a load inside a solve would sit before the chain
+// maps' LDS DMA and its use would wait for the DMA too
+template <int B>
+__device__ __forceinline__ double2 part_r2(const SweepArgs& a) {
+  const int j = threadIdx.x & 15;
+  return csel(j < B && j < a.b, a.tab_k[4 * min(j, B - 1)], make_double2(0.0, 0.0));
+}
+
 // the sequential sweeps' solves: one wave walking the columns, or (CH) the partitioned solve
 // of a.G workgroups of kSweepChunks / 2 waves (round: the solve's index in the launch)
 template <int B, bool SR, bool SO, bool CH, bool LY>
 __device__ __forceinline__ void solve(const SweepArgs& a, int s, int round, const SolveIO& io,
-                                      double2* ys, bool& ok,
+                                      const double2 R2, double2* ys, bool& ok,
                                       unsigned long long (&tk)[kSweepProfSlots]) {
   if constexpr (CH)
-    bt_solve_chunked<B, SR, SO, LY>(a, s, round, io, ys, ok, tk);
+    bt_solve_chunked<B, SR, SO, LY>(a, s, round, io, R2, ys, ok, tk);
   else
     bt_solve<B, SR, SO>(a, s, io, ys);
 }
@@ -979,7 +1119,9 @@ __global__ __launch_bounds__(CH ? kPartThreads : kSW) void sweep_forward_kernel(
   bool ok = true;
   int round = 0;
   unsigned long long tk[kSweepProfSlots] = {};
-  solve<B, false, false, CH, LY>(a, 0, round++, solve_io(u, 0, one, uF, 0, 0.0, one, n), ys, ok, tk);
+  const double2 R2 = part_r2<B>(a);
+  solve<B, false, false, CH, LY>(a, 0, round++,
+                                 solve_io(u, 0, one, uF, 0, 0.0, one, n), R2, ys, ok, tk);
   const double2* R1 = a.tab_i + 2 * n;
   int c0, c1;
   own_columns<CH>(a, c0, c1);
@@ -994,7 +1136,7 @@ __global__ __launch_bounds__(CH ? kPartThreads : kSW) void sweep_forward_kernel(
     solve<B, false, true, CH, LY>(a, m - b, round++,
                               solve_io(u + (size_t)(m - 1) * n, b - 1, one, u + (size_t)m * n,
                                        b - 1, 1.0, cneg(BS), n),
-                              ys, ok, tk);
+                              R2, ys, ok, tk);
   }
   prof_flush<CH>(a, tk);
 }
@@ -1029,19 +1171,20 @@ __global__ __launch_bounds__(CH ? kPartThreads : kSW) void sweep_backward_kernel
   bool ok = true;
   int round = 0;
   unsigned long long tk[kSweepProfSlots] = {};
+  const double2 R2 = part_r2<B>(a);
   for (int m = n - 1; m >= b + 1; --m) {
     const double2 BN = a.tab_glob[4 * (m - 1) + 2];  // c4 of global layer m-1 (code.py:131-140)
     solve<B, true, false, CH, LY>(a, m - b, round++,
                               solve_io(u + (size_t)m * n, b - 1, BN, u + (size_t)(m - 1) * n,
                                        b - 1, 1.0, mone, n),
-                              ys, ok, tk);
+                              R2, ys, ok, tk);
   }
   // H_F is block diagonal: only its last layer sees the (last-layer-only) right-hand side
   const double2 BN = a.tab_glob[4 * (b - 1) + 2];
   solve<B, true, false, CH, LY>(a, 0, round++,
                             solve_io(u + (size_t)b * n, b - 1, BN, uF + (size_t)(b - 1) * n, b - 1,
                                      1.0, mone, n),
-                            ys, ok, tk);
+                            R2, ys, ok, tk);
   prof_flush<CH>(a, tk);
   int c0, c1;
   own_columns<CH>(a, c0, c1);
@@ -1113,6 +1256,9 @@ void launch_all(const SweepArgs& a, int what, double2* u, double2* uF, int asis,
       hipLaunchKernelGGL((sweep_chunk_setup_kernel<B>), dim3(a.nsys * a.chunks), dim3(kSW), 0,
                          st, a);
       hipLaunchKernelGGL((sweep_wg_setup_kernel<B>), dim3(a.nsys * a.G), dim3(kSW), 0, st, a);
+      if (a.G > 2)
+        hipLaunchKernelGGL((sweep_grid_setup_kernel<B>), dim3(a.nsys * 2 * a.G), dim3(kSW), 0,
+                           st, a);
       break;
     default:
       break;

@@ -30,8 +30,17 @@ struct SweepArgs {
   // per workgroup the prefix (forward, 0) / suffix (backward, 1) products of its chunk maps
   // (sweep_wg_setup_kernel).
   // Carries cross workgroups as tagged granules, gran [2 dir][2 parity][G][kSweepGranStride].
+  // Tm [nsys][2][sweep_grid_tri(G)][B][B]: the grid maps of the product-form grid step,
+  // T(w, u) = Phi_{w-1} .. Phi_{u+1} (forward; backward Phi_{w+1} .. Phi_{u-1}) for every
+  // workgroup w and upstream workgroup u at distance d = |w - u| >= 2, at
+  // sweep_grid_tri(cnt_w) + d - 2 (cnt_w: the workgroups upstream of w; sweep_grid_setup_kernel).
+  // Rw [nsys][G][2][8][B][B] and Sw [nsys][G][2][16][B][B]: the split chunk chain's second-half
+  // prefixes and the suffix products that publish the workgroup's vector (sweep_wg_setup_kernel)
   int G;
   double2* Pw;
+  double2* Rw;
+  double2* Sw;
+  double2* Tm;
   unsigned long long* gran;
   unsigned* timeout;  // set when a grid wait gives up (the output is then garbage)
   unsigned seq;       // launch sequence number of the granule tags (1 .. 2^17 - 1)
@@ -61,18 +70,27 @@ bool sweep_coop_launch();
 int sweep_block(int b);
 size_t sweep_scratch_per_wave(int n);  // padded block size B (4, 8, 12, 16) or 0 if b > 16
 // what: 0 factor (one wave per system), 1 forward sweep, 2 middle sweep, 3 backward sweep,
-// 4 the chunk products Psi_f / Psi_b and the workgroup products Pw (after 0; needs a.chunks =
-// kSweepChunks a.G > 0, Pf, Pb, Pw).  With a.chunks > 0 the forward and backward sweeps run
-// every solve partitioned over the chunks: a.G workgroups of kSweepChunks / 2 waves (one
-// cooperative launch per sweep when G > 1), dependent depth ~2 (n / chunks + 2 kSweepChunks
-// + G) steps instead of 2 n.
+// 4 the chunk products Psi_f / Psi_b, the workgroup products Pw and the grid maps Tm (after 0;
+// needs a.chunks = kSweepChunks a.G > 0, Pf, Pb, Pw, Tm).  With a.chunks > 0 the forward and
+// backward sweeps run every solve partitioned over the chunks: a.G workgroups of kSweepChunks
+// / 2 waves (one cooperative launch per sweep when G > 1), dependent depth ~2 (n / chunks +
+// kSweepChunks + 2) steps instead of 2 n.
 void launch_sweep(const SweepArgs& a, int what, double2* u, double2* uF, int asis,
                   hipStream_t st);
 constexpr int kSweepChunks = 16;  // chunks per workgroup of a partitioned solve (two per wave)
 constexpr int kSweepGranStride = 64;  // u64 granules per (direction, parity, workgroup)
+// grid maps per half-wave of the product-form grid step requested ahead of the grid exchange
+// (held in registers; with more than 2 + kSweepChunks kSweepGridMapsHeld workgroups the rest
+// is loaded after it); kSweepMaxWgs the cap of a launch
+constexpr int kSweepGridMapsHeld = 2;
+constexpr int kSweepMaxWgs = 64;
+// grid maps of a workgroup with cnt upstream workgroups before its own (distances 2 .. cnt)
+__host__ __device__ inline size_t sweep_grid_tri(int cnt) {
+  return cnt >= 2 ? (size_t)(cnt - 1) * (size_t)(cnt - 2) / 2 : 0;
+}
 // scratch (double2) of one partitioned solve: the n B-vectors + per-thread dummy slots
 size_t sweep_chunk_scratch(int n);
-// largest workgroup count of a partitioned solve for block size B (LDS of the grid chain)
+// largest workgroup count of a partitioned solve for block size B
 int sweep_part_max_wgs(int B);
 // whether a partitioned solve over G workgroups keeps its B-vectors in LDS (else in yscr)
 bool sweep_part_ys_lds(int B, int G, int n);

@@ -318,8 +318,9 @@ int hh_op_sweep_workgroups(hh_op* op, int workgroups, int* active);
  * per-workgroup accumulators, 0 stops; phase_us (optional, cap entries) first receives the
  * sums so far, in microseconds of workgroup w's thread-0 wall clock: phase_us[16 w + k], k =
  * 0 chunk-local forward, 1 / 5 map staging, 2 / 6 zero-carry chunk chain + publish | polls,
- * 3 / 7 grid chain + chunk chain, 4 fix-up + chunk-local backward, 8 fix-up + output (k = 1-3
- * forward recurrence, 5-7 backward), summed over every solve of every sweep since enabled. */
+ * 3 / 7 grid step, 4 fix-up + chunk-local backward, 8 fix-up + output (k = 1-3 forward
+ * recurrence, 5-7 backward), summed over every solve of every sweep since enabled; up to 64
+ * workgroups (w < 64). */
 int hh_op_sweep_profile(hh_op* op, int enable, double* phase_us, int cap);
 /* Process-wide tuning of the Krylov streaming kernels (multidot / update): non-temporal
  * basis loads on (1) / off (0) / by vector length (-1, default: on above 2^21 rank-local

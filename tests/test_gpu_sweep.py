@@ -204,17 +204,20 @@ def test_sweep_thomas_as_is_matches_reference_golden(ctx, name, form):
                                           (200, 16, "c2", 0), (257, 3, "c1", 0),
                                           (257, 3, "c1", 8), (331, 12, "c2", 0),
                                           (331, 12, "c2", 2), (700, 12, "c1", 0),
-                                          (700, 16, "c1", 0)])
+                                          (700, 16, "c1", 0), (700, 16, "c1", 21),
+                                          (1300, 12, "c2", 40)])
 def test_sweep_partitioned_vs_sequential_and_oracle(ctx, n, b, kind, wgs):
     """ragged chunks (n not a multiple of 8), every block size B = 4, 8, 12, 16, both sweeps,
-    one workgroup and several (wgs 0: by n -- 700: 10 workgroups, every solve's carries cross
-    workgroups through the granule exchange)"""
+    one workgroup and several (wgs 0: by n -- 700: 21 workgroups, every solve's carries cross
+    workgroups through the granule exchange; 21 at B = 16 and 40 at B = 12: more upstream
+    workgroups than the grid maps each half-wave holds ahead of the exchange, so the rest are
+    loaded after it)"""
     om, h, eta = O.problem_params(n, b, 5.0, 2.0)
     cm = medium(kind, n)
     A = H.build_A_matrix(b, 81.0, eta, om, h, n, cm, context=ctx)
     x = rand_complex(n * n, n + 3)
     st = O.SweepState(b, 81.0, eta, om, h, n, cm) if n <= 200 else None
-    want = min(wgs if wgs else n // 64, 32 if b <= 12 else 12, n // 32) or 1
+    want = min(wgs if wgs else n // 32, 64, n // 32) or 1
     for reference in (False, True):
         Mp = H.Sweeping(A, reference=reference, form="thomas", workgroups=wgs)
         yp = Mp @ x
@@ -260,13 +263,13 @@ def test_sweep_partitioned_large_linearity(ctx):
 
 def test_sweep_partitioned_workgroups_agree_with_dense(ctx):
     """n = 1023 (the dense form's largest persistent-chain size): the partitioned apply over
-    1, 4 and 15 (auto) workgroups agrees with the dense transfer form to rounding"""
+    1, 4, 15 and 31 (auto) workgroups agrees with the dense transfer form to rounding"""
     n, b = 1023, 12
     om, h, eta = O.problem_params(n, b, 128.0, 2.0)
     A = H.build_A_matrix(b, 100.0, eta, om, h, n, O.init_c1_mat(.5, .5, n), context=ctx)
     x = rand_complex(n * n, 11)
     yd = H.Sweeping(A, form="dense") @ x
-    for wgs, want in ((1, 1), (4, 4), (0, 15)):
+    for wgs, want in ((1, 1), (4, 4), (15, 15), (0, 31)):
         M = H.Sweeping(A, form="thomas", workgroups=wgs)
         y = M @ x
         assert M.partitioned and M.workgroups == want

@@ -39,8 +39,8 @@ for n in [int(v) for v in args] or [1023]:
         A.apply_device(x, y, _ffi.HH_APPLY_PREC)
     A.ctx.synchronize()
     t_apply = (time.perf_counter() - t0) / reps
-    out = (ctypes.c_double * (32 * 16))()
-    _ffi.check(_ffi.lib.hh_op_sweep_profile(A.handle, 0, out, 32 * 16))
+    out = (ctypes.c_double * (64 * 16))()
+    _ffi.check(_ffi.lib.hh_op_sweep_profile(A.handle, 0, out, 64 * 16))
     G = M.workgroups
     ph = np.array(out[:G * 16]).reshape(G, 16)[:, :9]
     solves = reps * 2 * (n - b + 1)  # forward + backward sweeps, one H_F solve each
