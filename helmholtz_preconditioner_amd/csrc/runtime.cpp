@@ -224,8 +224,6 @@ struct hh_op {
   double2* sw_Pb = nullptr;
   double2* sw_Pw = nullptr;     // workgroup maps of the multi-workgroup partitioned solves
   double2* sw_Tm = nullptr;     // their grid maps
-  double2* sw_Rw = nullptr;     // split-chain and suffix workgroup maps
-  double2* sw_Sw = nullptr;
   unsigned long long* sw_gran = nullptr;  // their grid-exchange granules
   int sw_wgs = 0;               // requested workgroups per partitioned solve (0: by n)
   unsigned long long* sw_prof = nullptr;  // diagnostic phase ticks (hh_op_sweep_profile)
@@ -1310,8 +1308,6 @@ static void op_release(hh_op* op) {
   dfree(op->sw_Pb);
   dfree(op->sw_Pw);
   dfree(op->sw_Tm);
-  dfree(op->sw_Rw);
-  dfree(op->sw_Sw);
   dfree(op->sw_gran);
   dfree(op->sw_prof);
   dfree(op->sw_y);
@@ -1418,15 +1414,13 @@ static void sweep_part_release(hh_op* op) {
   dfree(op->sw_Pb);
   dfree(op->sw_Pw);
   dfree(op->sw_Tm);
-  dfree(op->sw_Rw);
-  dfree(op->sw_Sw);
   dfree(op->sw_gran);
-  op->sw_Pf = op->sw_Pb = op->sw_Pw = op->sw_Tm = op->sw_Rw = op->sw_Sw = nullptr;
+  op->sw_Pf = op->sw_Pb = op->sw_Pw = op->sw_Tm = nullptr;
   op->sw_gran = nullptr;
   SweepArgs& a = op->sweep;
   a.chunks = 0;
   a.G = 0;
-  a.Pf = a.Pb = a.Pw = a.Tm = a.Rw = a.Sw = nullptr;
+  a.Pf = a.Pb = a.Pw = a.Tm = nullptr;
   a.gran = nullptr;
 }
 
@@ -1461,16 +1455,12 @@ static void sweep_chunk_configure(hh_op* op) {
   const size_t telems = (size_t)a.nsys * 2 * sweep_grid_tri(G) * B * B;
   size_t free_b = 0, total_b = 0;
   HIPC(hipMemGetInfo(&free_b, &total_b));
-  const size_t relems = welems / 2;  // Rw: 8 maps per (system, workgroup, direction); Sw: 16
-  if ((2 * elems + 2 * welems + relems + telems) * sizeof(double2) > free_b / 10 * 8)
-    return;  // sequential solves
+  if ((2 * elems + welems + telems) * sizeof(double2) > free_b / 10 * 8) return;  // sequential
   try {
     op->sw_Pf = dalloc<double2>(elems);
     op->sw_Pb = dalloc<double2>(elems);
     op->sw_Pw = dalloc<double2>(welems);
     op->sw_Tm = dalloc<double2>(std::max<size_t>(telems, 1));
-    op->sw_Rw = dalloc<double2>(relems);
-    op->sw_Sw = dalloc<double2>(welems);
     op->sw_gran = dalloc<unsigned long long>(sweep_part_granules(G));
   } catch (...) {
     sweep_part_release(op);
@@ -1483,8 +1473,6 @@ static void sweep_chunk_configure(hh_op* op) {
   a.Pb = op->sw_Pb;
   a.Pw = op->sw_Pw;
   a.Tm = op->sw_Tm;
-  a.Rw = op->sw_Rw;
-  a.Sw = op->sw_Sw;
   a.gran = op->sw_gran;
   a.timeout = reinterpret_cast<unsigned*>(op->red + kRedTimeout);
   launch_sweep(a, 4, nullptr, nullptr, 0, op->ctx->stream);

@@ -398,20 +398,15 @@ __global__ __launch_bounds__(kSW) void sweep_chunk_setup_kernel(const SweepArgs 
   }
 }
 
-// Setup: the workgroup maps of one (system, workgroup) per wave (after the chunk products).
-// With F_p the map of the chunk at chain position p (forward: chunk p, Psi_f at its last column;
-// backward: chunk 15 - p, Psi_b at its first column):
-//   Pw[..][dir][p] = F_p .. F_0, the map from the workgroup's carry to the end of position p
-//     ([15] is the whole workgroup's map Phi);
-//   Rw[..][dir][t] = F_{8+t} .. F_8 (t < 7), from the end of position 7 to the end of 8 + t
-//     (the second half of the split chunk chain);
-//   Sw[..][dir][p] = F_15 .. F_{p+1} (p < 15), from the end of position p to the workgroup's
-//     end (the suffix sum that publishes the workgroup's zero-carry vector).
+// Setup: the workgroup maps of one (system, workgroup) per wave (after the chunk products),
+// with F_k = Psi_f[end_k], B_k = Psi_b[lo_k] the chunk maps (end_k / lo_k: the chunk's last /
+// first column): forward Pw[..][0][q] = F_q .. F_0 (the map from the workgroup's carry to the
+// end of chunk q), backward Pw[..][1][q] = B_{15-q} .. B_15 (from the carry past the workgroup
+// to the start of chunk 15 - q); [15] is the whole workgroup's map Phi.
 template <int B>
 __global__ __launch_bounds__(kSW) void sweep_wg_setup_kernel(const SweepArgs a) {
   constexpr int KG = B / kGroups;
   constexpr size_t PS = (size_t)B * B;
-  constexpr int KL = kSweepChunks;
   __shared__ double2 Q[2][B][B];
   const int n = a.n, G = a.G, K = a.chunks;
   const int s = blockIdx.x / G, wg = blockIdx.x % G;
@@ -421,74 +416,41 @@ __global__ __launch_bounds__(kSW) void sweep_wg_setup_kernel(const SweepArgs a) 
   const double2 z = make_double2(0.0, 0.0);
   for (int dir = 0; dir < 2; ++dir) {
     const double2* src = (dir == 0 ? a.Pf : a.Pb) + (size_t)s * n * PS;
-    const size_t wsel = ((size_t)s * G + wg) * 2 + dir;
-    auto fmap = [&](int p) {  // F_p
-      const int k = KL * wg + (dir == 0 ? p : KL - 1 - p);
-      return src + (size_t)(dir == 0 ? chunk_lo(n, K, k + 1) - 1 : chunk_lo(n, K, k)) * PS;
-    };
-    auto put = [&](const double2 (&v)[KG], int t, double2* out) {
-      if (row) {
-        sfor<0, KG>([&](auto c2) {
-          constexpr int c = decltype(c2)::value;
-          Q[t & 1][j][g * KG + c] = v[c];
-          out[pidx<B>(j, g * KG + c)] = v[c];
-        });
-      }
-      wave_sync();
-    };
-    // left products F_{p1-1} .. F_{p0} into out[0 .. p1-p0)
-    auto left = [&](int p0, int p1, double2* out) {
-      for (int t = 0; t < p1 - p0; ++t) {
-        const double2* f = fmap(p0 + t);
-        double2 prow[B];
-        sfor<0, B>([&](auto mc) {
-          constexpr int m = decltype(mc)::value;
-          prow[m] = f[pidx<B>(jl, m)];
-        });
-        double2 v[KG];
-        sfor<0, KG>([&](auto c2) {
-          constexpr int c = decltype(c2)::value;
-          const int cx = g * KG + c;
-          double2 acc = z;
-          if (t == 0) {
-            sfor<0, B>([&](auto mc) {
-              constexpr int m = decltype(mc)::value;
-              acc = csel(m == cx, prow[m], acc);
-            });
-          } else {
-            sfor<0, B>([&](auto mc) {
-              constexpr int m = decltype(mc)::value;
-              acc = cfma(prow[m], Q[(t - 1) & 1][m][cx], acc);
-            });
-          }
-          v[c] = acc;
-        });
-        put(v, t, out + (size_t)t * PS);
-      }
-    };
-    left(0, KL, a.Pw + wsel * KL * PS);
-    left(KL / 2, KL - 1, a.Rw + wsel * (KL / 2) * PS);
-    // right products: Sw[p] = Sw[p+1] F_{p+1}, Sw[14] = F_15
-    double2* sw = a.Sw + wsel * KL * PS;
-    for (int t = 0; t < KL - 1; ++t) {
-      const int p = KL - 2 - t;
-      const double2* f = fmap(p + 1);
+    double2* out = a.Pw + (((size_t)s * G + wg) * 2 + dir) * kSweepChunks * PS;
+    for (int q = 0; q < kSweepChunks; ++q) {  // forward: chunks in order; backward: from the last
+      const int k = kSweepChunks * wg + (dir == 0 ? q : kSweepChunks - 1 - q);
+      const int col = dir == 0 ? chunk_lo(n, K, k + 1) - 1 : chunk_lo(n, K, k);
+      double2 prow[B];
+      sfor<0, B>([&](auto mc) {
+        constexpr int m = decltype(mc)::value;
+        prow[m] = src[(size_t)col * PS + pidx<B>(jl, m)];
+      });
       double2 v[KG];
       sfor<0, KG>([&](auto c2) {
         constexpr int c = decltype(c2)::value;
         const int cx = g * KG + c;
         double2 acc = z;
-        if (t == 0) {
-          acc = f[pidx<B>(jl, cx)];
+        if (q == 0) {
+          sfor<0, B>([&](auto mc) {
+            constexpr int m = decltype(mc)::value;
+            acc = csel(m == cx, prow[m], acc);
+          });
         } else {
           sfor<0, B>([&](auto mc) {
             constexpr int m = decltype(mc)::value;
-            acc = cfma(Q[(t - 1) & 1][jl][m], f[pidx<B>(m, cx)], acc);
+            acc = cfma(prow[m], Q[(q - 1) & 1][m][cx], acc);
           });
         }
         v[c] = acc;
       });
-      put(v, t, sw + (size_t)p * PS);
+      if (row) {
+        sfor<0, KG>([&](auto c2) {
+          constexpr int c = decltype(c2)::value;
+          Q[q & 1][j][g * KG + c] = v[c];
+          out[(size_t)q * PS + pidx<B>(j, g * KG + c)] = v[c];
+        });
+      }
+      wave_sync();
     }
   }
 }
@@ -850,7 +812,7 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
     } else {
       const int cnt = fwd ? wg : G - 1 - wg;  // (block-uniform) upstream workgroups
       // this half's grid maps, distances d = 2 + cl + KL t: the first TM requested now (used in
-      // step 3), any further ones (G > 2 + TM KL) loaded in step 3
+      // step 3), any beyond the next T2 (G > 2 + (TM + T2) KL) loaded in step 3
       constexpr int TM = B >= 16 ? 1 : kSweepGridMapsHeld;  // (B = 16: registers)
       double2 tm[TM][KG];
       const double2* Tb = a.Tm + ((size_t)(s * 2 + dir) * sweep_grid_tri(G) +
@@ -860,13 +822,26 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
         const int d = 2 + cl + KL * t;
         if (d <= cnt) ld_row(tm[t], Tb, d - 2);
       });
+      // the next T2 of them (G > 2 + TM KL): waves 1..7 request theirs before polling, wave 0
+      // after its chain (held through the polls, not through the chain: registers)
+      constexpr int T2 = 1;
+      double2 tm2[T2][KG];
+      auto load_tm2 = [&]() {
+        if (2 + KL * TM <= cnt)
+          sfor<0, T2>([&](auto tc) {
+            const int d = 2 + cl + KL * (TM + (int)decltype(tc)::value);
+            if (d <= cnt) ld_row(tm2[decltype(tc)::value], Tb, d - 2);
+          });
+      };
       if (w == 0) {
         const double2 v = chain(fwdc, bv, KL + 1);
         const bool other = fwd ? wg + 1 < G : wg > 0;  // someone reads it
         if (other && lane < B)
           st_gran4(a.gran + ((size_t)(dir * 2 + (round & 1)) * G + wg) * kSweepGranStride +
                        4 * lane, part_tag(a.seq, round, dir), v);
+        load_tm2();
       } else {
+        load_tm2();
         poll(dir);
       }
       ok = __syncthreads_and(ok);
@@ -884,7 +859,15 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
             acc = csel(d <= cnt, cadd(acc, rowdot(tm[t], &gin[gi * 16])), acc);
           }
         });
-        for (int t = TM; 2 + KL * t <= cnt; ++t) {
+        sfor<0, T2>([&](auto tc) {
+          constexpr int t = TM + decltype(tc)::value;
+          if (2 + KL * t <= cnt) {
+            const int d = 2 + cl + KL * t;
+            const int gi = fwd ? max(wg - d, 0) : min(d - 1, G - 1);
+            acc = csel(d <= cnt, cadd(acc, rowdot(tm2[decltype(tc)::value], &gin[gi * 16])), acc);
+          }
+        });
+        for (int t = TM + T2; 2 + KL * t <= cnt; ++t) {
           const int d = 2 + cl + KL * t;
           const int gi = fwd ? max(wg - d, 0) : min(d - 1, G - 1);
           double2 m[KG];

@@ -34,12 +34,8 @@ struct SweepArgs {
   // T(w, u) = Phi_{w-1} .. Phi_{u+1} (forward; backward Phi_{w+1} .. Phi_{u-1}) for every
   // workgroup w and upstream workgroup u at distance d = |w - u| >= 2, at
   // sweep_grid_tri(cnt_w) + d - 2 (cnt_w: the workgroups upstream of w; sweep_grid_setup_kernel).
-  // Rw [nsys][G][2][8][B][B] and Sw [nsys][G][2][16][B][B]: the split chunk chain's second-half
-  // prefixes and the suffix products that publish the workgroup's vector (sweep_wg_setup_kernel)
   int G;
   double2* Pw;
-  double2* Rw;
-  double2* Sw;
   double2* Tm;
   unsigned long long* gran;
   unsigned* timeout;  // set when a grid wait gives up (the output is then garbage)
