@@ -761,17 +761,32 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
     const double2* mr = mats + mi * PS + pidx<B>(jl, g * KG);
     sfor<0, KG>([&](auto cc) { m[decltype(cc)::value] = mr[decltype(cc)::value * 2 * B]; });
   };
+  // (the step's chunk-end value is read a step ahead too, and the row sum runs as two
+  // interleaved FMA chains: the step's dependent span is the LDS round trip of bv, half the
+  // row's FMAs and the half-wave sum)
   auto chain = [&](auto fwdc, double2 (*bv)[16], int start) {
     constexpr bool fwd = decltype(fwdc)::value;
     double2 v = z;
-    double2 mq[2][KG];
+    double2 mq[2][KG], yq[2];
     ldm(mq[0], fwd ? 0 : KL - 1);
+    yq[0] = yvl[fwd ? 0 : KL - 1][jl];
     sfor<0, KL>([&](auto qc) {
       constexpr int q = decltype(qc)::value;
       constexpr int k = fwd ? q : KL - 1 - q;
-      if constexpr (q + 1 < KL) ldm(mq[(q + 1) & 1], fwd ? k + 1 : k - 1);
+      if constexpr (q + 1 < KL) {
+        ldm(mq[(q + 1) & 1], fwd ? k + 1 : k - 1);
+        yq[(q + 1) & 1] = yvl[fwd ? k + 1 : k - 1][jl];
+      }
       const int prev = q == 0 ? start : (fwd ? k - 1 : k + 1);
-      v = cadd(yvl[k][jl], rowdot(mq[q & 1], &bv[prev][0]));
+      const double2* vec = &bv[prev][0];
+      double2 a0 = z, a1 = z;
+      sfor<0, KG>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        if constexpr (c % 2 == 0) a0 = cfma(mq[q & 1][c], vec[g * KG + c], a0);
+        else a1 = cfma(mq[q & 1][c], vec[g * KG + c], a1);
+      });
+      const double2 acc = cadd(a0, a1);
+      v = cadd(yq[q & 1], make_double2(sum2(acc.x), sum2(acc.y)));
       if (lane < 16) bv[k][lane] = v;
       wave_sync();
     });
