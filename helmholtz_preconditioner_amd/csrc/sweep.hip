@@ -212,6 +212,7 @@ struct SolveIO {
   size_t out_ld;
   double alpha_old;
   double2 omul;
+  int s_next;  // the launch's next partitioned solve's system (prefetched), or -1
 };
 
 template <int B, bool SR, bool SO>
@@ -512,6 +513,9 @@ __global__ __launch_bounds__(kSW) void sweep_grid_setup_kernel(const SweepArgs a
   }
 }
 
+#ifndef HH_SWEEP_TOUCH
+#define HH_SWEEP_TOUCH 1
+#endif
 template <int B>
 constexpr int chunk_ring() { return B <= 4 ? 4 : (B == 8 ? 3 : 2); }  // (no spills at 256 VGPRs)
 template <int B>
@@ -804,6 +808,47 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
   };
   // the workgroup-map selector of this (system, workgroup, direction)
   auto wsel = [&](int dir) { return ((size_t)s * G + wg) * 2 + dir; };
+  // waves 1..7 before their polls: L2 prefetch of what every chunk loads first after this
+  // exchange -- forward: its fix-up ring's first Psi_f and backward ring's first P matrices,
+  // its workgroup-map row; backward: its fix-up ring's first Psi_b, its map row and the next
+  // solve's first P matrices.  One 4-byte LDS-DMA load per 128-byte line into the slack after
+  // the maps (no register held; the first poll's wait, which these waves pay anyway, covers
+  // it -- the wave that runs the chain issues none, its LDS reads would wait for them).
+  auto touch_next = [&](int dir, int s_next) {
+    constexpr int LN = (int)((PSB + 127u) / 128u);  // lines of one B x B matrix
+    constexpr int NMAT = 5;                         // matrices per chunk
+    constexpr int TOT = KL * NMAT * LN;
+    constexpr int STEP = kPartThreads - kSW;
+    constexpr int NIT = (TOT + STEP - 1) / STEP;
+    const bool has_in = dir == 0 ? wg > 0 : wg < G - 1;
+#pragma unroll 1
+    for (int it = 0; it < NIT; ++it) {  // (not unrolled: registers; the polls wait anyway)
+      const int idx = min(tid - kSW + it * STEP, TOT - 1);
+      const int c = idx / (NMAT * LN), r = idx - c * (NMAT * LN);
+      const int m = r / LN, l = r - m * LN;
+      const int k = KL * wg + c;
+      const int clo = chunk_lo(n, K, k), chi = chunk_lo(n, K, k + 1);
+      const double2* base;
+      int i;
+      if (m < 2) {  // the fix-up ring's first two
+        base = dir == 0 ? Pf : Pb;
+        i = clo + min(m, chi - clo - 1);
+      } else if (m == 2) {  // the carry's workgroup-map row (none for an edge workgroup)
+        base = has_in ? a.Pw + wsel(dir) * KL * PS : (dir == 0 ? Pf : Pb);
+        i = has_in ? (dir == 0 ? max(c - 1, 0) : max(KL - 2 - c, 0)) : clo;
+      } else if (dir == 0) {  // the backward chunk-local ring's first two
+        base = P;
+        i = chi - 1 - min(m - 3, chi - clo - 1);
+      } else {  // the next solve's forward ring
+        base = s_next >= 0 ? a.P + (size_t)s_next * n * PS : P;
+        i = clo + min(m - 3, chi - clo - 1);
+      }
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(reinterpret_cast<const char*>(base) +
+                                                          (size_t)i * PSB + (unsigned)l * 128u),
+          (__attribute__((address_space(3))) void*)(mats + KL * PS), 4, 0, 0);
+    }
+  };
   // steps 2-3 of one direction (after the chunk-local pass and its barrier)
   auto boundaries = [&](auto dirc, double2 (*bv)[16]) {
     constexpr int dir = decltype(dirc)::value;
@@ -856,6 +901,9 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
                        4 * lane, part_tag(a.seq, round, dir), v);
         load_tm2();
       } else {
+#if HH_SWEEP_TOUCH
+        touch_next(dir, io.s_next);
+#endif
         load_tm2();
         poll(dir);
       }
@@ -1047,7 +1095,7 @@ __device__ __forceinline__ void bt_solve_chunked(const SweepArgs& a, int s, int 
 
 __device__ __forceinline__ SolveIO solve_io(const double2* rhs, int rhs_first, double2 rmul,
                                             double2* out, int out_first, double alpha_old,
-                                            double2 omul, size_t ld) {
+                                            double2 omul, size_t ld, int s_next = -1) {
   SolveIO io;
   io.rhs = rhs;
   io.rhs_first = rhs_first;
@@ -1058,6 +1106,7 @@ __device__ __forceinline__ SolveIO solve_io(const double2* rhs, int rhs_first, d
   io.out_ld = ld;
   io.alpha_old = alpha_old;
   io.omul = omul;
+  io.s_next = s_next;
   return io;
 }
 
@@ -1119,7 +1168,8 @@ __global__ __launch_bounds__(CH ? kPartThreads : kSW) void sweep_forward_kernel(
   unsigned long long tk[kSweepProfSlots] = {};
   const double2 R2 = part_r2<B>(a);
   solve<B, false, false, CH, LY>(a, 0, round++,
-                                 solve_io(u, 0, one, uF, 0, 0.0, one, n), R2, ys, ok, tk);
+                                 solve_io(u, 0, one, uF, 0, 0.0, one, n, b + 1 < n ? 1 : -1),
+                                 R2, ys, ok, tk);
   const double2* R1 = a.tab_i + 2 * n;
   int c0, c1;
   own_columns<CH>(a, c0, c1);
@@ -1133,7 +1183,7 @@ __global__ __launch_bounds__(CH ? kPartThreads : kSW) void sweep_forward_kernel(
     const double2 BS = a.tab_glob[4 * m + 1];
     solve<B, false, true, CH, LY>(a, m - b, round++,
                               solve_io(u + (size_t)(m - 1) * n, b - 1, one, u + (size_t)m * n,
-                                       b - 1, 1.0, cneg(BS), n),
+                                       b - 1, 1.0, cneg(BS), n, m + 1 < n ? m + 1 - b : -1),
                               R2, ys, ok, tk);
   }
   prof_flush<CH>(a, tk);
@@ -1174,7 +1224,7 @@ __global__ __launch_bounds__(CH ? kPartThreads : kSW) void sweep_backward_kernel
     const double2 BN = a.tab_glob[4 * (m - 1) + 2];  // c4 of global layer m-1 (code.py:131-140)
     solve<B, true, false, CH, LY>(a, m - b, round++,
                               solve_io(u + (size_t)m * n, b - 1, BN, u + (size_t)(m - 1) * n,
-                                       b - 1, 1.0, mone, n),
+                                       b - 1, 1.0, mone, n, m - 1 - b),
                               R2, ys, ok, tk);
   }
   // H_F is block diagonal: only its last layer sees the (last-layer-only) right-hand side
