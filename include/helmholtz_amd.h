@@ -307,9 +307,9 @@ int hh_op_sl_fusion(hh_op* op, int enable);
  * 0 for sequential ones. */
 int hh_op_sweep_mode(hh_op* op, int mode, int* active);
 /* Workgroups sharing each partitioned block-Thomas solve (speed only; results agree to
- * rounding): 0 (default) by n (about 4 columns per chunk, at most 32 -- 12 for PML widths
- * b > 12 -- and the CU count), else that many, clamped to the same limits and to 2 columns
- * per chunk.  G > 1 runs each forward / backward sweep as one cooperative launch of G
+ * rounding): 0 (default) by n (2 columns per chunk, at most 64 and the CU count, fewer when
+ * the solve's vectors would not fit LDS), else that many, clamped to 64, the CU count and 2
+ * columns per chunk.  G > 1 runs each forward / backward sweep as one cooperative launch of G
  * workgroups that exchange the solves' chunk carries through device memory.  Applies at the
  * next sweeping setup, or at once if the operator is already factored.  active (optional)
  * receives the workgroup count in use, 0 when the solves are not partitioned. */
