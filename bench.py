@@ -115,7 +115,9 @@ def parse():
                    help="timed applies of the same grid with a constant medium (reported as "
                         "spmv_constant_medium; 0 = skip; not run when --medium const)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-gmres-iters", type=int, default=4)
+    p.add_argument("--cpu-gmres-iters", type=int, default=0,
+                   help="inner iterations of the CPU GMRES baseline (0 = one restart cycle, "
+                        "BASELINE.md 2: --restart iterations)")
     p.add_argument("--virtual-slabs", type=int, default=1)
     p.add_argument("--rotate", type=int, default=3,
                    help="distinct (x, y) vector pairs the timed applies cycle through: like the "
@@ -163,26 +165,28 @@ def local_f1(omega, n, j0, j1, r1=.5, r2=.125):
     return np.exp(-(4 * omega / np.pi) ** 2 * ((x[None, :] - r1) ** 2 + (yy - r2) ** 2)).ravel()
 
 
-TRAFFIC_DB = "profiles/r03_pmc_traffic.json"
+TRAFFIC_DB = "profiles/r05_pmc_traffic.json"
+TRAFFIC_DB_R03 = "profiles/r03_pmc_traffic.json"
 
 
-def measured_traffic(n, medium, world, stencil=5):
-    """HBM bytes per apply-kernel launch from the rocprofv3 PMC passes committed under profiles/
-    (FETCH_SIZE x2 + WRITE_SIZE in separate passes, the gfx950 correction of
-    MI355X_MICROARCH.md; tools/gpu_session.sh step `pmcset` -> tools/pmc_traffic.py) for this
-    grid, medium and stencil.  PMC counters cannot be read inside the timed run, so this is the
-    committed measurement of the same kernel and workload: (bytes, ratio to the algorithmic
-    bytes, source), or Nones for a workload without a record (e.g. a rank's slab at N > 1)."""
-    path = os.path.join(ROOT, TRAFFIC_DB)
-    if world != 1 or not os.path.exists(path):
-        return None, None, None
+def measured_traffic(n, medium, rows, stencil=5):
+    """HBM traffic of the apply kernel per launch, as a ratio to its algorithmic bytes, from the
+    rocprofv3 PMC passes committed under profiles/ (FETCH_SIZE x2 + WRITE_SIZE in separate
+    passes, the gfx950 correction of MI355X_MICROARCH.md; tools/pmc_traffic.py --merge) for this
+    grid width, slab height (`rows`: the whole grid on one rank, a rank's slab at N > 1 --
+    measured on one GPU as a virtual slab of the same shape), medium and stencil.  PMC counters
+    cannot be read inside the timed run, so this is the committed measurement of the same kernel
+    and workload: (ratio, source), or Nones for a shape without a record."""
     kind = "const" if medium == "const" else medium
-    rec = json.load(open(path)).get(f"n{n}_{kind}_s{stencil}")
-    if not rec:
-        return None, None, None
-    return (int(rec["traffic"]), round(rec["ratio"], 4),
-            f"{TRAFFIC_DB}: FETCH_SIZE x2 + WRITE_SIZE per launch of {rec['kernel'][:60]}..., "
-            f"same grid / medium / stencil")
+    for db, key in ((TRAFFIC_DB, f"n{n}_rows{rows}_{kind}_s{stencil}"),
+                    (TRAFFIC_DB_R03, f"n{n}_{kind}_s{stencil}" if rows == n else None)):
+        path = os.path.join(ROOT, db)
+        rec = json.load(open(path)).get(key) if key and os.path.exists(path) else None
+        if rec:
+            return (round(rec["ratio"], 4),
+                    f"{db}[{key}]: FETCH_SIZE x2 + WRITE_SIZE per launch of "
+                    f"{rec['kernel'][:60]}..., same grid width / slab rows / medium / stencil")
+    return None, None
 
 
 def make_medium(kind, n, cols):
@@ -220,7 +224,7 @@ def cpu_baseline(args, n, omega, h, eta, c_mat):
            "sample": f"{reps} scipy csr_matvec applies of the identical {n}x{n} operator "
                      f"(oracle CSR, {A.nnz} nnz), {t_spmv * 1e3:.1f} ms each; CSR build "
                      f"{t_build:.1f} s untimed"}
-    if not args.no_gmres and args.cpu_gmres_iters > 0:
+    if not args.no_gmres and args.cpu_gmres_iters >= 0:
         if args.precond == "sl" and args.stencil == 9:
             import scipy.sparse.linalg
             Ab = O.build_A9_matrix(args.b, args.C, eta, omega, h, n, c_mat / np.sqrt(1 + 0.5j))
@@ -241,15 +245,46 @@ def cpu_baseline(args, n, omega, h, eta, c_mat):
         else:
             M = None
         f = local_f1(omega, n, 0, n)
+        its = args.cpu_gmres_iters or args.restart
+        # OpenBLAS (scipy's level-1 BLAS in gmres) on the CPUs this process may use
+        ncpu = host_cpu_share()
+        try:
+            from threadpoolctl import threadpool_info, threadpool_limits
+            lim = threadpool_limits(limits=ncpu, user_api="blas")
+            thr = ",".join(f"{d.get('internal_api')}={d.get('num_threads')}"
+                           for d in threadpool_info() if d.get("user_api") == "blas") or str(ncpu)
+        except ImportError:
+            lim, thr = None, os.environ.get("OPENBLAS_NUM_THREADS", "default")
         t0 = time.perf_counter()
-        O.gmres_reference(A, f, M=M, rtol=1e-14, restart=args.restart, maxiter=args.cpu_gmres_iters)
+        O.gmres_reference(A, f, M=M, rtol=1e-14, restart=args.restart, maxiter=its)
         t_g = time.perf_counter() - t0
-        thr = os.environ.get("OPENBLAS_NUM_THREADS", str(os.cpu_count()))
-        out["gmres_iters_per_s"] = round(args.cpu_gmres_iters / t_g, 4)
-        out["gmres_sample"] = (f"{args.cpu_gmres_iters} scipy gmres inner iterations "
-                               f"({args.precond} preconditioner), OpenBLAS threads={thr}")
+        if lim is not None:
+            lim.restore_original_limits()
+        out["gmres_iters_per_s"] = round(its / t_g, 4)
+        cyc = " (one restart cycle)" if its == args.restart else ""
+        out["gmres_sample"] = (f"{its} scipy gmres inner iterations{cyc}, GMRES({args.restart}), "
+                               f"{args.precond} preconditioner, {t_g:.1f} s; OpenBLAS threads="
+                               f"{thr} (the CPUs this process may use: {ncpu})")
+        out["gmres_threads"] = ncpu
     out["host"] = host_description()
     return out
+
+
+def host_cpu_share():
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU quota (a GPU box's
+    share of a larger host: os.cpu_count() shows every CPU of the machine)."""
+    n = len(os.sched_getaffinity(0))
+    try:  # cgroup v2, then v1
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+    except (OSError, ValueError):
+        try:
+            quota = open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read().strip()
+            period = open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read().strip()
+        except OSError:
+            quota, period = "max", "1"
+    if quota not in ("max", "-1"):
+        n = min(n, max(1, int(int(quota) / int(period))))
+    return n
 
 
 def host_description():
@@ -264,7 +299,7 @@ def host_description():
     except OSError:
         pass
     return f"{model}, {os.cpu_count()} logical CPUs (process affinity: " \
-           f"{len(os.sched_getaffinity(0))})"
+           f"{len(os.sched_getaffinity(0))}, CPU share incl. cgroup quota: {host_cpu_share()})"
 
 
 def timed_applies(A, ctx, R, steps, warmup):
@@ -328,21 +363,32 @@ def gmres_bytes(args, its, bpp, N):
     return sum((bpp + pre) * N + 16 * (j + 2) * N + 16 * (j + 3) * N for j in js), fused
 
 
-FUSED_TRAFFIC_DB = "profiles/r04_pmc_fused.json"
+FUSED_TRAFFIC_DB = "profiles/r05_pmc_fused.json"
+# the environment knobs that change the one-pass kernels' traffic: a record applies only to a run
+# with the same values (unset = the build's default)
+FUSED_KNOBS = ("HH_FUSED_ITER", "HH_FUSED_KEEP", "HH_FUSED_ROWS", "HH_BASIS_PAD", "HH_SLK",
+               "HH_SLK_ROWS", "HH_CYCLE_MERGE")
 
 
-def fused_pass_traffic(n, medium, precond, world):
+def fused_knobs():
+    return {k: os.environ[k] for k in FUSED_KNOBS if k in os.environ}
+
+
+def fused_pass_traffic(n, rows, medium, precond, restart):
     """Measured HBM traffic of the one-pass iteration's pass kernels over a restart cycle, as a
     ratio to their algorithmic bytes (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes, separate
-    runs; tools/pmc_fused.py --merge): (ratio, per-K ratios, source), or Nones for a workload
-    without a record."""
+    runs; tools/pmc_fused.py --merge), for this grid width, slab height (a rank's slab at N > 1,
+    recorded as a virtual slab on one GPU), medium, preconditioner and restart, recorded with
+    the same kernel knobs (FUSED_KNOBS) as this run: (ratio, per-K ratios, source), or Nones for
+    a workload without a record."""
     path = os.path.join(ROOT, FUSED_TRAFFIC_DB)
-    if world != 1 or not os.path.exists(path):
+    if not os.path.exists(path):
         return None, None, None
-    rec = json.load(open(path)).get(f"n{n}_{medium}_{precond}")
-    if not rec:
+    key = f"n{n}_rows{rows}_{medium}_{precond}_r{restart}"
+    rec = json.load(open(path)).get(key)
+    if not rec or rec.get("knobs", {}) != fused_knobs():
         return None, None, None
-    return rec["ratio"], rec["per_K"], f"{FUSED_TRAFFIC_DB}: {rec['source']}"
+    return rec["ratio"], rec["per_K"], f"{FUSED_TRAFFIC_DB}[{key}]: {rec['source']}"
 
 
 def gmres_path_bytes(args, its, bpp, N, path):
@@ -542,11 +588,17 @@ def main():
             # one pass over the basis (fused.hip fused_iter_kernel)
             "solve_path": A.last_solve_path(),
         }
-        gmres_block["pass_frac_of_peak"] = round(gmres_block["pass_GBps"] / HBM_PEAK_GBPS, 4)
+        # pass_GBps counts the bytes of the whole n^2 grid (all ranks): the fraction is of the
+        # peak of the `world` devices the ranks run on (one per rank; a one-GPU rehearsal of N
+        # ranks shares one device, so its fraction reads N times low)
+        gmres_block["pass_frac_of_peak"] = round(gmres_block["pass_GBps"] /
+                                                 (HBM_PEAK_GBPS * world), 4)
+        gmres_block["peak_devices"] = world
         if gmres_block["solve_path"] == "one-pass":
             # the passes' measured HBM traffic per algorithmic byte over a cycle (PMC counters
             # cannot run inside the timed solve: the committed record of the same workload)
-            ratio, per_k, src = fused_pass_traffic(n, args.medium, args.precond, world)
+            ratio, per_k, src = fused_pass_traffic(n, j1 - j0, args.medium, args.precond,
+                                                   args.restart)
             gmres_block["pass_traffic_vs_algorithmic"] = ratio
             gmres_block["pass_traffic_source"] = src
 
@@ -570,8 +622,10 @@ def main():
             "ms_per_step": round(tc * 1e3 / args.const_steps, 5),
             "bytes_per_unknown": Ac.bytes_per_point,
             "pct_hbm_peak": round(100.0 * vc / (HBM_PEAK_GBPS * world), 2)}
-        ct, cr, _ = measured_traffic(n, "const", world, args.stencil)
-        const_block.update(traffic=ct, traffic_vs_algorithmic=cr)
+        cr, _ = measured_traffic(n, "const", j1 - j0, args.stencil)
+        const_block.update(traffic=None if cr is None else round(cr * Ac.bytes_per_point *
+                                                                 (j1 - j0) * n),
+                           traffic_vs_algorithmic=cr)
         Ac.close()
         del Ac
 
@@ -632,7 +686,9 @@ def main():
         "device_ms_per_step": round(dev_ms / args.steps, 5),
         "init_s": round(t_init, 3),
     }
-    traffic, traffic_ratio, traffic_src = measured_traffic(n, args.medium, world, args.stencil)
+    # (ratio measured per launch over the slab's rows; traffic = that ratio x this launch's bytes)
+    traffic_ratio, traffic_src = measured_traffic(n, args.medium, j1 - j0, args.stencil)
+    traffic = None if traffic_ratio is None else int(round(traffic_ratio * bpp * interior_rows * n))
     result["roofline"] = {
         "bound": "hbm",
         "achieved": round(achieved_min, 1),

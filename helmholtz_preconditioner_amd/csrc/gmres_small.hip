@@ -724,7 +724,7 @@ hipError_t launch_one(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds
   // cooperatively instead (the runtime's own residency check; ~55 us per launch), for A/B timing.
   static const bool coop = [] {
     const char* e = std::getenv("HH_SMALL_COOP");
-    return e && e[0] == '1';
+    return e && e[0] == '1' && !under_profiler();
   }();
   if (!coop) {
     hipLaunchKernelGGL((gmres_small_cycle_kernel<C, J>), grid, block, lds, s, a);

@@ -1,0 +1,83 @@
+// Device helpers shared by the one-pass GMRES iteration kernels (fused.hip: M none / Jacobi and
+// the two-sweep shifted Laplace at two blocks per CU; fused_slk.hip: the shifted-Laplace pass
+// that keeps its whole basis window on chip at one block per CU).  DESIGN 3g.
+#pragma once
+#include <cstddef>
+
+#include "hh_internal.hpp"
+#include "hh_complex.hpp"
+
+namespace hh {
+namespace fusedk {
+
+constexpr int kT = 256;  // threads per block = columns per strip
+
+struct double2x2 {
+  double2 a, b;
+};
+__device__ __forceinline__ double2x2 make_double2x2(double2 a, double2 b) { return {a, b}; }
+
+// by-value select (a select of lvalues would become a select of addresses)
+__device__ __forceinline__ double2 csel(bool c, double2 a, double2 b) {
+  return make_double2(c ? a.x : b.x, c ? a.y : b.y);
+}
+
+// Global-address-space views: a row pointer made opaque to the optimiser (asm "+s", so neither
+// per-vector address registers nor strength-reduced pointers appear) must stay a GLOBAL pointer,
+// or every load through it becomes a flat load with a 64-bit VGPR address.
+typedef double d2v __attribute__((ext_vector_type(2)));
+using gd2 = const __attribute__((address_space(1))) d2v;
+__device__ __forceinline__ gd2* gptr(const double2* p) { return (gd2*)p; }
+// *(row + byte offset): `row` uniform (scalar registers), `boff` the lane's 32-bit byte offset --
+// the global_load saddr form: one VGPR of address for every vector of a row instead of a 64-bit
+// address per vector
+__device__ __forceinline__ double2 ld_at(gd2* row, unsigned boff) {
+  using gc = const __attribute__((address_space(1))) char;
+  const d2v v = *(gd2*)((gc*)row + boff);
+  return make_double2(v.x, v.y);
+}
+
+// The band of this block: tiles dealt to XCDs in contiguous runs (block b -> XCD b % 8).
+struct Band {
+  bool live;
+  int tx, rb, re;
+};
+__device__ __forceinline__ Band band_of(const FusedArgs& a) {
+  const int tiles_x = (a.n + kT - 1) / kT, T = tiles_x * a.bands;
+  const int per_xcd = (T + 7) / 8;
+  const int tile = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+  Band b;
+  b.live = tile < T;
+  b.tx = b.live ? tile % tiles_x : 0;
+  const int ty = b.live ? tile / tiles_x : 0;
+  const int step = a.row_step > 0 ? a.row_step : a.rows;
+  b.rb = a.row_begin + ty * step;
+  b.re = min(b.rb + a.rows, a.row_end);
+  return b;
+}
+
+// u_K at row r (uniform), column col, given the value formed from the (clamped) row: rows inside
+// [rlo, rhi) are formed from memory; the others are zero (FROW_ZERO) or the neighbour rank's
+// received rows (FROW_HALO; H halo rows per side)
+template <int H>
+__device__ __forceinline__ double2 row_value(const FusedArgs& a, int rlo, int rhi, int r, int col,
+                                             double2 formed) {
+  if (r >= rlo && r < rhi) return formed;
+  if (r < 0)
+    return a.lo_mode == FROW_HALO ? a.halo_lo[(size_t)(r + H) * a.n + col] : make_double2(0.0, 0.0);
+  return a.hi_mode == FROW_HALO ? a.halo_hi[(size_t)(r - a.nl) * a.n + col] : make_double2(0.0, 0.0);
+}
+
+// the update coefficients c_k = raw_k s_k^2 (update_kernel's expression), k < K, into LDS
+template <int K>
+__device__ __forceinline__ void load_coef(const FusedArgs& a, double2* coef) {
+  const int t = threadIdx.x;
+  if (t < K) {
+    const double sk = a.vscale[t];
+    const double2 hk = cscale(make_double2(a.raw[2 * t], a.raw[2 * t + 1]), sk);
+    coef[t] = cscale(hk, sk);
+  }
+}
+
+}  // namespace fusedk
+}  // namespace hh

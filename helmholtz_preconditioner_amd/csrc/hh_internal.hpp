@@ -244,6 +244,12 @@ struct FusedArgs {
   double* partials;        // this launch's partial rows
   const int* stop;
 };
+// Running under rocprofv3 (its preloaded rocprofiler-sdk: ROCPROFILER_LIBRARY_CTOR /
+// ROCPROF_OUTPUT_PATH in the environment, or a rocprofiler library in LD_PRELOAD)?  ROCm 7.2:
+// a process that made any cooperative launch dies with SIGSEGV inside exit() once
+// rocprofiler-sdk has finalised (tools/exit_probe.py), so the grid-wide sweeps and
+// the small-grid cycle then launch plainly (their waits are bounded either way); logged once.
+bool under_profiler();
 constexpr int kFusedMaxK = 20;  // K <= this (restart <= kFusedMaxK + 1)
 // basis vectors whose projection re-read is served from the pass's own LDS copy (HH_FUSED_KEEP:
 // 0 = every re-read from the memory system, for A/B)
@@ -251,6 +257,11 @@ constexpr int kFusedKeepDefault = 17;
 int fused_iter_rows(int n, int rows);  // band height for a slab of `rows` rows
 int fused_iter_blocks(int n, int bands);
 void launch_fused_iter(int K, const FusedArgs& a, int blocks, hipStream_t stream);
+// the shifted-Laplace pass with the whole basis window on chip (fused_slk.hip; one block per
+// CU): used for K >= HH_SLK (default 1; 0 = never), with its own band height
+bool fused_slk_use(int K);
+int fused_slk_rows(int n, int rows);
+void launch_fused_slk(int K, const FusedArgs& a, int blocks, hipStream_t stream);
 // u_K on rows [r0, r0 + c0) and [r1, r1 + c1) of a.V / a.win (rank-local), written to a.uout:
 // the rows a neighbouring rank's pass reads as its halo (fused_iter_kernel's arithmetic)
 void launch_fused_edge(int K, const FusedArgs& a, int r0, int c0, int r1, int c1,

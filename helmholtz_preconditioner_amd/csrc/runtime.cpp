@@ -63,6 +63,20 @@ static cd s2(double x, double C, double eta, cd om) {
 }
 static double2 d2(cd z) { return make_double2(z.real(), z.imag()); }
 
+bool under_profiler() {
+  static const bool on = [] {
+    const char* pre = std::getenv("LD_PRELOAD");
+    const bool p = std::getenv("ROCPROFILER_LIBRARY_CTOR") || std::getenv("ROCPROF_OUTPUT_PATH") ||
+                   (pre && std::strstr(pre, "rocprofiler"));
+    if (p)
+      std::fprintf(stderr, "[helmholtz_amd] rocprofv3 detected: grid-wide sweeps and the "
+                           "small-grid cycle use plain launches (no cooperative launch: ROCm's "
+                           "exit-time queue teardown after rocprofiler-sdk finalised, DESIGN 3b)\n");
+    return p;
+  }();
+  return on;
+}
+
 }  // namespace hh
 
 using namespace hh;
@@ -788,7 +802,8 @@ int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double*
   double2* uout = op->V + (size_t)K * ldv;
   const int width = 2 * (K + 1) + 2;
   const int rows_rank = op->je - op->jb;
-  const int R = fused_iter_rows(n, rows_rank);
+  const bool slk = sl && fused_slk_use(K);
+  const int R = slk ? fused_slk_rows(n, rows_rank) : fused_iter_rows(n, rows_rank);
   FusedArgs base{};
   base.ldv = ldv;
   base.raw = raw;
@@ -828,7 +843,10 @@ int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double*
     const int blocks = fused_iter_blocks(n, a.bands);
     REQUIRE((size_t)(nparts + blocks) * width <= op->partials_cap,
             "partials workspace too small for the one-pass iteration (%d blocks)", nparts + blocks);
-    launch_fused_iter(K, a, blocks, st);
+    if (slk)
+      launch_fused_slk(K, a, blocks, st);
+    else
+      launch_fused_iter(K, a, blocks, st);
     nparts += blocks;
   };
   hipEvent_t t_halo = nullptr;

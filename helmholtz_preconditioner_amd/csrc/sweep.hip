@@ -540,10 +540,19 @@ constexpr size_t kPartLdsBudget = 160 * 1024;
 // wait until at most N of this wave's vector-memory operations are outstanding (vmcnt only;
 // they complete in issue order).  After an LDS DMA and N later loads: waits for the DMA alone,
 // where the compiler's own wait before the next LDS access would take every load with it.
+// The count N is hand-derived from the loads issued after the DMA (the sfor ring); it is right
+// only while the compiler emits exactly those after it.  tools/check_sweep_waitcnt.py checks the
+// built ISA (every LDS read after an LDS DMA is covered by a wait that retires the DMA);
+// -DHH_SWEEP_WAIT_ALL builds every such wait as vmcnt(0) (make waitall) for A/B runs of the
+// linearity / determinism tests.
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+#ifdef HH_SWEEP_WAIT_ALL
+  __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));
+#else
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+#endif
 }
 
 // base[byte offset]: a scalar base plus a 32-bit lane offset in bytes is the form the
@@ -1330,7 +1339,7 @@ size_t sweep_part_granules(int G) { return (size_t)2 * 2 * G * kSweepGranStride;
 bool sweep_coop_launch() {
   static const bool coop = [] {
     const char* e = std::getenv("HH_SWEEP_COOP");
-    return !(e && e[0] == '0');
+    return !(e && e[0] == '0') && !under_profiler();
   }();
   return coop;
 }

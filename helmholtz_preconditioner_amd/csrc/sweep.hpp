@@ -60,8 +60,8 @@ __host__ __device__ constexpr int pidx(int j, int c) {
 // at launch; HH_SWEEP_COOP=0 launches them as plain kernels, whose grid-wide waits are bounded
 // anyway (a timeout word the host checks).  (ROCm 7.2 + rocprofv3: a process that made ANY
 // cooperative launch dies with SIGSEGV inside exit() -- libamdhip64's exit handler tearing down
-// an HSA queue after rocprofiler-sdk finalised, tools/exit_probe.py; profiling runs
-// of the sweep set HH_SWEEP_COOP=0.)
+// an HSA queue after rocprofiler-sdk finalised, tools/exit_probe.py, DESIGN 3b: under
+// rocprofv3 the launches are plain automatically, hh_internal.hpp under_profiler.)
 bool sweep_coop_launch();
 int sweep_block(int b);
 size_t sweep_scratch_per_wave(int n);  // padded block size B (4, 8, 12, 16) or 0 if b > 16

@@ -1,4 +1,4 @@
-"""CPU tier, N > 1: the row-slab decomposition over torch.distributed gloo (world 2, 3).
+"""CPU tier, N > 1: the row-slab decomposition over torch.distributed gloo (world 2, 3, 4, 8).
 
 * slab ownership (dist.slab_bounds == the C runtime's formula) tiles [0, n);
 * the file rendezvous hands rank 0's 128-byte id to every rank;
@@ -88,7 +88,9 @@ def _gloo_worker(rank, world, port, case, out, lagged=False):
                                                ("gmres_n128_jacobi.npz", 3, True),
                                                ("gmres_n64_c1_none.npz", 2, "onepass"),
                                                ("gmres_n128_jacobi.npz", 3, "onepass"),
-                                               ("gmres_n128_none.npz", 4, "onepass")])
+                                               ("gmres_n128_none.npz", 4, "onepass"),
+                                               ("gmres_n128_none.npz", 8, "onepass"),
+                                               ("gmres_n128_jacobi.npz", 8, True)])
 def test_distributed_gmres_mirror_matches_reference(case, world, lagged):
     """lagged: the one-allreduce iteration (the runtime's lagged path across ranks) -- the
     golden histories to 1e-9, with ONE allreduce per inner iteration inside the restart cycles

@@ -50,7 +50,8 @@ def ctx():
     c.close()
 
 
-def _solve_pair(ctx, n, c_mat, wave_num, precond, K):
+def _solve_pair(ctx, n, c_mat, wave_num, precond, K, path=None):
+    """the device solve (asserting the cycle form it ran, `path`) and the oracle's scipy solve"""
     om, h, eta = H.problem_params(n, B, wave_num, ALPHA)
     f = H.init_f1_mat(.5, .125, om, n).ravel()
     A = H.build_A_matrix(B, C, eta, om, h, n, c_mat, context=ctx)
@@ -58,6 +59,8 @@ def _solve_pair(ctx, n, c_mat, wave_num, precond, K):
                                                                   damping=0.7)
     x, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=K, M=M,
                             callback=lambda r: None, callback_type="legacy", return_history=True)
+    if path is not None:  # (the path the parity is credited to: the bench's default path)
+        assert A.last_solve_path() == path, A.last_solve_path()
     A.close()
     R = O.build_A_matrix(B, C, eta, om, h, n, c_mat)
     Mr = (O.jacobi_preconditioner(R) if precond == "jacobi" else
@@ -81,12 +84,13 @@ def _assert_parity(dev, ref, K):
 
 def test_config2_jacobi_gmres_1024(ctx):
     n, K = 1024, 100
-    _assert_parity(*_solve_pair(ctx, n, H.constant_c_mat(n), 64.0, "jacobi", K), K)
+    _assert_parity(*_solve_pair(ctx, n, H.constant_c_mat(n), 64.0, "jacobi", K, "one-pass"), K)
 
 
 def test_config3_shifted_laplace_gmres_4096(ctx):
     n, K = 4096, 20
-    _assert_parity(*_solve_pair(ctx, n, H.marmousi_like_c_mat(n), 100.0, "sl", K), K)
+    _assert_parity(*_solve_pair(ctx, n, H.marmousi_like_c_mat(n), 100.0, "sl", K, "one-pass"),
+                   K)
 
 
 # --------------------------------------------------------------------- config 4, 2 / 4 ranks

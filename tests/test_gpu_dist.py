@@ -134,15 +134,17 @@ def test_uneven_slabs_default_limits(tmp_path):
 
 
 @pytest.mark.parametrize("world,slabs,transport", [(2, 1, "shm"), (3, 2, "shm"), (4, 1, "shm"),
+                                                  (8, 1, "shm"), (8, 2, "shm"),
                                                   (2, 1, "rccl"), (3, 1, "rccl"),
-                                                  (4, 2, "rccl")])
+                                                  (4, 2, "rccl"), (8, 1, "rccl")])
 def test_fused_pass_ranks_match_single_domain(tmp_path, world, slabs, transport):
     """The one-pass iteration across ranks (runtime.cpp run_fused: u_K's edge rows formed
     first, exchanged on the halo stream while the interior rows run, the boundary rows behind
     the exchange; one allreduce per pass) for none / Jacobi / the two-sweep shifted Laplace
-    (two edge rows), over both transports, with and without virtual slabs inside the ranks:
-    every rank reports the one-pass path, and matches the single domain's one-pass solve to
-    1e-8."""
+    (two edge rows), over both transports, with and without virtual slabs inside the ranks, up
+    to the node's 8 ranks (n = 150: 18-19 rows a rank, 9-10 a virtual slab -- the shifted
+    Laplace's two edge rows and the bands' four halo rows all inside a neighbour): every rank
+    reports the one-pass path, and matches the single domain's one-pass solve to 1e-8."""
     n = 150
     parts = _run_workers(tmp_path, world, n, ["--slabs", str(slabs), "--krylov", "fused"],
                          transport=transport, timeout=240)

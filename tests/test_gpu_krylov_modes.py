@@ -248,6 +248,25 @@ def test_fused_pass_lds_kept_basis_is_bit_identical(ctx, n, kind, monkeypatch):
         assert np.array_equal(x, out[0][0])
 
 
+def test_fused_keep_knob_refuses_unbuilt_counts(ctx, monkeypatch):
+    """HH_FUSED_KEEP selects between the two built forms (0: no LDS copy, 17: the default);
+    any other count (round 3's A/B values 4, 8) is refused with an error instead of silently
+    running 17"""
+    n = 300
+    om, h, eta = O.problem_params(n, 12, n / 40.0, 2.0)
+    A = H.build_A_matrix(12, 81.0, eta, om, h, n, medium("c1", n), context=ctx)
+    A.krylov_mode("fused")
+    A.small_cycle("off")
+    f = O.init_f1_mat(.5, .125, om, n).ravel()
+    monkeypatch.setenv("HH_FUSED_KEEP", "4")
+    with pytest.raises(H.HHError, match="HH_FUSED_KEEP"):
+        H.gmres(A, f, rtol=1e-12, restart=20, maxiter=3, M="jacobi")
+    monkeypatch.setenv("HH_FUSED_KEEP", "0")
+    H.gmres(A, f, rtol=1e-12, restart=20, maxiter=3, M="jacobi")
+    assert A.last_solve_path() == "one-pass"
+    A.krylov_mode("auto")
+
+
 @pytest.mark.parametrize("n,slabs", [(150, 2), (300, 3), (613, 4)])
 @pytest.mark.parametrize("precond", [None, "jacobi", "sl"])
 def test_fused_pass_virtual_slabs_match_single_slab(ctx, n, slabs, precond):
@@ -277,7 +296,12 @@ def test_fused_pass_virtual_slabs_match_single_slab(ctx, n, slabs, precond):
     assert i1 == i2 and len(h1) == len(h2)
     # the first iterations to rounding (the reordered sums' last bits); later iterations
     # amplify that rounding (DESIGN 6 'Where history parity is defined at all'): the whole
-    # history and the field within the parity contract
+    # history and the field within the parity contract.  Measured (tools/slab_drift.py,
+    # profiles/r05/r05_slab_drift_cpu_613_jacobi.log): the numpy mirror of this very solve
+    # (tests/dist_mirror.py gmres_dist_onepass), whose slab split changes NOTHING but the inner
+    # products' summation order, drifts 1.0e-15 by iteration 5 and 1.5e-8 by iteration 10 at
+    # n = 613 / 4 slabs / Jacobi (a stagnating run: presid 4e-7 throughout), and scipy itself
+    # 6.9e-4 on f vs f (1 + 1e-15) -- the device's 1.35e-8 (round 4) is that amplification
     assert np.max(np.abs(h1[:5] - h2[:5]) / h1[:5]) < 1e-10
     assert np.max(np.abs(h1 - h2) / h1) < TOL
     assert relerr(x2, x1) < TOL
@@ -324,3 +348,48 @@ def test_fused_cycle_end_merge_matches_solve_and_xupdate(tmp_path, n, kind, rest
     assert np.array_equal(a["hist"][:c], b["hist"][:c])
     assert np.max(np.abs(a["hist"] - b["hist"]) / b["hist"]) < 1e-9
     assert relerr(a["x"], b["x"]) < 1e-11
+
+
+_SLK_CHILD = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import helmholtz_preconditioner_amd as H
+n, kind, slabs, restart, K, out = (int(sys.argv[2]), sys.argv[3], int(sys.argv[4]),
+                                    int(sys.argv[5]), int(sys.argv[6]), sys.argv[7])
+om, h, eta = H.problem_params(n, 12, n / 40.0, 2.0)
+cm = H.marmousi_like_c_mat(n) if kind == "marmousi" else H.init_c1_mat(.5, .5, n)
+ctx = H.Context(device=0, virtual_slabs=slabs)
+A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, context=ctx)
+A.krylov_mode("fused")
+A.small_cycle("off")
+M = H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7)
+f = H.init_f1_mat(.5, .125, om, n).ravel()
+x, info, hist = H.gmres(A, f, rtol=1e-12, restart=restart, maxiter=K, M=M,
+                        callback=lambda r: None, callback_type="legacy", return_history=True)
+assert A.last_solve_path() == "one-pass"
+np.savez(out, x=x, info=info, hist=hist)
+'''
+
+
+@pytest.mark.parametrize("n,kind,slabs,rows", [(300, "c1", 1, 16), (1100, "marmousi", 1, 32),
+                                               (613, "marmousi", 3, 16), (257, "c1", 2, 8)])
+def test_fused_sl_keep_kernel_bit_identical(tmp_path, n, kind, slabs, rows):
+    """fused_slk.hip (the shifted-Laplace pass with its whole basis window on chip: a three-row
+    LDS ring for 11 vectors, a four-slot register ring for the rest, one block per CU) against
+    fused.hip fused_sl_iter_kernel (5 vectors kept, the rest re-read) on the same bands
+    (HH_FUSED_ROWS = HH_SLK_ROWS): the same arithmetic in the same order, so histories and
+    fields are bit-identical -- restart 21, 25 iterations (K = 1 .. 20: both rings, and a second
+    cycle), ragged strips and bands, virtual slabs (rows formed in place across slabs)"""
+    import subprocess
+    import sys
+    res = []
+    for slk in ("0", "1"):
+        out = tmp_path / f"slk{slk}.npz"
+        env = dict(os.environ, HH_SLK=slk, HH_FUSED_ROWS=str(rows), HH_SLK_ROWS=str(rows))
+        subprocess.run([sys.executable, "-c", _SLK_CHILD, ROOT, str(n), kind, str(slabs), "21",
+                        "25", str(out)], env=env, check=True, timeout=240)
+        res.append(np.load(out))
+    a, b = res
+    assert int(a["info"]) == int(b["info"]) and len(a["hist"]) == len(b["hist"]) == 25
+    assert np.array_equal(a["hist"], b["hist"])
+    assert np.array_equal(a["x"], b["x"])

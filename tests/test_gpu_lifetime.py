@@ -84,15 +84,15 @@ def test_exit_with_live_handles(tmp_path, profiled):
     operators, then contexts, before the HIP runtime's exit handlers (and a profiler's
     finalisation) run.  Also under rocprofv3 --kernel-trace, where round 3 saw a SIGSEGV inside
     exit() (profiles/r03i): that one is ROCm's own teardown after any cooperative launch
-    (tools/exit_probe.py), so the profiled run takes the grid-wide sweep as a plain
-    launch (HH_SWEEP_COOP=0)."""
+    (tools/exit_probe.py): the library detects the profiler and takes the grid-wide
+    sweep as a plain launch by itself (no environment override), and says so on stderr."""
     import shutil
     import subprocess
     import sys
     cmd = [sys.executable, "-c", _LIVE_AT_EXIT, ROOT]
     env = dict(os.environ, TMPDIR=str(tmp_path))
     if profiled:
-        env["HH_SWEEP_COOP"] = "0"
+        env.pop("HH_SWEEP_COOP", None)
         rp = shutil.which("rocprofv3")
         if rp is None:
             pytest.skip("rocprofv3 not on PATH")
@@ -101,3 +101,4 @@ def test_exit_with_live_handles(tmp_path, profiled):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "exiting with live handles" in r.stdout
+    assert ("rocprofv3 detected" in r.stderr) == profiled, r.stderr[-3000:]

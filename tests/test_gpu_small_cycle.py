@@ -245,13 +245,17 @@ print("ok")
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
 
-def test_small_cycle_refusal_after_cycles_hands_over():
+@pytest.mark.parametrize("precond", [None, "jacobi"])
+@pytest.mark.parametrize("cbtype", ["legacy", "pr_norm"])
+def test_small_cycle_refusal_after_cycles_hands_over(precond, cbtype):
     """A refusal after cycles have run (simulated: HH_SMALL_REFUSE_AT=2 makes the gate refuse the
     solve's second launch, after the first batch of 16 restart cycles) hands the solve to the
-    regular cycle at that restart boundary -- x, V[0] = M r, |r|^2, |M r|^2 and the device's
-    ptol state as the last completed cycle left them -- instead of failing: same info and
-    history (1e-9) as the uninterrupted small-cycle solve.  Child processes: the knob is read
-    once per process."""
+    regular cycle at that restart boundary -- x, V[0] = M r, |r|^2, |M r|^2 (Jacobi: its own
+    report slot) and the device's ptol state as the last completed cycle left them -- instead
+    of failing: same info and history (1e-9) as the uninterrupted small-cycle solve, for M none
+    and Jacobi, in legacy mode (maxiter caps inner iterations) and in the restart-loop mode of
+    pr_norm (maxiter caps cycles; ptol and its growth factor read back from the device).  Child
+    processes: the knob is read once per process."""
     import subprocess
     import sys
     code = r'''
@@ -266,8 +270,10 @@ om, h, eta = O.problem_params(n, b, wn, 2.0)
 A = H.build_A_matrix(b, C, eta, om, h, n, medium("c1", n))
 f = O.init_f1_mat(.5, .125, om, n).ravel()
 A.small_cycle("on")
-x, info, hist = H.gmres(A, f, rtol=1e-3, restart=2, maxiter=40, callback=lambda r: None,
-                        callback_type="legacy", return_history=True)
+M = None if sys.argv[2] == "none" else sys.argv[2]
+cb = sys.argv[3]
+x, info, hist = H.gmres(A, f, rtol=1e-10, restart=2, maxiter=40 if cb == "legacy" else 20, M=M,
+                        callback=lambda r: None, callback_type=cb, return_history=True)
 np.savez(sys.argv[1], x=x, info=info, hist=hist, path=A.last_solve_path())
 '''
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -276,13 +282,13 @@ np.savez(sys.argv[1], x=x, info=info, hist=hist, path=A.last_solve_path())
         for at in ("0", "2"):
             out = os.path.join(td, f"r{at}.npz")
             env = dict(os.environ, HH_SMALL_REFUSE_AT=at)
-            r = subprocess.run([sys.executable, "-c", code, out], cwd=root, env=env,
-                               capture_output=True, text=True, timeout=240)
+            r = subprocess.run([sys.executable, "-c", code, out, precond or "none", cbtype],
+                               cwd=root, env=env, capture_output=True, text=True, timeout=240)
             assert r.returncode == 0, r.stdout + r.stderr
             res.append(np.load(out))
     a, b = res
     assert str(a["path"]) == "small-cycle" and str(b["path"]) == "small-cycle refused -> regular"
-    assert int(a["info"]) == int(b["info"]) and len(a["hist"]) == len(b["hist"]) == 40
+    assert int(a["info"]) == int(b["info"]) and len(a["hist"]) == len(b["hist"]) >= 40
     assert np.array_equal(a["hist"][:32], b["hist"][:32])  # (the 16 cycles before the refusal)
     assert np.all(np.abs(a["hist"] - b["hist"]) <= 1e-9 * np.abs(a["hist"]) + 1e-15)
     assert np.linalg.norm(a["x"] - b["x"]) <= 1e-9 * np.linalg.norm(a["x"])

@@ -11,11 +11,12 @@ N = n * n
 rows = []
 with open(path) as fh:
     for r in csv.DictReader(fh):
-        m = re.search(r"fused(_sl)?_iter_kernel<(\d+)", r["Name"])
+        m = re.search(r"fused_(sl_iter|slk|iter)_kernel<(\d+)", r["Name"])
         if m:
             K = int(m.group(2))
             ns = float(r["AverageNs"])
             gbs = (16 * (K + 3) + ic) * N / ns
-            rows.append((K, m.group(1) or "", int(r["Calls"]), ns / 1e3, gbs))
+            rows.append((K, "" if m.group(1) == "iter" else "_" + m.group(1), int(r["Calls"]),
+                         ns / 1e3, gbs))
 for K, sl, calls, us, gbs in sorted(rows):
-    print(f"fused{sl}_iter_kernel<{K:2d}>  calls {calls:5d}  avg {us:9.1f} us  {gbs / 1e3:5.2f} TB/s")
+    print(f"fused{sl}<{K:2d}>  calls {calls:5d}  avg {us:9.1f} us  {gbs / 1e3:5.2f} TB/s")
