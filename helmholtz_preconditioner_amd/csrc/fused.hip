@@ -169,8 +169,17 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
   for (int k = 0; k <= K; ++k) acc[k] = z;
   double nw = 0.0, nu = 0.0;
   if (bd.live) {
-    double2 uS = unew(rb - 1, (unsigned)ic);
-    double2 uC = unew(rb, (unsigned)ic);
+    // direction: odd bands march downwards (a.alt), so that neighbouring bands, which start
+    // together, reach their shared boundary rows at the same time -- the halo rows a band
+    // re-forms from the basis are then read while the owning band reads them (L2 hits), where
+    // bands all marching up read them a band's length apart (round 4: 1.13-1.27x the pass's
+    // bytes at 1024^2, 8-row bands).  Per point the same arithmetic; only the order in which a
+    // band's rows add into its partial row changes.
+    const bool dn = a.alt && (bd.ty & 1);
+    const int d = dn ? -1 : 1;
+    const int r_first = dn ? re - 1 : rb;
+    double2 uB = unew(r_first - d, (unsigned)ic);  // the row behind the march
+    double2 uC = unew(r_first, (unsigned)ic);
     if constexpr (KL > 0) {
 #pragma unroll
       for (int q = 0; q < KL; ++q) vkeep[q][t] = hold[q];
@@ -178,12 +187,13 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
 #pragma unroll
     for (int q = 0; q < KR; ++q) rcur[q] = rnext[q];
     int buf = 0;
-    for (int r0 = rb; r0 < re; ++r0) {
-      int r = r0;
+    for (int s0 = 0; s0 < re - rb; ++s0) {
+      int r = r_first + d * s0;
       asm volatile("" : "+s"(r), "+s"(kz));
       EdgeLd el{z, z};
       if (ew || ee) el = unew1_issue(r, ie);  // (wave-uniform: the two edge waves only)
-      const double2 uN = unew(r + 1, (unsigned)ic);
+      const double2 uA = unew(r + d, (unsigned)ic);  // the row ahead
+      const double2 uS = csel(dn, uA, uB), uN = csel(dn, uB, uA);
       double2 ue = z;
       if (ew || ee) ue = unew1_finish(r, ie, el);
       urow[buf][1 + t] = csel(act, uC, z);
@@ -247,14 +257,14 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
         __builtin_amdgcn_sched_barrier(0);
       }
       acc[K] = cfma_conj(uo, w, acc[K]);
-      if constexpr (KL > 0) {  // (row r + 1's basis for the next step's projections)
+      if constexpr (KL > 0) {  // (row r + d's basis for the next step's projections)
 #pragma unroll
         for (int q2 = 0; q2 < KL; ++q2) vkeep[q2][t] = hold[q2];
       }
 #pragma unroll
       for (int q2 = 0; q2 < KR; ++q2) rcur[q2] = rnext[q2];
-      uS = uC;
-      uC = uN;
+      uB = uC;
+      uC = uA;
       buf ^= 1;
     }
   }
@@ -782,6 +792,16 @@ using FusedTable = FTable<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16,
 static_assert(kFusedMaxK == 20, "table covers 1..kFusedMaxK");
 
 }  // namespace
+
+// HH_FUSED_ALT=0 turns the alternating march off (A/B); read once
+constexpr bool kFusedAltDefault = false;
+bool fused_alt_dir() {
+  static const bool on = [] {
+    const char* e = std::getenv("HH_FUSED_ALT");
+    return e ? e[0] != '0' : kFusedAltDefault;
+  }();
+  return on;
+}
 
 // Band height: 8 rows at 1024^2, 32 at 4096^2 (profiles/r03t/r03s_ab_rows*), 64 from 8192^2;
 // HH_FUSED_ROWS overrides.  The partial rows (one per block) stay within kMaxStreamBlocks.

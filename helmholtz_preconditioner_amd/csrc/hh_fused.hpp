@@ -40,7 +40,7 @@ __device__ __forceinline__ double2 ld_at(gd2* row, unsigned boff) {
 // The band of this block: tiles dealt to XCDs in contiguous runs (block b -> XCD b % 8).
 struct Band {
   bool live;
-  int tx, rb, re;
+  int tx, ty, rb, re;  // strip, band index, rows [rb, re)
 };
 __device__ __forceinline__ Band band_of(const FusedArgs& a) {
   const int tiles_x = (a.n + kT - 1) / kT, T = tiles_x * a.bands;
@@ -51,6 +51,7 @@ __device__ __forceinline__ Band band_of(const FusedArgs& a) {
   b.tx = b.live ? tile % tiles_x : 0;
   const int ty = b.live ? tile / tiles_x : 0;
   const int step = a.row_step > 0 ? a.row_step : a.rows;
+  b.ty = ty;
   b.rb = a.row_begin + ty * step;
   b.re = min(b.rb + a.rows, a.row_end);
   return b;

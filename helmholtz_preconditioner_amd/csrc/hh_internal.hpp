@@ -243,6 +243,7 @@ struct FusedArgs {
   double damping;          // SL: damped-Jacobi weight
   double* partials;        // this launch's partial rows
   const int* stop;
+  int alt;                 // fused_iter_kernel: odd bands march downwards (fused_alt_dir)
 };
 // Running under rocprofv3 (its preloaded rocprofiler-sdk: ROCPROFILER_LIBRARY_CTOR /
 // ROCPROF_OUTPUT_PATH in the environment, or a rocprofiler library in LD_PRELOAD)?  ROCm 7.2:
@@ -260,6 +261,9 @@ void launch_fused_iter(int K, const FusedArgs& a, int blocks, hipStream_t stream
 // the shifted-Laplace pass with the whole basis window on chip (fused_slk.hip; one block per
 // CU): used for K >= HH_SLK (default 1; 0 = never), with its own band height
 bool fused_slk_use(int K);
+// fused_iter_kernel's odd bands march downwards (HH_FUSED_ALT, read once), so the halo rows a
+// band re-forms are read while their owners read them too (fused.hip)
+bool fused_alt_dir();
 int fused_slk_rows(int n, int rows);
 void launch_fused_slk(int K, const FusedArgs& a, int blocks, hipStream_t stream);
 // u_K on rows [r0, r0 + c0) and [r1, r1 + c1) of a.V / a.win (rank-local), written to a.uout:

@@ -817,6 +817,7 @@ int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double*
   base.mshift = op->mshift;
   base.damping = op->damping;
   base.stop = op->stop_flag;
+  base.alt = (!sl && fused_alt_dir()) ? 1 : 0;
   int nparts = 0;
   auto launch = [&](int si, int r0, int r1, int rows, int step, hipStream_t st) {
     if (r1 <= r0) return;

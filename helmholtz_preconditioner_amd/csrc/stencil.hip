@@ -39,6 +39,8 @@
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
 #include "hh_stencil9.hpp"
+#include "hh_error.hpp"
+#include <algorithm>
 
 #include <type_traits>
 
@@ -457,14 +459,13 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
 // flat stream's access pattern); the two halo rows a tile shares with each vertical
 // neighbour come mostly from L2 / the Infinity Cache.  Same per-point arithmetic as
 // stencil_tile: bit-identical results.
+// One tile t of tile_kernel (and of the persistent tile_persist_kernel, which loops over tiles)
 template <int EPI, bool CONSTC, int R, bool NT, bool NTU>
-__global__ __launch_bounds__(kStencilThreads) void tile_kernel(const StencilArgs a) {
+__device__ __forceinline__ void tile_do(const StencilArgs& a, const int t) {
   static_assert(EPI == EPI_AX || EPI == EPI_JAC, "tile shape: plain and Jacobi-fused apply");
-  if (a.stop && *a.stop) return;  // queued GMRES cycle already stopped
   constexpr int TPB = kStencilThreads;
   const int n = a.n;
   const int tiles_x = a.tiles_x;
-  const int t = blockIdx.x;
   const int tx = t % tiles_x, ty = t / tiles_x;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int i = tx * TPB + tid;
@@ -526,6 +527,23 @@ __global__ __launch_bounds__(kStencilThreads) void tile_kernel(const StencilArgs
       else store2(a.out0 + (size_t)r * n + ic_, cscale(cdiv(Au, D), sin), NT);
     }
   }
+}
+
+template <int EPI, bool CONSTC, int R, bool NT, bool NTU>
+__global__ __launch_bounds__(kStencilThreads) void tile_kernel(const StencilArgs a) {
+  if (a.stop && *a.stop) return;  // queued GMRES cycle already stopped
+  tile_do<EPI, CONSTC, R, NT, NTU>(a, blockIdx.x);
+}
+
+// The same tiles from a persistent grid (a.grid_blocks blocks, as many as are resident at
+// once): block b takes tiles b, b + G, b + 2 G, ... -- the resident blocks still sweep one
+// contiguous window of tiles, without the dispatch of tiles_x * tiles_y blocks and with a
+// tail of at most one tile per block (tuning variants kTilePersist + R).  Bit-identical.
+template <int EPI, bool CONSTC, int R, bool NT, bool NTU>
+__global__ __launch_bounds__(kStencilThreads) void tile_persist_kernel(const StencilArgs a,
+                                                                       int tiles) {
+  if (a.stop && *a.stop) return;
+  for (int t = blockIdx.x; t < tiles; t += gridDim.x) tile_do<EPI, CONSTC, R, NT, NTU>(a, t);
 }
 
 // The tile shape for the 9-point operator (stencil_tile's separable S9 form, same association,
@@ -696,9 +714,12 @@ constexpr int kLongRow = 4608;
 // R rows per tile.
 constexpr int kTileVariant = 96;
 constexpr int kTileDefault = kTileVariant + 4;  // 4-row tiles, cached u, NT 1/c^2 and stores
+// + 64: the same tiles from a persistent grid (tile_persist_kernel; cached u, NT 1/c^2 and
+// stores; R rows per tile): kTilePersist + R
+[[maybe_unused]] constexpr int kTilePersist = kTileVariant + 64;
 constexpr bool tile_variant_known(int v) {
   const int w = v - kTileVariant, R = w % 16;
-  return w >= 0 && w < 64 && R >= 2 && R <= 8 && R != 7;
+  return w >= 0 && (w < 64 || w < 80) && R >= 2 && R <= 8 && R != 7;
 }
 // The 9-point operator instantiates the four LDS-exchange shapes below and takes the 5-point
 // defaults: in its separable form (101-109 VGPRs, 4 waves per SIMD) it runs at the 5-point
@@ -832,7 +853,7 @@ int stencil_grid_blocks(int n, int rows, int rows_per_block, int row_step) {
 int stencil_default_variant() { return kDefaultVariant; }
 bool stencil_variant_valid(int v) {
   return (v >= 0 && v <= 27) || (v >= 30 && v <= 33) || (v >= 42 && v <= 45) || sl2_variant(v) ||
-         (v >= kTileVariant && v < kTileVariant + 64 && tile_variant_known(v));
+         (v >= kTileVariant && v < kTileVariant + 80 && tile_variant_known(v));
 }
 
 void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_out[1],
@@ -855,16 +876,37 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_
     v = stencil_resolve_variant(epi, kVariantInSolve, a.n);
   if (v >= kTileVariant) {  // non-marching tiles (plain / Jacobi 5-point apply, tile_kernel)
     const int w = v - kTileVariant, R = w % 16;
-    const bool ntu = (w / 16) % 2 == 1, nt = w < 32;
+    const bool ntu = (w / 16) % 2 == 1 && w < 64, nt = w < 32 || w >= 64;
     // (padding tiles_x to a multiple of 8, which would put vertically adjacent tiles on one
     // XCD, measured 3-7 % SLOWER at n = 5792 and 11584: profiles/r01y_tune_tile_pad.log)
     a.tiles_x = (a.n + kStencilThreads - 1) / kStencilThreads;
     const int tiles = a.tiles_x * ((rows + R - 1) / R);
+    const bool pers = w >= 64 && !a.tab_r2x;  // (5-point only)
     nblocks_out[0] = 0;
     auto go = [&](auto ke, auto kr) {
       constexpr int E = decltype(ke)::value;
       constexpr int RR = decltype(kr)::value;
       const dim3 g(tiles), b(kStencilThreads);
+      if (pers) {  // persistent grid: every resident slot once
+        static int slots = 0;
+        if (slots == 0) {
+          int dev = 0, cus = 0, per = 0;
+          HIPC(hipGetDevice(&dev));
+          HIPC(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+          HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &per, reinterpret_cast<const void*>(&tile_persist_kernel<E, false, RR, true, false>),
+              kStencilThreads, 0));
+          slots = std::max(1, cus * per);
+        }
+        const dim3 gp(std::min(tiles, slots));
+        if (const_c)
+          hipLaunchKernelGGL((tile_persist_kernel<E, true, RR, true, false>), gp, b, 0, stream, a,
+                             tiles);
+        else
+          hipLaunchKernelGGL((tile_persist_kernel<E, false, RR, true, false>), gp, b, 0, stream,
+                             a, tiles);
+        return;
+      }
       if (a.tab_r2x) {  // 9-point operator
         if (const_c) {
           if (!nt) hipLaunchKernelGGL((tile9_kernel<E, true, RR, false, false>), g, b, 0, stream, a);

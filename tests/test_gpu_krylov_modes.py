@@ -393,3 +393,44 @@ def test_fused_sl_keep_kernel_bit_identical(tmp_path, n, kind, slabs, rows):
     assert int(a["info"]) == int(b["info"]) and len(a["hist"]) == len(b["hist"]) == 25
     assert np.array_equal(a["hist"], b["hist"])
     assert np.array_equal(a["x"], b["x"])
+
+
+_ALT_CHILD = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import helmholtz_preconditioner_amd as H
+n, kind, pc, out = int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
+om, h, eta = H.problem_params(n, 12, n / 40.0, 2.0)
+cm = H.marmousi_like_c_mat(n) if kind == "marmousi" else H.init_c1_mat(.5, .5, n)
+A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm)
+A.krylov_mode("fused")
+A.small_cycle("off")
+f = H.init_f1_mat(.5, .125, om, n).ravel()
+x, info, hist = H.gmres(A, f, rtol=1e-12, restart=20, maxiter=30, M=None if pc == "none" else pc,
+                        callback=lambda r: None, callback_type="legacy", return_history=True)
+assert A.last_solve_path() == "one-pass"
+np.savez(out, x=x, info=info, hist=hist)
+'''
+
+
+@pytest.mark.parametrize("n,kind,pc", [(1024, "c1", "jacobi"), (613, "marmousi", "none")])
+def test_fused_pass_alternating_march_matches(tmp_path, n, kind, pc):
+    """HH_FUSED_ALT=1 (fused_iter_kernel's odd bands march downwards, so a band's re-formed halo
+    rows are read while their owner reads them) against the all-upward march: per point the
+    same arithmetic, only the order of a band's rows in its partial row differs -- the first
+    iterations to rounding, the 30-iteration history and the field within the parity
+    contract."""
+    import subprocess
+    import sys
+    res = []
+    for alt in ("0", "1"):
+        out = tmp_path / f"alt{alt}.npz"
+        env = dict(os.environ, HH_FUSED_ALT=alt)
+        subprocess.run([sys.executable, "-c", _ALT_CHILD, ROOT, str(n), kind, pc, str(out)],
+                       env=env, check=True, timeout=240)
+        res.append(np.load(out))
+    a, b = res
+    assert int(a["info"]) == int(b["info"]) and len(a["hist"]) == len(b["hist"]) == 30
+    assert np.max(np.abs(a["hist"][:5] - b["hist"][:5]) / a["hist"][:5]) < 1e-10
+    assert np.max(np.abs(a["hist"] - b["hist"]) / a["hist"]) < TOL
+    assert relerr(b["x"], a["x"]) < TOL

@@ -18,6 +18,17 @@ sys.path.insert(0, ROOT)
 import helmholtz_preconditioner_amd as H  # noqa: E402
 from helmholtz_preconditioner_amd import _ffi  # noqa: E402
 
+def device_used_bytes():
+    """bytes in use on the current device (hipMemGetInfo: total - free), for the peak-memory
+    figure of the preconditioner's operator data"""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    free, total = ctypes.c_size_t(), ctypes.c_size_t()
+    if hip.hipMemGetInfo(ctypes.byref(free), ctypes.byref(total)) != 0:
+        return None
+    return total.value - free.value
+
+
 args = sys.argv[1:]
 form, maxiter, wgs = "auto", 300, 0
 while args and args[0].startswith("--"):
@@ -35,11 +46,13 @@ for n in ns:
     cm, f = H.init_c1_f1(om, n)
     A = H.build_A_matrix(b, C, eta, om, h, n, cm)
     A.ctx.synchronize()
+    mem0 = device_used_bytes()
     t0 = time.perf_counter()
     Msw = H.Sweeping(A, form=form, workgroups=wgs)
     Msw.configure()
     A.ctx.synchronize()
     t_setup = time.perf_counter() - t0
+    mem1 = device_used_bytes()
     x, y = A.vector(f.ravel()), A.vector()
     A.apply_device(x, y, _ffi.HH_APPLY_PREC)
     t0 = time.perf_counter()
@@ -66,6 +79,9 @@ for n in ns:
     A.close()
     line = (f"n={n} b={b} wn={wn} form={form} ({kind}): setup {t_setup*1e3:.1f} ms, apply {t_apply*1e3:.2f} ms{gbs}, "
             f"corrected-sweep GMRES {len(hist)} its info={info} in {t_solve:.3f} s")
+    if mem0 is not None and mem1 is not None:
+        line += (f" | device memory: operator {mem0 / 1e9:.2f} GB, + preconditioner "
+                 f"{(mem1 - mem0) / 1e9:.2f} GB = {mem1 / 1e9:.2f} GB in use after setup")
     if n <= 255 and os.path.isdir(os.path.join(ROOT, "oracle")):
         from oracle import helmholtz_oracle as O
         t0 = time.perf_counter()
