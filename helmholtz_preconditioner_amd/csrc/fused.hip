@@ -155,12 +155,7 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
   };
   auto unew1_finish = [&](int r, int c, const EdgeLd& e) {
     const int k = lane & 31;
-    double2 tk = csel(k < K, cmul(coef[min(k, K - 1)], e.vk), z);
-#pragma unroll
-    for (int off = 16; off > 0; off >>= 1) {
-      tk.x += __shfl_xor(tk.x, off);
-      tk.y += __shfl_xor(tk.y, off);
-    }
+    const double2 tk = half_sum2(csel(k < K, cmul(coef[min(k, K - 1)], e.vk), z));
     return row_value<1>(a, rlo, rhi, r, c, csub(e.wv, tk));
   };
   const double2 AW = a.tab_i[ic], AE = a.tab_i[n + ic], R1 = a.tab_i[2 * n + ic];
@@ -201,7 +196,7 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
       if (ee && lane == kWave - 1) urow[buf][kT + 1] = csel(ehas, ue, z);
       __syncthreads();
       const double2 uW = urow[buf][t], uE = urow[buf][t + 2];
-      const double* q = reinterpret_cast<const double*>(a.tab_j) + 8 * (size_t)r;
+      const cdouble_p q = crow(a.tab_j, r);
       const double2 R2 = make_double2(q[0], q[1]), BS = make_double2(q[2], q[3]);
       const double2 BN = make_double2(q[4], q[5]), OM = make_double2(q[6], q[7]);
       const size_t p = (size_t)r * n + ic;
@@ -382,16 +377,9 @@ __global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
   };
   auto unew2_finish = [&](int r1, int c1, int r2, int c2, const EdgeLd& e) {
     const int k = lane & 31;
-    double2 tk = csel(k < K, cmul(coef[min(k, K - 1)], e.vk), z);
-#pragma unroll
-    for (int off = 16; off > 0; off >>= 1) {
-      tk.x += __shfl_xor(tk.x, off);
-      tk.y += __shfl_xor(tk.y, off);
-    }
-    const double2 ua = make_double2(__shfl(tk.x, 0), __shfl(tk.y, 0));
-    const double2 ub = make_double2(__shfl(tk.x, 32), __shfl(tk.y, 32));
-    const double2 wa = make_double2(__shfl(e.wv.x, 0), __shfl(e.wv.y, 0));
-    const double2 wb = make_double2(__shfl(e.wv.x, 32), __shfl(e.wv.y, 32));
+    const double2 tk = half_sum2(csel(k < K, cmul(coef[min(k, K - 1)], e.vk), z));
+    const double2 ua = rlane2(tk, 0), ub = rlane2(tk, 32);
+    const double2 wa = rlane2(e.wv, 0), wb = rlane2(e.wv, 32);
     return make_double2x2(row_value<2>(a, rlo, rhi, r1, c1, csub(wa, ua)),
                           row_value<2>(a, rlo, rhi, r2, c2, csub(wb, ub)));
   };
@@ -405,7 +393,7 @@ __global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
     double2 W, E, S, N, D, Db;
   };
   auto coefs = [&](int r, int c, double icv) {
-    const double* q = reinterpret_cast<const double*>(a.tab_j) + 8 * (ptrdiff_t)min(max(r, -2), nl + 1);
+    const cdouble_p q = crow(a.tab_j, min(max(r, -2), nl + 1));
     const double2 R2 = make_double2(q[0], q[1]), BS = make_double2(q[2], q[3]);
     const double2 BN = make_double2(q[4], q[5]), OM = make_double2(q[6], q[7]);
     const double2 AW = a.tab_i[c], AE = a.tab_i[n + c], R1 = a.tab_i[2 * n + c];
@@ -510,7 +498,7 @@ __global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
         // D_beta and the reciprocal of |D_beta|^2 always carried
         double2 W2 = Wm, E2 = Em, S2 = Sm, N2 = Nm;
         if constexpr (!kCarry) {
-          const double* q = reinterpret_cast<const double*>(a.tab_j) + 8 * (size_t)r;
+          const cdouble_p q = crow(a.tab_j, r);
           const double2 R2 = make_double2(q[0], q[1]), BS = make_double2(q[2], q[3]);
           const double2 BN = make_double2(q[4], q[5]);
           const double2 AW = a.tab_i[ic], AE = a.tab_i[n + ic], R1 = a.tab_i[2 * n + ic];
@@ -794,7 +782,7 @@ static_assert(kFusedMaxK == 20, "table covers 1..kFusedMaxK");
 }  // namespace
 
 // HH_FUSED_ALT=0 turns the alternating march off (A/B); read once
-constexpr bool kFusedAltDefault = false;
+constexpr bool kFusedAltDefault = true;  // config 2: +3.6 % (profiles/r05/r05b_ab_alt.log)
 bool fused_alt_dir() {
   static const bool on = [] {
     const char* e = std::getenv("HH_FUSED_ALT");

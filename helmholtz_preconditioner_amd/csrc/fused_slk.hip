@@ -84,7 +84,7 @@ void fused_slk_kernel(const FusedArgs a) {
   // the operator's coefficients at row r (clamped to the slab's tables), column tables given
   // (stencil.hip's expressions and order)
   auto coefs = [&](int r, double2 AW, double2 AE, double2 R1, double icv) {
-    const double* q = reinterpret_cast<const double*>(a.tab_j) + 8 * (ptrdiff_t)min(max(r, -2), nl + 1);
+    const cdouble_p q = crow(a.tab_j, min(max(r, -2), nl + 1));
     const double2 R2 = make_double2(q[0], q[1]), BS = make_double2(q[2], q[3]);
     const double2 BN = make_double2(q[4], q[5]), OM = make_double2(q[6], q[7]);
     Co o;
@@ -114,12 +114,46 @@ void fused_slk_kernel(const FusedArgs a) {
     return (r >= 0 && r < nl) || (r < 0 && a.lo_mode != FROW_ZERO) ||
            (r >= nl && a.hi_mode != FROW_ZERO);
   };
-  // ---- the loads of one row (issued a step ahead)
+  // u_K of a row outside the slab (rows -2, -1 and nl, nl + 1): received from the neighbour
+  // rank (FROW_HALO) or zero (FROW_ZERO) -- fused.hip row_value as selects over a value loaded
+  // unconditionally with the row's other loads (a load under a branch makes every later use
+  // of any load wait for all of them: vmcnt(0) at the join)
+  const bool lo_halo = a.lo_mode == FROW_HALO, hi_halo = a.hi_mode == FROW_HALO;
+  const double2* h_lo = lo_halo ? a.halo_lo : a.win;  // (a valid address either way)
+  const double2* h_hi = hi_halo ? a.halo_hi : a.win;
+  auto halo_ld = [&](int r, int col) {
+    const bool lo = r < 0;
+    const double2* base = lo ? h_lo : h_hi;
+    const int idx = lo ? min(max(r + 2, 0), 1) : min(max(r - nl, 0), 1);
+    return base[(size_t)idx * n + col];
+  };
+  auto row_sel = [&](int r, double2 formed, double2 hv) {
+    const bool halo = r < 0 ? lo_halo : hi_halo;
+    return csel(r >= rlo && r < rhi, formed, csel(halo, hv, z));
+  };
+  // ---- the loads of one row (issued a step ahead; all unconditional)
   double2 pw, pv[KS];                      // w_{K-1} and the LDS-ring vectors of row L
   double2 rg[4][KR > 0 ? KR : 1];          // register ring: rows (slot = step mod 4)
   double pic[2], pice[2];                  // 1/c^2 of row L - 1 (own, edge column), by parity
   double2 pe_w = z, pe_v = z;              // edge waves: w and c_k u_k terms (unew2)
+  double2 ph = z, peh = z;                 // halo values of the own point and the edge point
   auto issue = [&](int L, int s_ring, int s_par) {
+    const int Lc = min(L, re + 1);
+    // first the edge terms (fused.hip unew2: the other waves load the same in-cache addresses,
+    // so no load sits under a branch) and the halo values -- the loads a step waits for last
+    // are then the row's basis, and no wait for them also waits for the step's stores
+    {
+      const int h = lane >> 5, k = lane & 31;
+      const int r = h ? Lc - 1 : Lc, c = h ? io : ie;
+      const int rr = min(max(r, rlo), rhi - 1);
+      const ptrdiff_t p = (ptrdiff_t)rr * n + c;
+      pe_w = a.win[p];
+      pe_v = (a.V + p)[(size_t)min(k, K - 1) * a.ldv];
+      peh = halo_ld(r, c);
+    }
+    pice[s_par] = icv_at(Lc - 1, ie);
+    pic[s_par] = icv_at(Lc - 1, ic);
+    ph = halo_ld(Lc, ic);
     const int rc = min(max(L, rlo), rhi - 1);
     gd2* vrow = gptr(a.V + (ptrdiff_t)rc * n);
     gd2* wrow = gptr(a.win + (ptrdiff_t)rc * n);
@@ -130,17 +164,6 @@ void fused_slk_kernel(const FusedArgs a) {
     for (int q = 0; q < KS; ++q) pv[q] = ld_at(vrow + (size_t)q * a.ldv, bo);
 #pragma unroll
     for (int q = 0; q < KR; ++q) rg[s_ring][q] = ld_at(vrow + (size_t)(KS + q) * a.ldv, bo);
-    const int Lc = min(L, re + 1);
-    pic[s_par] = icv_at(Lc - 1, ic);
-    if (ew || ee) {  // (wave-uniform: the edge waves' lane-parallel terms, fused.hip unew2)
-      const int h = lane >> 5, k = lane & 31;
-      const int r = h ? Lc - 1 : Lc, c = h ? io : ie;
-      const int rr = min(max(r, rlo), rhi - 1);
-      const ptrdiff_t p = (ptrdiff_t)rr * n + c;
-      pe_w = a.win[p];
-      pe_v = (a.V + p)[(size_t)min(k, K - 1) * a.ldv];
-      pice[s_par] = icv_at(Lc - 1, ie);
-    }
   };
   double2 acc[K + 1];
 #pragma unroll
@@ -153,6 +176,11 @@ void fused_slk_kernel(const FusedArgs a) {
     double invm = 1.0;
     double2 Wm = z, Em = z, Sm = z, Nm = z;
     int buf = 0;
+    // row r's w_K and u_K are stored one step later, before that step's prefetch: a store
+    // issued between the prefetch and its use (under the branch that skips rows outside the
+    // band) made the compiler wait for every load at the next use (vmcnt(0) at the join)
+    double2 sw = z, su = z;
+    int sr = -1;  // (uniform) the row pending, or -1
     issue(rb - 2, 0, 0);
     for (int L0 = rb - 2; L0 <= re + 1; L0 += 4) {
 #pragma unroll
@@ -178,29 +206,29 @@ void fused_slk_kernel(const FusedArgs a) {
             }
           }
           asm volatile("" : "+v"(w.x), "+v"(w.y));
-          uN = row_value<2>(a, rlo, rhi, Lc, ic, w);
+          uN = row_sel(Lc, w, ph);
         }
         {
           const int slot = (Lc % 3 + 3) % 3;
 #pragma unroll
           for (int q = 0; q < KS; ++q) vkeep[slot][q][t] = pv[q];
         }
+        if (sr >= 0 && act) {  // (the last step's row)
+          const size_t p = (size_t)sr * n + ic;
+          a.wout[p] = sw;
+          a.uout[p] = su;
+        }
+        sr = -1;
         // the edge waves' u_K at (L, ie) and (L - 1, io): the terms summed by shuffles
         double2 euN = z, eo = z;
         if (ew || ee) {
           const int k = lane & 31;
-          double2 tk = csel(k < K, cmul(coef[min(k, K - 1)], pe_v), z);
-#pragma unroll
-          for (int off = 16; off > 0; off >>= 1) {
-            tk.x += __shfl_xor(tk.x, off);
-            tk.y += __shfl_xor(tk.y, off);
-          }
-          const double2 ua = make_double2(__shfl(tk.x, 0), __shfl(tk.y, 0));
-          const double2 ub = make_double2(__shfl(tk.x, 32), __shfl(tk.y, 32));
-          const double2 wa = make_double2(__shfl(pe_w.x, 0), __shfl(pe_w.y, 0));
-          const double2 wb = make_double2(__shfl(pe_w.x, 32), __shfl(pe_w.y, 32));
-          euN = csel(ehas, row_value<2>(a, rlo, rhi, Lc, ie, csub(wa, ua)), z);
-          eo = csel(ohas, row_value<2>(a, rlo, rhi, Lc - 1, io, csub(wb, ub)), z);
+          const double2 tk = half_sum2(csel(k < K, cmul(coef[min(k, K - 1)], pe_v), z));
+          const double2 ua = rlane2(tk, 0), ub = rlane2(tk, 32);
+          const double2 wa = rlane2(pe_w, 0), wb = rlane2(pe_w, 32);
+          const double2 ha = rlane2(peh, 0), hb = rlane2(peh, 32);
+          euN = csel(ehas, row_sel(Lc, csub(wa, ua), ha), z);
+          eo = csel(ohas, row_sel(Lc - 1, csub(wb, ub), hb), z);
         }
         // row L + 1's loads, in flight during the rest of the step
         issue(L + 1, (s + 1) & 3, (s + 1) & 1);
@@ -250,17 +278,15 @@ void fused_slk_kernel(const FusedArgs a) {
         // 1/|D_beta|^2 carried from the last step
         const int r = Lc - 2;
         if (real && r >= rb && r < re) {  // (block-uniform)
-          const size_t p = (size_t)r * n + ic;
           double2 Az = cmul(Sm, z1a);
           Az = cfma(Wm, zW, Az);
           Az = cfma(Dbm, z1b, Az);
           Az = cfma(Em, zE, Az);
           Az = cfma(Nm, z1c, Az);
           const double2 w = csel(act, cadd(z1b, cscale(cdivr(csub(Tm, Az), Dbm, invm), damp)), z);
-          if (act) {
-            a.wout[p] = w;
-            a.uout[p] = uP;
-          }
+          sw = w;
+          su = uP;
+          sr = r;
           const double2 uo = csel(act, uP, z);
           nu = fma(uo.x, uo.x, fma(uo.y, uo.y, nu));
           nw = fma(w.x, w.x, fma(w.y, w.y, nw));
@@ -287,6 +313,11 @@ void fused_slk_kernel(const FusedArgs a) {
         Nm = c1.N;
         buf ^= 1;
       }
+    }
+    if (sr >= 0 && act) {
+      const size_t p = (size_t)sr * n + ic;
+      a.wout[p] = sw;
+      a.uout[p] = su;
     }
   }
   double v[2 * (K + 1) + 2];

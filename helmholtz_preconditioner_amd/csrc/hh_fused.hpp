@@ -6,6 +6,7 @@
 
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
+#include "hh_wave.hpp"
 
 namespace hh {
 namespace fusedk {
@@ -35,6 +36,32 @@ __device__ __forceinline__ double2 ld_at(gd2* row, unsigned boff) {
   using gc = const __attribute__((address_space(1))) char;
   const d2v v = *(gd2*)((gc*)row + boff);
   return make_double2(v.x, v.y);
+}
+
+// Row tables through the constant address space: loads of a uniform address become scalar
+// loads (s_load, waited for by lgkmcnt).  Through a plain pointer they were vector loads, and
+// the vmcnt wait for them also waited for every load issued earlier -- the next row's prefetch.
+using cdouble_p = const __attribute__((address_space(4))) double*;
+__device__ __forceinline__ cdouble_p crow(const double2* tab, ptrdiff_t r) {
+  return (cdouble_p)(reinterpret_cast<const double*>(tab) + 8 * r);
+}
+
+// Sum over the 32 lanes of this lane's half-wave, fixed order, the same bits on every lane of
+// the half: pairs, quads, 8 and 16 by DPP lane moves (hh_wave.hpp), then the half's two rows
+// by permlane16_swap -- VALU only, where an xor-shuffle tree is 5 dependent ds_bpermute
+// rounds (the edge waves' critical path in the one-pass kernels)
+__device__ __forceinline__ double half_sum(double v) {
+  v += dpp_mov<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141, 0xf>(v);  // row_half_mirror
+  v += dpp_mov<0x140, 0xf>(v);  // row_mirror
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __hiloint2double(h16[0], l16[0]) + __hiloint2double(h16[1], l16[1]);
+}
+__device__ __forceinline__ double2 half_sum2(double2 v) {
+  return make_double2(half_sum(v.x), half_sum(v.y));
 }
 
 // The band of this block: tiles dealt to XCDs in contiguous runs (block b -> XCD b % 8).

@@ -1,7 +1,9 @@
 """A/B of the GMRES inner-iteration modes on one grid, interleaved in one process: "two"
 (projections, then the updated vector's norm), "one" (lagged normalisation, one reduction
 per iteration) and "fused" (one pass over the basis per iteration; env MODES selects), BASELINE config 2 by default (1024^2, constant medium, wn 64, Jacobi,
-GMRES(20), K = 100 inner iterations).  usage: python tools/ab_krylov_mode.py [n] [wn] [reps]"""
+GMRES(20), K = 100 inner iterations).  usage: python tools/ab_krylov_mode.py [n] [wn] [reps]
+env VSLABS=S: the grid as S virtual slabs of one rank (one pass launch per slab: the per-rank
+slab shapes of an S-rank run, for PMC records of N > 1 lines)"""
 import os
 import sys
 import time
@@ -19,7 +21,9 @@ MODES = [m for m in os.environ.get("MODES", "two,one,fused").split(",")]
 om, h, eta = H.problem_params(n, 12, wn, 2.0)
 PRE = os.environ.get("PRECOND", "jacobi")  # jacobi | sl (config 3: Marmousi-like, SL beta 0.5)
 cm = H.marmousi_like_c_mat(n) if PRE == "sl" else H.constant_c_mat(n)
-A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm)
+VS = int(os.environ.get("VSLABS", "1"))
+ctx = H.Context(device=0, virtual_slabs=VS) if VS > 1 else None
+A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, context=ctx)
 f = H.init_f1_mat(.5, .125, om, n).ravel()
 M = H.ShiftedLaplace(A, beta=0.5, sweeps=2, damping=0.7) if PRE == "sl" else "jacobi"
 hist = {}

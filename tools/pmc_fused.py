@@ -4,9 +4,11 @@ algorithmic bytes: reads (K + 1) 16 B per unknown (the K basis vectors v_0 .. v_
 writes 32 B (u_{j+1} into V[K], w_{j+1}); + 8 B read of 1/c^2 for a non-constant medium.
 FETCH_SIZE is doubled (gfx950 correction for 16-B/lane coalesced reads, MI355X_MICROARCH.md),
 as in tools/pmc_traffic.py.
-usage: python tools/pmc_fused.py FETCH_CSV WRITE_CSV --n N [--medium const|marmousi]
-       [--merge DB.json --key KEY]  (records the cycle's ratio and the per-K ratios under KEY,
-       for bench.py's GMRES block)"""
+usage: python tools/pmc_fused.py FETCH_CSV WRITE_CSV --n N [--rows R] [--medium const|marmousi]
+       [--precond jacobi|sl|none] [--restart 20] [--knobs K=V,...] [--merge DB.json]
+       (records the cycle's ratio and the per-K ratios under the key bench.py looks up,
+       n{N}_rows{R}_{medium}_{precond}_r{restart}, with the kernel knobs the profiled run set;
+       --rows: the slab height of one pass launch -- a virtual slab of the profiled run)"""
 import argparse
 import csv
 import json
@@ -31,10 +33,14 @@ def main():
     p.add_argument("write")
     p.add_argument("--n", type=int, required=True)
     p.add_argument("--medium", default="const")
+    p.add_argument("--rows", type=int, default=0)
+    p.add_argument("--precond", default="jacobi")
+    p.add_argument("--restart", type=int, default=20)
+    p.add_argument("--knobs", default="")
     p.add_argument("--merge")
-    p.add_argument("--key")
     a = p.parse_args()
-    N = a.n * a.n
+    rows = a.rows or a.n
+    N = a.n * rows
     fetch, write = load(a.fetch), load(a.write)
     tot_t = tot_a = 0.0
     per_k = {}
@@ -54,9 +60,11 @@ def main():
     if tot_a:
         print(f"all launches: {tot_t / 1e9:.2f} GB vs {tot_a / 1e9:.2f} GB algorithmic = "
               f"{tot_t / tot_a:.3f}x")
-        if a.merge and a.key:
+        if a.merge:
+            key = f"n{a.n}_rows{rows}_{a.medium}_{a.precond}_r{a.restart}"
+            knobs = dict(kv.split("=", 1) for kv in a.knobs.split(",") if kv)
             db = json.load(open(a.merge)) if os.path.exists(a.merge) else {}
-            db[a.key] = {"ratio": round(tot_t / tot_a, 4), "per_K": per_k,
+            db[key] = {"ratio": round(tot_t / tot_a, 4), "per_K": per_k, "knobs": knobs,
                          "source": f"{os.path.basename(os.path.dirname(a.fetch))}, "
                                    f"{os.path.basename(os.path.dirname(a.write))}"}
             json.dump(db, open(a.merge, "w"), indent=1, sort_keys=True)

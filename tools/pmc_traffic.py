@@ -4,9 +4,10 @@ bytes of a 16-B/lane coalesced read stream: doubled) next to each kernel's algor
 (read u 16 + 1/c^2 8, write y 16 per unknown; 16 + 16 for a constant medium).
 
 usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV --n N --medium M [--stencil S]
-                                   [--merge OUT_JSON]
---merge adds the record under key "n{N}_{M}_s{S}" to OUT_JSON (bench.py's measured_traffic
-reads profiles/r03_pmc_traffic.json).
+                                   [--rows R] [--merge OUT_JSON]
+--merge adds the record under key "n{N}_rows{R}_{M}_s{S}" to OUT_JSON (bench.py's
+measured_traffic reads profiles/r05_pmc_traffic.json); --rows: the rows of one apply launch (a
+virtual slab of the profiled run, tools/prof_stencil.py --virtual-slabs; default the grid).
 """
 import argparse
 import csv
@@ -31,9 +32,11 @@ def main():
     p.add_argument("--n", type=int, required=True)
     p.add_argument("--medium", default="marmousi")
     p.add_argument("--stencil", type=int, default=5)
+    p.add_argument("--rows", type=int, default=0)
     p.add_argument("--merge")
     a = p.parse_args()
-    N = a.n * a.n
+    rows = a.rows or a.n
+    N = a.n * rows
     rd = (16 if a.medium == "const" else 24) * N
     wr = 16 * N
     fetch, write = load(a.fetch), load(a.write)
@@ -51,7 +54,7 @@ def main():
         break  # the apply kernel with the most launches (the timed ones)
     if rec and a.merge:
         db = json.load(open(a.merge)) if os.path.exists(a.merge) else {}
-        db[f"n{a.n}_{a.medium}_s{a.stencil}"] = rec
+        db[f"n{a.n}_rows{rows}_{a.medium}_s{a.stencil}"] = rec
         json.dump(db, open(a.merge, "w"), indent=1, sort_keys=True)
 
 

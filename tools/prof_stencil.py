@@ -19,11 +19,15 @@ p.add_argument("--variant", type=int, default=-1)
 p.add_argument("--rpb", type=int, default=0)
 p.add_argument("--rotate", type=int, default=3, help="distinct (x, y) pairs, as bench.py")
 p.add_argument("--stencil", type=int, default=5, choices=[5, 9])
+p.add_argument("--virtual-slabs", type=int, default=1,
+               help="the grid as S slabs of one rank: one apply launch per slab (a rank's slab "
+                    "shape of an S-rank run)")
 a = p.parse_args()
 n = a.n
 om, h, eta = H.problem_params(n, 12, 100.0, 2.0)
 cm = H.marmousi_like_c_mat(n) if a.medium == "marmousi" else H.constant_c_mat(n)
-A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, stencil=a.stencil)
+ctx = H.Context(device=0, virtual_slabs=a.virtual_slabs) if a.virtual_slabs > 1 else None
+A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, stencil=a.stencil, context=ctx)
 if a.variant >= 0 or a.rpb > 0:
     A.tune(variant=a.variant, rows_per_block=a.rpb)
 xs, ys = [A.vector() for _ in range(a.rotate)], [A.vector() for _ in range(a.rotate)]
