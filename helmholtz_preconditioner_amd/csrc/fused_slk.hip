@@ -60,14 +60,22 @@ void fused_slk_kernel(const FusedArgs a) {
   const int ic = min(i, n - 1);
   const int rb = bd.rb, re = bd.re;
   const int rlo = a.lo_mode == FROW_MEM ? -2 : 0, rhi = a.hi_mode == FROW_MEM ? nl + 2 : nl;
-  // edge waves: wave 0 the W edge column i0-1 (outer i0-2, inner i0 = LDS slot 1), the last
-  // wave the E edge column i0+kT (outer i0+kT+1, inner i0+kT-1 = LDS slot kT)
-  const bool ew = wv == 0, ee = wv == kT / kWave - 1;
-  const int ie_raw = ew ? i0 - 1 : i0 + kT, io_raw = ew ? i0 - 2 : i0 + kT + 1;
-  const bool ehas = (ew || ee) && ie_raw >= 0 && ie_raw < n;
-  const bool ohas = (ew || ee) && io_raw >= 0 && io_raw < n;
+  // The strip's two edge columns, W: i0-1 (outer i0-2, inner i0 = LDS slot 1) and E: i0+kT
+  // (outer i0+kT+1, inner i0+kT-1 = LDS slot kT), take work from all four waves: waves 0 (W)
+  // and 3 (E) form u_K at (L, edge) and (L-1, outer) by lane-parallel sums before the row's
+  // barrier and publish them in LDS; waves 1 (W) and 2 (E) form the edge column's T and z1
+  // after it.  (fused_sl_iter_kernel keeps both on waves 0 and 3, whose extra ~130 instructions
+  // per step the other waves then waited for at every barrier -- at one wave per SIMD that idle
+  // time is the SIMD's.)  The same values by the same arithmetic.
+  const bool west = wv < 2;                           // this wave's side
+  const bool eu = wv == 0 || wv == 3, ez = wv == 1 || wv == 2;
+  const int ie_raw = west ? i0 - 1 : i0 + kT, io_raw = west ? i0 - 2 : i0 + kT + 1;
+  const bool ehas = ie_raw >= 0 && ie_raw < n;
+  const bool ohas = io_raw >= 0 && io_raw < n;
   const int ie = min(max(ie_raw, 0), n - 1), io = min(max(io_raw, 0), n - 1);
-  const int islot = ew ? 1 : kT;  // LDS slot of the edge column's inner neighbour
+  const int islot = west ? 1 : kT;  // LDS slot of the edge column's inner neighbour
+  const int eslot = west ? 0 : kT + 1;  // LDS slot of the edge column
+  __shared__ double2 eus[2][2][2];  // [buf][side][u_K(L, edge), u_K(L-1, outer)]
   load_coef<K>(a, coef);
   __syncthreads();
   const double sin = *a.sin;
@@ -219,9 +227,9 @@ void fused_slk_kernel(const FusedArgs a) {
           a.uout[p] = su;
         }
         sr = -1;
-        // the edge waves' u_K at (L, ie) and (L - 1, io): the terms summed by shuffles
+        // waves 0 / 3: u_K at (L, ie) and (L - 1, io), the terms summed across the half-waves
         double2 euN = z, eo = z;
-        if (ew || ee) {
+        if (eu) {
           const int k = lane & 31;
           const double2 tk = half_sum2(csel(k < K, cmul(coef[min(k, K - 1)], pe_v), z));
           const double2 ua = rlane2(tk, 0), ub = rlane2(tk, 32);
@@ -235,14 +243,12 @@ void fused_slk_kernel(const FusedArgs a) {
         __builtin_amdgcn_sched_barrier(0);
         urow[buf][1 + t] = csel(act, uC, z);
         zrow[buf][1 + t] = csel(act, z1b, z);
-        if (ew && lane == 0) {
-          urow[buf][0] = euC;
-          zrow[buf][0] = ez1b;
+        if (eu && lane == 0) {
+          urow[buf][eslot] = euC;
+          eus[buf][west ? 0 : 1][0] = euN;
+          eus[buf][west ? 0 : 1][1] = eo;
         }
-        if (ee && lane == kWave - 1) {
-          urow[buf][kT + 1] = euC;
-          zrow[buf][kT + 1] = ez1b;
-        }
+        if (ez && lane == 0) zrow[buf][eslot] = ez1b;
         __syncthreads();
         const double2 uW = urow[buf][t], uE = urow[buf][t + 2];
         const double2 zW = zrow[buf][t], zE = zrow[buf][t + 2];
@@ -260,11 +266,14 @@ void fused_slk_kernel(const FusedArgs a) {
           return make_double2(fma(x.x, b.x, x.y * b.y) * inv, fma(x.y, b.x, -x.x * b.y) * inv);
         };
         const double2 z1c = csel(act && v1, cscale(cdivr(T1, c1.Db, inv1), damp), z);
-        // the same at the edge column (edge waves; broadcast values)
+        // waves 1 / 2: the same at the edge column (broadcast values; u_K of the edge and outer
+        // columns from waves 0 / 3 through LDS)
         double2 ez1c = z;
-        if (ew || ee) {
+        if (ez) {
+          euN = eus[buf][west ? 0 : 1][0];
+          eo = eus[buf][west ? 0 : 1][1];
           const double2 uin = urow[buf][islot];
-          const double2 eW = ew ? eo : uin, eE = ew ? uin : eo;
+          const double2 eW = west ? eo : uin, eE = west ? uin : eo;
           const Co ce = coefs(Lc - 1, AWe, AEe, R1e, pice[s & 1]);
           double2 Ae = cmul(ce.S, euP);
           Ae = cfma(ce.W, eW, Ae);
@@ -348,9 +357,11 @@ static_assert(kFusedMaxK == 20, "table covers 1..kFusedMaxK");
 
 }  // namespace
 
-// HH_SLK: the smallest K that takes this kernel (0 = never), read once; the default
-// kSlkMinK (0 until measured on hardware)
-constexpr int kSlkMinK = 0;
+// HH_SLK: the smallest K that takes this kernel (0 = never), read once.  Default 2: at K = 1
+// (two vectors) fused_sl_iter_kernel's two blocks per CU win, 336 vs 412 us at 4096^2; from
+// K = 4 this kernel does, 478 vs 493 us ... 1240 vs 1862 us at K = 19
+// (profiles/r05/r05e_slk0_tbps.txt, r05e_slk1_tbps.txt)
+constexpr int kSlkMinK = 2;
 int fused_slk_min_k() {
   static const int v = [] {
     const char* e = std::getenv("HH_SLK");
