@@ -94,7 +94,7 @@ def test_multiprocess_slabs_match_single_domain(tmp_path, world, slabs, stencil)
         _single_domain(150, stencil), world, 150)
 
 
-def _check_against_single_domain(parts, ref, world, n):
+def _check_against_single_domain(parts, ref, world, n, tol=1e-8):
     assert parts[0]["j0"] == 0 and parts[-1]["j1"] == n
     for a, b in zip(parts, parts[1:]):
         assert a["j1"] == b["j0"]
@@ -113,7 +113,7 @@ def _check_against_single_domain(parts, ref, world, n):
                          len(href), float(herr)))
         xerr = np.linalg.norm(x - ref[f"x_{name}"]) / np.linalg.norm(ref[f"x_{name}"])
         errs.append((name, "x", 0, 0, 0, 0, float(xerr)))
-    bad = [e for e in errs if e[2] != e[3] or e[4] != e[5] or not e[6] < 1e-8]
+    bad = [e for e in errs if e[2] != e[3] or e[4] != e[5] or not e[6] < tol]
     assert not bad, "\n".join(map(str, errs))
     assert all(float(p["maxrank"]) == world - 1 for p in parts)
     if "x_default" in ref:
@@ -152,7 +152,12 @@ def test_fused_pass_ranks_match_single_domain(tmp_path, world, slabs, transport)
     for name in ("none", "jacobi", "sl"):
         assert ref[f"path_{name}"] == "one-pass"
         assert all(str(p[f"path_{name}"]) == "one-pass" for p in parts), name
-    _check_against_single_domain(parts, ref, world, n)
+    # 16 slabs (8 ranks x 2): the Jacobi field lands 1.2e-8 from the single domain after 50
+    # iterations -- the summation order alone does that: the numpy mirror of this solve on 1 vs
+    # 16 slabs differs by 1.7e-8 in the field, 1.2e-9 in the history, and scipy on f vs
+    # f (1 + 1e-15) by 7.7e-6 (tools/slab_drift.py --n 150 --slabs 16 --restart 20 --iters 50,
+    # profiles/r05/r05_slab_drift_cpu_150_16slabs_jacobi.log)
+    _check_against_single_domain(parts, ref, world, n, tol=1e-7 if world * slabs >= 16 else 1e-8)
 
 
 @pytest.mark.parametrize("world", [2, 3])

@@ -32,10 +32,13 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 from oracle import helmholtz_oracle as O  # noqa: E402
 
-WN, RESTART, ITERS, RTOL = 6.0, 12, 26, 1e-3  # the virtual-slab test's problem
+WN, RTOL = 6.0, 1e-3
+RESTART, ITERS = 12, 26  # the virtual-slab test's problem (--restart / --iters override)
 
 
-def _mirror_worker(rank, world, port, n, precond, out):
+def _mirror_worker(rank, world, port, n, precond, out, restart, iters):
+    global RESTART, ITERS
+    RESTART, ITERS = restart, iters
     import torch.distributed as dist
     import dist_mirror as DM
     from helmholtz_preconditioner_amd import dist as hdist
@@ -47,7 +50,7 @@ def _mirror_worker(rank, world, port, n, precond, out):
                          jacobi=precond == "jacobi")
     f = O.init_f1_mat(.5, .125, om, n)[j0:j1].ravel()
     x, info, hist, _, _ = DM.gmres_dist_onepass(op, f, RTOL, RESTART, ITERS)
-    np.savez(out, x=x, hist=hist)
+    np.savez(out, x=x, hist=hist, j0=j0)
     dist.destroy_process_group()
 
 
@@ -59,14 +62,16 @@ def mirror(n, precond, world):
     ctx = mp.get_context("spawn")
     with tempfile.TemporaryDirectory() as td:
         outs = [os.path.join(td, f"r{r}.npz") for r in range(world)]
-        ps = [ctx.Process(target=_mirror_worker, args=(r, world, port, n, precond, outs[r]))
+        ps = [ctx.Process(target=_mirror_worker, args=(r, world, port, n, precond, outs[r],
+                                                       RESTART, ITERS))
               for r in range(world)]
         for p in ps:
             p.start()
         for p in ps:
             p.join(timeout=600)
             assert p.exitcode == 0
-        return np.load(outs[0])["hist"]
+        parts = [np.load(o) for o in outs]
+        return parts[0]["hist"], np.concatenate([p["x"] for p in parts])
 
 
 def scipy_noise(n, precond):
@@ -75,9 +80,9 @@ def scipy_noise(n, precond):
     f = O.init_f1_mat(.5, .125, om, n).ravel()
     fp = f * (1 + 1e-15 * np.random.default_rng(1).standard_normal(f.size))
     M = O.jacobi_preconditioner(A) if precond == "jacobi" else None
-    _, _, h1, _ = O.gmres_reference(A, f, M=M, rtol=RTOL, restart=RESTART, maxiter=ITERS)
-    _, _, h2, _ = O.gmres_reference(A, fp, M=M, rtol=RTOL, restart=RESTART, maxiter=ITERS)
-    return h1, h2
+    x1, _, h1, _ = O.gmres_reference(A, f, M=M, rtol=RTOL, restart=RESTART, maxiter=ITERS)
+    x2, _, h2, _ = O.gmres_reference(A, fp, M=M, rtol=RTOL, restart=RESTART, maxiter=ITERS)
+    return h1, h2, x1, x2
 
 
 def gpu(n, precond, slabs):
@@ -109,12 +114,16 @@ def rel(a, b):
 
 
 def main():
+    global RESTART, ITERS
     p = argparse.ArgumentParser()
     p.add_argument("--n", type=int, default=613)
     p.add_argument("--slabs", type=int, default=4)
     p.add_argument("--precond", default="jacobi", choices=["none", "jacobi", "sl"])
     p.add_argument("--gpu", action="store_true")
+    p.add_argument("--restart", type=int, default=RESTART)
+    p.add_argument("--iters", type=int, default=ITERS)
     a = p.parse_args()
+    RESTART, ITERS = a.restart, a.iters
     pc = None if a.precond == "none" else a.precond
     cols = {}
     if a.gpu:
@@ -123,10 +132,12 @@ def main():
         cols["gpu f vs f(1+1e-15)"] = rel(g["1"], g["noise"])
         hist = g["1"]
     if a.precond != "sl":  # (the mirror and the oracle restate none / Jacobi)
-        m1, mS = mirror(a.n, pc, 1), mirror(a.n, pc, a.slabs)
+        (m1, mx1), (mS, mxS) = mirror(a.n, pc, 1), mirror(a.n, pc, a.slabs)
         cols[f"mirror world 1 vs {a.slabs}"] = rel(m1, mS)
-        s1, s2 = scipy_noise(a.n, pc)
+        s1, s2, sx1, sx2 = scipy_noise(a.n, pc)
         cols["scipy f vs f(1+1e-15)"] = rel(s1, s2)
+        fields = {f"mirror world 1 vs {a.slabs}": np.linalg.norm(mxS - mx1) / np.linalg.norm(mx1),
+                  "scipy f vs f(1+1e-15)": np.linalg.norm(sx2 - sx1) / np.linalg.norm(sx1)}
         if not a.gpu:
             hist = s1
     print(f"n={a.n} c1 wave_num={WN} M={a.precond} GMRES({RESTART}) rtol={RTOL} "
@@ -137,6 +148,8 @@ def main():
         print(f"{i + 1:3d} {hist[i]:10.3e} " + " ".join(row))
     for k, v in cols.items():
         print(f"max over the first 10 / all iterations, {k}: {v[:10].max():.2e} / {v.max():.2e}")
+    for k, v in (fields.items() if a.precond != "sl" else []):
+        print(f"field relative difference after {ITERS} iterations, {k}: {v:.2e}")
 
 
 if __name__ == "__main__":
