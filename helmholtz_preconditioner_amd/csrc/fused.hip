@@ -605,36 +605,55 @@ __global__ __launch_bounds__(kT) void fused_edge_kernel(const FusedArgs a, int r
 
 // a, b of y = a + y_col b, scaled by the basis scales (x += sum (a_k + y_col b_k) v_k / sigma_k):
 // ab[k] = a_k vscale_k, ab[kMaxProj + k] = b_k vscale_k, k <= col.  Column col as started by
-// gmres_lag_kernel (unrotated); the previous columns final.  One thread (once per cycle).
+// gmres_lag_kernel (unrotated); the previous columns final.  One wave (once per cycle), lane
+// m holding row m: the rotation chain of column col run by every lane (uniform; lane k keeps
+// entry k), then a column-oriented back-substitution -- y_m = s_m / R_mm by lane m (the Smith
+// factors of every diagonal formed up front, in parallel), broadcast, and lanes k < m take
+// s_k -= y_m R_km -- so the serial chain is col steps of a few dependent multiplies.  The
+// row-oriented serial form (lane 0 alone, divisions on the chain) took 25 us per cycle even on
+// LDS operands, 58-60 us on global ones (profiles/r05/r05f_rocprof_c2_kernel_stats.csv,
+// r05i_rocprof_c2_kernel_stats.csv).  The subtraction order is gmres_solve_kernel's (m
+// descending), so a merged cycle end and the separate solve agree to rounding.
 __global__ void cycle_coef_kernel(GivensState g, int col, double2* ab) {
-  if (threadIdx.x != 0 || g.ctrl[0]) return;  // (the cycle stopped before its last column)
+  __shared__ double2 sH[(kFusedMaxK + 1) * (kFusedMaxK + 2)];  // H(c, k), c <= col, k <= col + 1
+  __shared__ double2 sG[2 * (kFusedMaxK + 1)];
+  if (g.ctrl[0]) return;  // (the cycle stopped before its last column)
   const int R1 = g.restart + 1;
-  auto H = [&](int c, int k) { return g.H[(size_t)c * R1 + k]; };
+  const int lane = threadIdx.x, me = min(lane, col);
+  for (int e = lane; e < (col + 1) * R1; e += kWave) sH[e] = g.H[e];
+  for (int e = lane; e < 2 * col; e += kWave) sG[e] = g.G[e];
+  const double2 s0 = g.S[me];
+  const double sv = g.vscale[me];
+  __syncthreads();
+  auto H = [&](int c, int k) { return sH[c * R1 + k]; };
   // column col's rows < col after the previous rotations (gmres_finish_column's chain)
-  double2 hc[kMaxProj];
-  double2 n0 = H(col, 0);
+  double2 n0 = H(col, 0), hc = make_double2(0.0, 0.0);
   for (int k = 0; k < col; ++k) {
-    const double c = g.G[2 * k].x;
-    const double2 sk = g.G[2 * k + 1], n1 = H(col, k + 1);
-    hc[k] = cadd(cscale(n0, c), cmul(sk, n1));
+    const double c = sG[2 * k].x;
+    const double2 sk = sG[2 * k + 1], n1 = H(col, k + 1);
+    const double2 v = cadd(cscale(n0, c), cmul(sk, n1));
+    if (lane == k) hc = v;
     n0 = cadd(cmul(make_double2(-sk.x, sk.y), n0), cscale(n1, c));
   }
-  double2 ya[kMaxProj], yb[kMaxProj];
-  ya[col] = make_double2(0.0, 0.0);
-  yb[col] = make_double2(1.0, 0.0);
-  for (int k = col - 1; k >= 0; --k) {
-    double2 sa = g.S[k], sb = cneg(hc[k]);
-    for (int m = k + 1; m < col; ++m) {
-      const double2 hmk = H(m, k);
-      sa = csub(sa, cmul(ya[m], hmk));
-      sb = csub(sb, cmul(yb[m], hmk));
+  const Smith f = smith_of(H(me, me));
+  // y = a + y_col b: a solves R a = S (a_col = 0), b solves R b = -hc (b_col = 1)
+  double2 sa = s0, sb = cneg(hc);
+  for (int m = col - 1; m >= 0; --m) {
+    if (lane == m) {
+      sa = smith_apply(sa, f);
+      sb = smith_apply(sb, f);
     }
-    ya[k] = cdiv_smith(sa, H(k, k));
-    yb[k] = cdiv_smith(sb, H(k, k));
+    const double2 ta = rlane2(sa, m), tb = rlane2(sb, m);
+    if (lane < m) {
+      const double2 h = H(m, lane);
+      sa = csub(sa, cmul(ta, h));
+      sb = csub(sb, cmul(tb, h));
+    }
   }
-  for (int k = 0; k <= col; ++k) {
-    ab[k] = cscale(ya[k], g.vscale[k]);
-    ab[kMaxProj + k] = cscale(yb[k], g.vscale[k]);
+  if (lane <= col) {
+    const bool last = lane == col;
+    ab[lane] = cscale(last ? make_double2(0.0, 0.0) : sa, sv);
+    ab[kMaxProj + lane] = cscale(last ? make_double2(1.0, 0.0) : sb, sv);
   }
 }
 
@@ -686,9 +705,12 @@ __global__ __launch_bounds__(kT) void cycle_end_kernel(const double2* __restrict
 
 // x += y_col vb once column col is finished: y_col = S[col] / H[col][col] (scipy's rule: S[col]
 // = 0 when H[col][col] == 0, iterative.py:815-816)
+// (a cycle that stopped before its last column col takes the solve + xupdate instead: decided
+// here, from the last column it executed, so the host need not read it first)
 __global__ __launch_bounds__(kT) void cycle_finish_kernel(GivensState g, int col,
                                                           const double2* vb, double2* x,
                                                           size_t len) {
+  if (g.ctrl[1] != col) return;
   const int R1 = g.restart + 1;
   const double2 hcc = g.H[(size_t)col * R1 + col];
   const double2 sc = g.S[col];
@@ -787,6 +809,16 @@ bool fused_alt_dir() {
   static const bool on = [] {
     const char* e = std::getenv("HH_FUSED_ALT");
     return e ? e[0] != '0' : kFusedAltDefault;
+  }();
+  return on;
+}
+
+// One-pass column on one rank: the partial-row reduce and the lag step in one launch
+// (gmres_lag_red_kernel); HH_LAG_RED=0 keeps the two launches (A/B).
+bool lag_red_merge() {
+  static const bool on = [] {
+    const char* e = std::getenv("HH_LAG_RED");
+    return e ? e[0] != '0' : true;
   }();
   return on;
 }

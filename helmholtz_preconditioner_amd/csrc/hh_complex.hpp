@@ -46,4 +46,26 @@ __device__ __forceinline__ double2 cdiv_smith(double2 a, double2 b) {
   }
 }
 
+// cdiv_smith split in two: the divisor's factors (its two divisions, independent of the
+// dividend: computed for every diagonal at once, off a back-substitution's serial chain) and
+// their application (multiplies only).  smith_apply(a, smith_of(b)) is cdiv_smith(a, b).
+struct Smith {
+  double rat, scl;
+  int mode;  // 0: |b.x| >= |b.y|, 1: |b.x| < |b.y|, 2: b == 0
+};
+__device__ __forceinline__ Smith smith_of(double2 b) {
+  if (fabs(b.x) >= fabs(b.y)) {
+    if (b.x == 0.0 && b.y == 0.0) return Smith{0.0, 0.0, 2};
+    const double rat = b.y / b.x;
+    return Smith{rat, 1.0 / (b.x + b.y * rat), 0};
+  }
+  const double rat = b.x / b.y;
+  return Smith{rat, 1.0 / (b.y + b.x * rat), 1};
+}
+__device__ __forceinline__ double2 smith_apply(double2 a, Smith f) {
+  if (f.mode == 0) return make_double2((a.x + a.y * f.rat) * f.scl, (a.y - a.x * f.rat) * f.scl);
+  if (f.mode == 1) return make_double2((a.x * f.rat + a.y) * f.scl, (a.y * f.rat - a.x) * f.scl);
+  return make_double2(a.x / 0.0, a.y / 0.0);
+}
+
 }  // namespace hh

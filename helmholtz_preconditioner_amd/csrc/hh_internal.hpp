@@ -168,9 +168,10 @@ void launch_multidot_reduced(const double2* V, size_t ldv, int K, const double2*
 void launch_update(const double2* V, size_t ldv, int K, const double* raw, const double* scale,
                    const double2* w, double2* w_out, size_t len, double* partials, int blocks,
                    hipStream_t stream, const int* stop = nullptr);
-//   xupdate: x += sum_k y_k V_k  (y complex, device, already including scales)
+//   xupdate: x += sum_k y_k V_k  (y complex, device, already including scales); ctl (nullable):
+//   the cycle's control words -- ctl[2] skips, k > ctl[1] count zero (krylov.hip xupdate_kernel)
 void launch_xupdate(const double2* V, size_t ldv, int K, const double2* y, double2* x,
-                    size_t len, int blocks, hipStream_t stream);
+                    size_t len, int blocks, hipStream_t stream, const int* ctl = nullptr);
 int stream_blocks(size_t len);
 void tune_krylov(int nt, int blocks);  // global knobs (tuning studies only)
 // Deterministic reduction of `count` partial rows of width `width` (fixed order):
@@ -264,6 +265,7 @@ bool fused_slk_use(int K);
 // fused_iter_kernel's odd bands march downwards (HH_FUSED_ALT, read once), so the halo rows a
 // band re-forms are read while their owners read them too (fused.hip)
 bool fused_alt_dir();
+bool lag_red_merge();  // HH_LAG_RED (default on)
 int fused_slk_rows(int n, int rows);
 void launch_fused_slk(int K, const FusedArgs& a, int blocks, hipStream_t stream);
 // u_K on rows [r0, r0 + c0) and [r1, r1 + c1) of a.V / a.win (rank-local), written to a.uout:
@@ -280,6 +282,7 @@ void launch_cycle_coef(const GivensState& g, int col, double2* ab, hipStream_t s
 void launch_cycle_end(int K, const double2* V, size_t ldv, const double* raw, const double* vscale,
                       const double2* ab, const double2* w, double2* x, double2* vb, size_t len,
                       double* partials, int blocks, hipStream_t stream, const int* stop);
+// x += y_col vb, only if the cycle reached its last column col (g.ctrl[1] == col)
 void launch_cycle_finish(const GivensState& g, int col, const double2* vb, double2* x, size_t len,
                          int blocks, hipStream_t stream);
 
@@ -302,6 +305,10 @@ void launch_gmres_column(const GivensState& g, int col, const double* red_dots,
 // One-allreduce iteration j (lagged normalisation; krylov.hip gmres_lag_kernel): finishes column
 // j-1 with |u_j|^2 = *sig2, starts column j from the raw dots red_dots (2(j+1) doubles, |w|^2
 // after them) and estimates the next SpMV input scale.  final_step: only finish column j-1.
+// launch_reduce + launch_gmres_lag in one launch (single rank: no allreduce between them)
+void launch_gmres_lag_red(const GivensState& g, int j, const double* partials, int count,
+                          int width, int cols, double* red, double eps, double ptol, int stop_col,
+                          hipStream_t stream);
 void launch_gmres_lag(const GivensState& g, int j, const double* red_dots, const double* sig2,
                       bool final_step, double eps, double ptol, int stop_col, hipStream_t stream);
 // Start of a cycle: S[0] = ||Mr||, vscale[0] = 1/||Mr|| from red[idx_m]; status[4] = ||r||.
@@ -367,7 +374,9 @@ size_t small_cycle_scratch_doubles(int n);
 // device (report slot 0: ctrl = 3) before any state changed, so the caller can take the regular
 // cycle
 hipError_t launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi, hipStream_t s);
-// End of a cycle: triangular solve for y, ycoef_k = y_k * vscale_k.
-void launch_gmres_solve(const GivensState& g, int col, hipStream_t stream);
+// End of a cycle: triangular solve for y, ycoef_k = y_k * vscale_k, over the columns the cycle
+// executed (g.ctrl[1] <= stop_col, read on the device); `merged`: a cycle that reached stop_col
+// was completed by the merged end instead (g.ctrl[2] = 1: the xupdate skips).
+void launch_gmres_solve(const GivensState& g, int stop_col, bool merged, hipStream_t stream);
 
 }  // namespace hh

@@ -166,18 +166,30 @@ __global__ __launch_bounds__(kT) void update_kernel(const double2* __restrict__ 
 }
 
 // x += sum_k y_k V_k (NT: the basis is dead after this pass; non-temporal loads at 4096^2).
+// ctl (the cycle's control words, nullable): ctl[2] != 0 skips the update (the merged cycle end
+// already applied it); otherwise only the ctl[1] + 1 vectors of the executed columns count --
+// the rest get coefficient 0 and re-read the last counted vector (finite, and cached: the
+// vectors past an early stop may never have been written), so the update of a cycle that
+// stopped early needs no host round trip for its length.  Full cycles: ctl[1] + 1 == K.
 template <int K, bool NT>
 __global__ __launch_bounds__(kT) void xupdate_kernel(const double2* __restrict__ V, size_t ldv,
                                                      const double2* __restrict__ y,
-                                                     double2* __restrict__ x, size_t len) {
+                                                     double2* __restrict__ x, size_t len,
+                                                     const int* ctl) {
+  int kc = K;
+  if (ctl) {
+    if (ctl[2]) return;
+    kc = min(max(ctl[1] + 1, 1), K);
+  }
   double2 c[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) c[k] = y[k];
+  for (int k = 0; k < K; ++k) c[k] = k < kc ? y[min(k, kc - 1)] : make_double2(0.0, 0.0);
   const size_t stride = (size_t)gridDim.x * kT;
   for (size_t p = (size_t)blockIdx.x * kT + threadIdx.x; p < len; p += stride) {
     double2 t = make_double2(0.0, 0.0);
 #pragma unroll
-    for (int k = 0; k < K; ++k) t = cfma(c[k], ldnt<NT>(V + (size_t)k * ldv + p), t);
+    for (int k = 0; k < K; ++k)
+      t = cfma(c[k], ldnt<NT>(V + (size_t)min(k, kc - 1) * ldv + p), t);
     x[p] = cadd(x[p], t);
   }
 }
@@ -251,29 +263,25 @@ __global__ __launch_bounds__(kT) void scale_copy_kernel(const double2* in, doubl
 }
 
 // LAPACK (3.10+) zlartg main branch: [c s; -conj(s) c] [f; g] = [r; 0], c real >= 0.
-__device__ void zlartg(double2 f, double2 g, double* c, double2* s, double2* r) {
-  if (g.x == 0.0 && g.y == 0.0) {
-    *c = 1.0;
-    *s = make_double2(0.0, 0.0);
-    *r = f;
-    return;
-  }
+// (by value: the pointer-output form kept c and r in scratch memory -- the branches' stores
+// through pointers defeated register promotion, 24 bytes of scratch per lane)
+struct Rot {
+  double c;
+  double2 s, r;
+};
+__device__ __forceinline__ Rot zlartg(double2 f, double2 g) {
+  if (g.x == 0.0 && g.y == 0.0) return Rot{1.0, make_double2(0.0, 0.0), f};
   if (f.x == 0.0 && f.y == 0.0) {
     const double d = hypot(g.x, g.y);
-    *c = 0.0;
-    *s = make_double2(g.x / d, -g.y / d);
-    *r = make_double2(d, 0.0);
-    return;
+    return Rot{0.0, make_double2(g.x / d, -g.y / d), make_double2(d, 0.0)};
   }
   const double f2 = cabs2(f);
   const double g2 = cabs2(g);
   const double h2 = f2 + g2;
   const double cc = sqrt(f2 / h2);
-  *c = cc;
-  *r = make_double2(f.x / cc, f.y / cc);
   const double d = sqrt(f2 * h2);
   const double2 fd = make_double2(f.x / d, f.y / d);
-  *s = cmul(cconj(g), fd);
+  return Rot{cc, cmul(cconj(g), fd), make_double2(f.x / cc, f.y / cc)};
 }
 
 // |w|^2 from the update kernel's per-block partials (column 0 of `width`), summed by one
@@ -340,8 +348,8 @@ __device__ __forceinline__ ColIn load_col_in(const GivensState& g, int col) {
   in.Sc = g.S[col];
   return in;
 }
-__device__ bool gmres_finish_column(const GivensState& g, int col, double2 hk, const ColIn& in,
-                                    double h0, double h1, double inv_sigma_next, double eps,
+__device__ __forceinline__ bool gmres_finish_column(const GivensState& g, int col, double2 hk,
+                                                    const ColIn& in, double h0, double h1, double inv_sigma_next, double eps,
                                     double ptol, int stop_col) {
   const int lane = threadIdx.x & (kWave - 1);
   const bool l0 = lane == 0;
@@ -365,9 +373,9 @@ __device__ bool gmres_finish_column(const GivensState& g, int col, double2 hk, c
     if (l0) h[k] = hn;
     n0 = cadd(cmul(make_double2(-s.x, s.y), n0), cscale(n1, c));  // -conj(s)*n0 + c*n1
   }
-  double c;
-  double2 s, r;
-  zlartg(n0, hsub, &c, &s, &r);
+  const Rot rot = zlartg(n0, hsub);
+  const double c = rot.c;
+  const double2 s = rot.s, r = rot.r;
   const double2 Sc = in.Sc;
   const double2 tmp = cmul(make_double2(-s.x, s.y), Sc);  // -conj(s) * S[col]
   const double presid = hypot(tmp.x, tmp.y);
@@ -453,41 +461,53 @@ __global__ void gmres_column_kernel(GivensState g, int col, const double* rd, co
 // The update (w -= sum_k d_k vscale[k]^2 u_k) follows with the exact vscale.  `final` (after the
 // cycle's last iteration): rd is unused and sig2 holds |u_j|^2 -- steps (a), (b) only.
 // One wave: entry k of a column on lane k (the sum of (d) in k order by readlane).
-__global__ void gmres_lag_kernel(GivensState g, int j, const double* rd, const double* sig2,
-                                 int final_step, double eps, double ptol, int stop_col) {
+// lag_body's operands that do not come from the reductions (the finish of column j-1 and the
+// start of column j read disjoint words: the finish writes only vscale[j], which the start takes
+// from vj), loaded from clamped addresses -- one memory latency for all of them
+struct LagIn {
+  int stopped;
+  double vs0, vcol, scol, sj, h0c, vkj;
+  double2 hk0;
+  ColIn in;
+};
+__device__ __forceinline__ LagIn lag_load(const GivensState& g, int j) {
   const int lane = threadIdx.x & (kWave - 1);
   const int R1 = g.restart + 1;
-  // every operand loaded up front, from clamped addresses (the finish of column j-1 and the start
-  // of column j read disjoint words: the finish writes only vscale[j], which the start takes
-  // from vj): one memory latency per launch
   const int col = max(j - 1, 0);
-  const int stopped = g.ctrl[0];
-  const double sig = *sig2;
-  const double vs0 = g.vscale[0], vcol = g.vscale[col], scol = g.sscale[col], sj_ = g.sscale[j];
-  const double h0c = g.status_it[4 * col + 2];  // stored when the column was started
-  const double2 hk0 = g.H[(size_t)col * R1 + min(lane, col)];  // (previous launch)
-  const ColIn in = load_col_in(g, col);
-  const int kj = min(lane, j);
-  const double vkj = g.vscale[kj];
-  const double* rdp = rd ? rd : sig2;  // (final step: rd unused, any valid words of red)
-  const double2 d = make_double2(rdp[2 * kj], rdp[2 * kj + 1]);
-  const double w2 = rdp[2 * (j + 1)];
-  if (stopped) return;
-  double vj = vs0;
+  LagIn L;
+  L.stopped = g.ctrl[0];
+  L.vs0 = g.vscale[0];
+  L.vcol = g.vscale[col];
+  L.scol = g.sscale[col];
+  L.sj = g.sscale[j];
+  L.h0c = g.status_it[4 * col + 2];                   // stored when the column was started
+  L.hk0 = g.H[(size_t)col * R1 + min(lane, col)];     // (previous launch)
+  L.in = load_col_in(g, col);
+  L.vkj = g.vscale[min(lane, j)];
+  return L;
+}
+// d = (rd[2k], rd[2k+1]) on lane k = min(lane, j), w2 = |w|^2, sig = |u_j|^2
+__device__ __forceinline__ void lag_compute(const GivensState& g, int j, const LagIn& L,
+                                            double2 d, double w2, double sig, int final_step,
+                                            double eps, double ptol, int stop_col) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int R1 = g.restart + 1;
+  const int col = max(j - 1, 0);
+  double vj = L.vs0;
   if (j >= 1) {
     const double sj = sqrt(sig);
     vj = 1.0 / sj;
-    const double f = vcol / scol;
+    const double f = L.vcol / L.scol;
     const double h1 = sj * f;
-    const double2 hk = lane <= col ? hk0 : make_double2(0.0, 0.0);
-    const bool stop = gmres_finish_column(g, col, hk, in, h0c, h1, vj, eps, ptol, stop_col);
+    const double2 hk = lane <= col ? L.hk0 : make_double2(0.0, 0.0);
+    const bool stop = gmres_finish_column(g, col, hk, L.in, L.h0c, h1, vj, eps, ptol, stop_col);
     if (stop || final_step) return;
   }
-  const double f = vj / sj_;
+  const double f = vj / L.sj;
   double2* h = g.H + (size_t)j * R1;
   double tv = 0.0, tw = 0.0;
   if (lane <= j) {
-    const double vk = lane == j ? vj : vkj;
+    const double vk = lane == j ? vj : L.vkj;
     h[lane] = cscale(cscale(d, vk), f);
     tv = cabs2(d) * vk;
     tw = vk;
@@ -500,6 +520,90 @@ __global__ void gmres_lag_kernel(GivensState g, int j, const double* rd, const d
     g.status_it[4 * j + 2] = sqrt(w2) * f;
     const double floor2 = fmax(w2 * 1e-28, 1e-300);
     g.sscale[j + 1] = 1.0 / sqrt(fmax(rest, floor2));
+  }
+}
+// every operand loaded up front: one memory latency per launch
+__device__ __forceinline__ void lag_body(const GivensState& g, int j, const double* rd,
+                                         const double* sig2, int final_step, double eps,
+                                         double ptol, int stop_col) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const LagIn L = lag_load(g, j);
+  const double sig = *sig2;
+  const int kj = min(lane, j);
+  const double* rdp = rd ? rd : sig2;  // (final step: rd unused, any valid words of red)
+  const double2 d = make_double2(rdp[2 * kj], rdp[2 * kj + 1]);
+  const double w2 = rdp[2 * (j + 1)];
+  if (L.stopped) return;
+  lag_compute(g, j, L, d, w2, sig, final_step, eps, ptol, stop_col);
+}
+
+__global__ void gmres_lag_kernel(GivensState g, int j, const double* rd, const double* sig2,
+                                 int final_step, double eps, double ptol, int stop_col) {
+  lag_body(g, j, rd, sig2, final_step, eps, ptol, stop_col);
+}
+
+// reduce_kernel + gmres_lag_kernel in ONE launch for a single rank (no allreduce between them),
+// bit-identical to the two.  reduce_kernel sums column k with 256 threads t (rows t, t + 256,
+// ... ascending, then the pairwise tree off = 128 .. 1); here lane c of wave w (8 waves) plays
+// those threads t = w + 8 q (q < 32) for column c -- each row read coalesced across the
+// columns, 32 loads in flight -- so the tree's levels 128 .. 8 pair two of its own sums (q,
+// q + 2^l) and the last three (4, 2, 1) pair waves: wave 0's lane c finishes them from LDS.
+// The sums land in `red` and LDS; wave 0 then runs the lag step on the LDS copy, its own
+// operands requested before the partial rows (their latencies overlap).  One launch instead of
+// two per one-pass inner iteration (~5 us each at 1024^2, where an iteration is ~60 us).
+// (16 waves of 16 virtual threads each hold 128 VGPRs at most and spilled -- 10.1 / 14.1 us;
+// a first version with reduce_kernel's strided per-column reads ran 13.9 us:
+// profiles/r05/r05i_*, r05j_*, r05k_rocprof_c2_kernel_stats.csv.)
+constexpr int kLagRedWaves = 8;
+constexpr int kLagRedThreads = kLagRedWaves * kWave;
+constexpr int kLagRedQ = kT / kLagRedWaves;  // virtual threads per lane
+__global__ __launch_bounds__(kLagRedThreads) void gmres_lag_red_kernel(
+    GivensState g, int j, const double* partials, int count, int width, int cols, double* red,
+    double eps, double ptol, int stop_col) {
+  __shared__ double wsum[kLagRedWaves][kWave];
+  __shared__ double sred[kWave];
+  const int w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+  const int c = min(lane, cols - 1);
+  // the lag step's own operands (and the stop flag) requested before the partial rows
+  LagIn L;
+  if (w == 0) L = lag_load(g, j);
+  double s[kLagRedQ];
+#pragma unroll
+  for (int q = 0; q < kLagRedQ; ++q) s[q] = 0.0;
+  for (int b0 = 0; b0 < count; b0 += kT) {
+    double v[kLagRedQ];
+#pragma unroll
+    for (int q = 0; q < kLagRedQ; ++q)
+      v[q] = partials[(size_t)min(b0 + w + kLagRedWaves * q, count - 1) * width + c];
+#pragma unroll
+    for (int q = 0; q < kLagRedQ; ++q)
+      if (b0 + w + kLagRedWaves * q < count) s[q] += v[q];
+  }
+#pragma unroll
+  for (int h = kLagRedQ / 2; h > 0; h >>= 1)  // tree levels off = 128 .. 8
+#pragma unroll
+    for (int q = 0; q < h; ++q) s[q] += s[q + h];
+  wsum[w][lane] = s[0];
+  __syncthreads();
+  if (w == 0) {
+    double x[kLagRedWaves];
+#pragma unroll
+    for (int q = 0; q < kLagRedWaves; ++q) x[q] = wsum[q][lane];
+#pragma unroll
+    for (int h = kLagRedWaves / 2; h > 0; h >>= 1)  // levels 4, 2, 1
+#pragma unroll
+      for (int q = 0; q < h; ++q) x[q] += x[q + h];
+    // (the cycle stopped: reduce_kernel and gmres_lag_kernel leave red and the state alone)
+    if (lane < cols && !L.stopped) {
+      sred[lane] = x[0];
+      red[lane] = x[0];
+    }
+  }
+  __syncthreads();
+  if (w == 0 && !L.stopped) {
+    const int kj = min(lane, j);
+    lag_compute(g, j, L, make_double2(sred[2 * kj], sred[2 * kj + 1]), sred[2 * (j + 1)],
+                sred[2 * (j + 1) + 1], 0, eps, ptol, stop_col);
   }
 }
 
@@ -517,22 +621,44 @@ __global__ void gmres_start_kernel(GivensState g, const double* red, int idx_r, 
   g.status[5] = mn;
 }
 
-__global__ void gmres_solve_kernel(GivensState g, int col) {
-  if (threadIdx.x != 0) return;
+// The triangular solve, one wave, lane m holding y_m: H copied to LDS by the whole wave (one
+// memory latency), the Smith factors of every diagonal formed at once, then the column-oriented
+// back-substitution -- y_k /= R_kk by lane k, broadcast, lanes m < k take y_m -= y_k R_mk -- the
+// same operations in the same order per y_m as the serial form (lane 0 alone, global operands:
+// a dependent round trip per operand, both divisions of every step on the chain).
+// The column comes from the device (ctl[1], the last one the cycle executed; the host learns it
+// only from the cycle's report, read after the residual): with `merged`, a cycle that reached
+// its last column `stop_col` already had its x update from cycle_end_kernel + cycle_finish_kernel
+// -- the solve then only raises ctl[2], which skips xupdate_kernel.
+__global__ void gmres_solve_kernel(GivensState g, int stop_col, int merged) {
+  __shared__ double2 sH[(kMaxProj + 1) * (kMaxProj + 2)];
+  const int col = min(max(g.ctrl[1], 0), stop_col);
+  const bool skip = merged && col == stop_col;
+  if (threadIdx.x == 0) g.ctrl[2] = skip;
+  if (skip) return;
   const int R1 = g.restart + 1;
-  auto H = [&](int c, int k) -> double2& { return g.H[(size_t)c * R1 + k]; };
-  if (H(col, col).x == 0.0 && H(col, col).y == 0.0) g.S[col] = make_double2(0.0, 0.0);
-  double2 y[kMaxProj];
-  for (int k = 0; k <= col; ++k) y[k] = g.S[k];
-  for (int k = col; k > 0; --k) {
-    if (y[k].x != 0.0 || y[k].y != 0.0) {
-      y[k] = cdiv_smith(y[k], H(k, k));
-      const double2 t = y[k];
-      for (int m = 0; m < k; ++m) y[m] = csub(y[m], cmul(t, H(k, m)));
+  const int lane = threadIdx.x, me = min(lane, col);
+  for (int e = lane; e < (col + 1) * R1; e += kWave) sH[e] = g.H[e];
+  double2 y = g.S[me];
+  const double sv = g.vscale[me];
+  __syncthreads();
+  auto H = [&](int c, int k) { return sH[c * R1 + k]; };
+  const double2 hcc = H(col, col);
+  if (hcc.x == 0.0 && hcc.y == 0.0) {
+    if (lane == 0) g.S[col] = make_double2(0.0, 0.0);
+    if (lane == col) y = make_double2(0.0, 0.0);
+  }
+  const Smith f = smith_of(H(me, me));
+  for (int k = col; k >= 0; --k) {
+    const double2 t0 = rlane2(y, k);
+    if (t0.x != 0.0 || t0.y != 0.0) {  // (uniform)
+      if (lane == k) y = smith_apply(y, f);
+      if (k == 0) break;
+      const double2 t = rlane2(y, k);
+      if (lane < k) y = csub(y, cmul(t, H(k, lane)));
     }
   }
-  if (y[0].x != 0.0 || y[0].y != 0.0) y[0] = cdiv_smith(y[0], H(0, 0));
-  for (int k = 0; k <= col; ++k) g.ycoef[k] = cscale(y[k], g.vscale[k]);
+  if (lane <= col) g.ycoef[lane] = cscale(y, sv);
 }
 
 // Krylov tuning knobs (hh_tune_krylov): non-temporal basis loads, streaming grid size;
@@ -598,11 +724,13 @@ void up_launch(const double2* V, size_t ldv, const double* raw, const double* sc
 }
 template <int K>
 void xu_launch(const double2* V, size_t ldv, const double2* y, double2* x, size_t len, int blocks,
-               hipStream_t s) {
+               hipStream_t s, const int* ctl) {
   if (krylov_nt(len))
-    hipLaunchKernelGGL((xupdate_kernel<K, true>), dim3(blocks), dim3(kT), 0, s, V, ldv, y, x, len);
+    hipLaunchKernelGGL((xupdate_kernel<K, true>), dim3(blocks), dim3(kT), 0, s, V, ldv, y, x, len,
+                       ctl);
   else
-    hipLaunchKernelGGL((xupdate_kernel<K, false>), dim3(blocks), dim3(kT), 0, s, V, ldv, y, x, len);
+    hipLaunchKernelGGL((xupdate_kernel<K, false>), dim3(blocks), dim3(kT), 0, s, V, ldv, y, x, len,
+                       ctl);
 }
 
 template <int... Ks>
@@ -611,7 +739,8 @@ struct KTable {
                       const int*, double*, int, unsigned*);
   using UP = void (*)(const double2*, size_t, const double*, const double*, const double2*,
                       double2*, size_t, double*, int, hipStream_t, const int*, const ColumnFuse*);
-  using XU = void (*)(const double2*, size_t, const double2*, double2*, size_t, int, hipStream_t);
+  using XU = void (*)(const double2*, size_t, const double2*, double2*, size_t, int, hipStream_t,
+                     const int*);
   static constexpr MD md[] = {md_launch<Ks>...};
   static constexpr UP up[] = {up_launch<Ks>...};
   static constexpr XU xu[] = {xu_launch<Ks>...};
@@ -670,8 +799,8 @@ void launch_update_column(const double2* V, size_t ldv, int K, const double* raw
 }
 
 void launch_xupdate(const double2* V, size_t ldv, int K, const double2* y, double2* x,
-                    size_t len, int blocks, hipStream_t stream) {
-  Table::xu[K - 1](V, ldv, y, x, len, blocks, stream);
+                    size_t len, int blocks, hipStream_t stream, const int* ctl) {
+  Table::xu[K - 1](V, ldv, y, x, len, blocks, stream, ctl);
 }
 
 void launch_reduce(const double* partials, int count, int width, int cols, double* out,
@@ -703,6 +832,12 @@ void launch_gmres_column(const GivensState& g, int col, const double* red_dots,
                      red_norm, norm_partials, norm_count, eps, ptol, stop_col);
 }
 
+void launch_gmres_lag_red(const GivensState& g, int j, const double* partials, int count,
+                          int width, int cols, double* red, double eps, double ptol, int stop_col,
+                          hipStream_t stream) {
+  hipLaunchKernelGGL(gmres_lag_red_kernel, dim3(1), dim3(kLagRedThreads), 0, stream, g, j,
+                     partials, count, width, cols, red, eps, ptol, stop_col);
+}
 void launch_gmres_lag(const GivensState& g, int j, const double* red_dots, const double* sig2,
                       bool final_step, double eps, double ptol, int stop_col, hipStream_t stream) {
   hipLaunchKernelGGL(gmres_lag_kernel, dim3(1), dim3(kWave), 0, stream, g, j, red_dots, sig2,
@@ -714,8 +849,9 @@ void launch_gmres_start(const GivensState& g, const double* red, int idx_r, int 
   hipLaunchKernelGGL(gmres_start_kernel, dim3(1), dim3(kWave), 0, stream, g, red, idx_r, idx_m);
 }
 
-void launch_gmres_solve(const GivensState& g, int col, hipStream_t stream) {
-  hipLaunchKernelGGL(gmres_solve_kernel, dim3(1), dim3(kWave), 0, stream, g, col);
+void launch_gmres_solve(const GivensState& g, int stop_col, bool merged, hipStream_t stream) {
+  hipLaunchKernelGGL(gmres_solve_kernel, dim3(1), dim3(kWave), 0, stream, g, stop_col,
+                     (int)merged);
 }
 
 }  // namespace hh

@@ -2438,15 +2438,23 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       for (int c2 = 0; c2 < stop_col; ++c2) {
         const int K = c2 + 1, K2 = K + 1;
         const int np = run_fused(op, K, Wb[c2 & 1], Wb[(c2 + 1) & 1], op->red + 16, g.sscale + K);
-        // (dots, |w|^2 and |u|^2 in one partial row: one reduce, one allreduce)
-        hipEvent_t k0 = tmark(op, s);
-        launch_reduce(op->partials, np, 2 * K2 + 2, 2 * K2 + 2, op->red + 16, s, stp);
-        tspan(op, HH_SPAN_MULTIDOT, k0, tmark(op, s));
-        allreduce_sum_dev(op, op->red + 16, 2 * K2 + 2);
-        hipEvent_t k1 = tmark(op, s);
-        launch_gmres_lag(g, c2 + 1, op->red + 16, op->red + 16 + 2 * K2 + 1, false, eps, ptol,
-                         stop_col, s);
-        tspan(op, HH_SPAN_COLUMN, k1, tmark(op, s));
+        // (dots, |w|^2 and |u|^2 in one partial row: one reduce, one allreduce; on one rank the
+        // reduce and the column in one launch)
+        if (c->world == 1 && 2 * K2 + 2 <= 64 && lag_red_merge()) {
+          hipEvent_t k1 = tmark(op, s);
+          launch_gmres_lag_red(g, c2 + 1, op->partials, np, 2 * K2 + 2, 2 * K2 + 2, op->red + 16,
+                               eps, ptol, stop_col, s);
+          tspan(op, HH_SPAN_COLUMN, k1, tmark(op, s));
+        } else {
+          hipEvent_t k0 = tmark(op, s);
+          launch_reduce(op->partials, np, 2 * K2 + 2, 2 * K2 + 2, op->red + 16, s, stp);
+          tspan(op, HH_SPAN_MULTIDOT, k0, tmark(op, s));
+          allreduce_sum_dev(op, op->red + 16, 2 * K2 + 2);
+          hipEvent_t k1 = tmark(op, s);
+          launch_gmres_lag(g, c2 + 1, op->red + 16, op->red + 16 + 2 * K2 + 1, false, eps, ptol,
+                           stop_col, s);
+          tspan(op, HH_SPAN_COLUMN, k1, tmark(op, s));
+        }
         HIPC(hipGetLastError());
       }
       {  // the last column's update and the norm that completes it
@@ -2563,10 +2571,19 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       HIPC(hipGetLastError());
     }
     op->stop_flag = nullptr;  // (the SolveScope also clears it if anything above throws)
-    // one sync: per-iteration statuses + the last column executed
+    // The cycle's report (per-iteration statuses + the last column executed) is copied behind
+    // it, and the x update of the columns it executed is queued without waiting for it: the
+    // merged end's finish or the triangular solve + x update, chosen on the device from that
+    // last column (cycle_finish_kernel, gmres_solve_kernel, xupdate_kernel's ctl).  The host's
+    // one sync per cycle is the residual norm's, below; the report is read after it.
     HIPC(hipMemcpyAsync(op->status_h, op->red, kRedReport * sizeof(double), hipMemcpyDeviceToHost,
                         s));
-    HIPC(hipStreamSynchronize(s));
+    if (merge_end)
+      launch_cycle_finish(g, stop_col, V + (size_t)(stop_col + 1) * ldv, x, L, blocks, s);
+    launch_gmres_solve(g, stop_col, merge_end, s);
+    launch_xupdate(V, ldv, stop_col + 1, g.ycoef, x, L, blocks, s, g.ctrl);
+    residual(op, b, x, V, 4);  // r = b - A x; V[0] = M r for the next cycle
+    read_dev(op, op->red + 4, st, 1);
     const double* sth = op->status_h + kRedStatus;
     int ctl[2];
     std::memcpy(ctl, op->status_h + kRedCtrl, 2 * sizeof(int));
@@ -2586,15 +2603,6 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     presid = sth[4 * col];
     breakdown = sth[4 * col + 1] != 0.0;
     op->stats.restarts++;
-    if (merge_end && col == stop_col) {
-      // (the cycle reached its last column, so cycle_end ran: x already holds x + V a)
-      launch_cycle_finish(g, col, V + (size_t)(col + 1) * ldv, x, L, blocks, s);
-    } else {
-      launch_gmres_solve(g, col, s);
-      launch_xupdate(V, ldv, col + 1, g.ycoef, x, L, blocks, s);
-    }
-    residual(op, b, x, V, 4);  // r = b - A x; V[0] = M r for the next cycle
-    read_dev(op, op->red + 4, st, 1);
     check_sweep_chain(op);  // (the M r of the last cycle is never read by a cycle report)
     rnorm = std::sqrt(st[0]);
     if (legacy && inner == maxiter) {

@@ -350,6 +350,27 @@ def test_fused_cycle_end_merge_matches_solve_and_xupdate(tmp_path, n, kind, rest
     assert relerr(a["x"], b["x"]) < 1e-11
 
 
+
+@pytest.mark.parametrize("n,kind,restart,K", [(300, "c1", 20, 45), (1100, "marmousi", 7, 22),
+                                              (1024, "c1", 21, 25)])
+def test_fused_lag_reduce_merge_bit_identical(tmp_path, n, kind, restart, K):
+    """One rank: the partial-row reduce and the lag step in one launch (krylov.hip
+    gmres_lag_red_kernel, reduce_kernel's 256-thread summation order played by 16 waves) against
+    the two launches (HH_LAG_RED=0): history and x bit for bit."""
+    import subprocess
+    import sys
+    res = []
+    for merge in ("1", "0"):
+        out = tmp_path / f"l{merge}.npz"
+        env = dict(os.environ, HH_LAG_RED=merge)
+        subprocess.run([sys.executable, "-c", _CHILD, ROOT, str(n), kind, str(restart), str(K),
+                        str(out)], env=env, check=True, timeout=240)
+        res.append(np.load(out))
+    a, b = res
+    assert int(a["info"]) == int(b["info"]) and len(a["hist"]) == len(b["hist"]) == K
+    assert np.array_equal(a["hist"], b["hist"])
+    assert np.array_equal(a["x"], b["x"])
+
 _SLK_CHILD = r'''
 import sys, numpy as np
 sys.path.insert(0, sys.argv[1])
