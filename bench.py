@@ -178,6 +178,8 @@ def measured_traffic(n, medium, rows, stencil=5):
     cannot be read inside the timed run, so this is the committed measurement of the same kernel
     and workload: (ratio, source), or Nones for a shape without a record."""
     kind = "const" if medium == "const" else medium
+    if os.environ.get("HH_TILE_XCD", "0") != "0":
+        return None, None  # (the records are of the default tile order)
     for db, key in ((TRAFFIC_DB, f"n{n}_rows{rows}_{kind}_s{stencil}"),
                     (TRAFFIC_DB_R03, f"n{n}_{kind}_s{stencil}" if rows == n else None)):
         path = os.path.join(ROOT, db)
@@ -367,7 +369,7 @@ FUSED_TRAFFIC_DB = "profiles/r05_pmc_fused.json"
 # the environment knobs that change the one-pass kernels' traffic: a record applies only to a run
 # with the same values (unset = the build's default)
 FUSED_KNOBS = ("HH_FUSED_ITER", "HH_FUSED_KEEP", "HH_FUSED_ROWS", "HH_BASIS_PAD", "HH_SLK",
-               "HH_SLK_ROWS", "HH_CYCLE_MERGE")
+               "HH_SLK_ROWS", "HH_CYCLE_MERGE", "HH_FUSED_ALT")
 
 
 def fused_knobs():

@@ -41,6 +41,7 @@
 #include "hh_stencil9.hpp"
 #include "hh_error.hpp"
 #include <algorithm>
+#include <cstdlib>
 
 #include <type_traits>
 
@@ -529,10 +530,22 @@ __device__ __forceinline__ void tile_do(const StencilArgs& a, const int t) {
   }
 }
 
+// a.tiles_per_xcd > 0: XCD-contiguous tile runs -- block b runs on XCD b % 8 and takes tile
+// (b % 8) tiles_per_xcd + b / 8, so each XCD sweeps its own contiguous run of tiles and a tile's
+// vertical neighbours (tiles_x apart) share its L2.  In plain order they do only when tiles_x
+// is a multiple of 8 (4096^2, 8192^2); at 5792^2 / 11584^2 (the 2- and 8-GPU weak-scaling
+// slabs) every halo row goes to another XCD's L2: 1.23-1.29x the algorithmic fetch
+// (profiles/r05/r05n_pmc_shapes.log) against 1.03x -- from the Infinity Cache: the map is the
+// slower one (tile_xcd_map).
 template <int EPI, bool CONSTC, int R, bool NT, bool NTU>
 __global__ __launch_bounds__(kStencilThreads) void tile_kernel(const StencilArgs a) {
   if (a.stop && *a.stop) return;  // queued GMRES cycle already stopped
-  tile_do<EPI, CONSTC, R, NT, NTU>(a, blockIdx.x);
+  int t = blockIdx.x;
+  if (a.tiles_per_xcd > 0) {
+    t = (blockIdx.x & 7) * a.tiles_per_xcd + (blockIdx.x >> 3);
+    if (t >= a.tiles_x * a.tiles_y) return;
+  }
+  tile_do<EPI, CONSTC, R, NT, NTU>(a, t);
 }
 
 // The same tiles from a persistent grid (a.grid_blocks blocks, as many as are resident at
@@ -836,6 +849,21 @@ int stencil_resolve_variant(int epi, int requested, int n) {
              : autov;
 }
 
+// The 5-point tile kernel's XCD-contiguous tile map (tile_kernel), HH_TILE_XCD=1; off by
+// default.  It does what it is for -- the fetch of the 5792^2 / 11584^2 slabs falls from
+// 1.23-1.29x to 1.006-1.021x the algorithmic bytes (profiles/r05/r05o_pmc_shapes_xcd.log) --
+// but every shape runs 1-6 % SLOWER (r05o_ab_xcd_*.log: 11584^2 constant medium 5.55 -> 5.21
+// TB/s): the plain order's cross-XCD halo re-reads are served by the Infinity Cache, not HBM
+// (FETCH_SIZE counts both), while eight separate per-XCD streams cost DRAM locality.
+bool tile_xcd_map(int tiles_x) {
+  static const bool on = [] {
+    const char* e = std::getenv("HH_TILE_XCD");
+    return e && e[0] == '1';
+  }();
+  (void)tiles_x;
+  return on;
+}
+
 int stencil_bands(int rows, int rows_per_block, int row_step) {
   if (row_step <= 0) row_step = rows_per_block;
   return rows <= rows_per_block ? 1 : (rows - rows_per_block + row_step - 1) / row_step + 1;
@@ -880,13 +908,16 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_
     // (padding tiles_x to a multiple of 8, which would put vertically adjacent tiles on one
     // XCD, measured 3-7 % SLOWER at n = 5792 and 11584: profiles/r01y_tune_tile_pad.log)
     a.tiles_x = (a.n + kStencilThreads - 1) / kStencilThreads;
-    const int tiles = a.tiles_x * ((rows + R - 1) / R);
+    a.tiles_y = (rows + R - 1) / R;
+    const int tiles = a.tiles_x * a.tiles_y;
     const bool pers = w >= 64 && !a.tab_r2x;  // (5-point only)
+    const bool xcd = !a.tab_r2x && !pers && tile_xcd_map(a.tiles_x);
+    a.tiles_per_xcd = xcd ? (tiles + 7) / 8 : 0;
     nblocks_out[0] = 0;
     auto go = [&](auto ke, auto kr) {
       constexpr int E = decltype(ke)::value;
       constexpr int RR = decltype(kr)::value;
-      const dim3 g(tiles), b(kStencilThreads);
+      const dim3 g(xcd ? 8 * a.tiles_per_xcd : tiles), b(kStencilThreads);
       if (pers) {  // persistent grid: every resident slot once
         static int slots = 0;
         if (slots == 0) {

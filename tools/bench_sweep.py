@@ -55,6 +55,8 @@ for n in ns:
     mem1 = device_used_bytes()
     x, y = A.vector(f.ravel()), A.vector()
     A.apply_device(x, y, _ffi.HH_APPLY_PREC)
+    A.ctx.synchronize()
+    mem2 = device_used_bytes()  # (+ the apply's workspaces and the two vectors)
     t0 = time.perf_counter()
     reps = 10 if Msw.dense or n <= 1023 else 2
     for _ in range(reps):
@@ -81,7 +83,8 @@ for n in ns:
             f"corrected-sweep GMRES {len(hist)} its info={info} in {t_solve:.3f} s")
     if mem0 is not None and mem1 is not None:
         line += (f" | device memory: operator {mem0 / 1e9:.2f} GB, + preconditioner "
-                 f"{(mem1 - mem0) / 1e9:.2f} GB = {mem1 / 1e9:.2f} GB in use after setup")
+                 f"{(mem1 - mem0) / 1e9:.2f} GB = {mem1 / 1e9:.2f} GB in use after setup, "
+                 f"{mem2 / 1e9:.2f} GB after the first apply")
     if n <= 255 and os.path.isdir(os.path.join(ROOT, "oracle")):
         from oracle import helmholtz_oracle as O
         t0 = time.perf_counter()
