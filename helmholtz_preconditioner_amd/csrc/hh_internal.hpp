@@ -90,6 +90,10 @@ struct StencilArgs {
   // nl, nl+1, and j0 is the slab's first global layer (z1 vanishes only off the grid)
   const double* invc2_halo;
   int j0;
+  // fused shifted-Laplace residual (sl_fused.hip sl2_res_kernel): in1 = b over the slab, and
+  // its two rows beyond each side (the neighbouring slab's, or zero rows off the grid)
+  const double2* in1_lo;
+  const double2* in1_hi;
 };
 
 struct PointArgs {
@@ -146,6 +150,11 @@ int stencil_bands(int rows, int rows_per_block, int row_step);  // tiles along j
 // rows per side and the extended tables (StencilArgs, fused SL fields); a.tab_r2x != nullptr
 // selects the 9-point operator.
 void launch_sl2(bool const_c, const StencilArgs& a, hipStream_t stream, int variant = -1);
+// v0 = M (b - A x) for the two-sweep shifted Laplace in one pass (5-point, one rank): a.u = x,
+// a.in1 / in1_lo / in1_hi = b, a.out0 = v0; per block |r|^2 and |M r|^2 into a.partials
+// (width kMaxNorms).  Returns the blocks launched (the partial rows written).
+int launch_sl2_res(bool const_c, const StencilArgs& a, hipStream_t stream);
+int sl2_res_blocks(int n, int rows, int rows_per_block);
 int stencil_rows_per_block(int n, int rows);
 void launch_point(int op, bool const_c, const PointArgs& a, int blocks, hipStream_t stream);
 int point_blocks(size_t len);

@@ -721,6 +721,57 @@ void norm2(hh_op* op, const double2* v, int dst) {
 }
 
 // v0 = M (b - A x); red[dst] = |b - A x|^2, red[dst+1] = |v0|^2
+// The shifted-Laplace residual v0 = M (b - A x) in one pass (sl_fused.hip sl2_res_kernel) where
+// it applies: one rank (b's rows beyond a slab are the neighbouring slab's or off the grid), the
+// 5-point operator, the two-sweep M; HH_SL_RES=0 keeps the three launches (r and z1, the second
+// sweep, |M r|^2).  v0 is bit-identical either way; the norms are summed in another order.
+bool sl_res_fused(const hh_op* op) {
+  static const bool on = [] {
+    const char* e = std::getenv("HH_SL_RES");
+    return !(e && e[0] == '0');
+  }();
+  return on && op->ctx->world == 1 && op->points == 5 && sl_fused_applies(op);
+}
+
+void run_sl2_res(hh_op* op, const double2* b, const double2* x, double2* v0, int dst) {
+  const int n = op->n;
+  const int S = (int)op->slabs.size();
+  int np = 0;
+  for (int si = 0; si < S; ++si) {
+    const Slab& s = op->slabs[si];
+    if (s.nl <= 0) continue;
+    StencilArgs a{};
+    const size_t prev_tail = si > 0 ? op->slabs[si - 1].off + (size_t)(op->slabs[si - 1].nl - 2) * n : 0;
+    const size_t next_head = si < S - 1 ? op->slabs[si + 1].off : 0;
+    a.u = x + s.off;
+    a.halo_lo = si > 0 ? x + prev_tail : op->zero_row;
+    a.halo_hi = si < S - 1 ? x + next_head : op->zero_row;
+    a.in1 = b + s.off;
+    a.in1_lo = si > 0 ? b + prev_tail : op->zero_row;
+    a.in1_hi = si < S - 1 ? b + next_head : op->zero_row;
+    a.invc2 = op->const_c ? nullptr : s.invc2;
+    a.invc2_halo = s.invc2_halo;
+    a.invc2_const = op->invc2_const;
+    a.tab_i = op->tab_i;
+    a.tab_j = s.tab_j;
+    a.j0 = s.j0;
+    a.n = n;
+    a.nl = s.nl;
+    a.row_begin = 0;
+    a.row_end = s.nl;
+    a.rows_per_block = s.rpb;
+    a.mshift = op->mshift;
+    a.damping = op->damping;
+    a.out0 = v0 + s.off;
+    a.partials = op->partials + (size_t)np * kMaxNorms;
+    REQUIRE((size_t)(np + sl2_res_blocks(n, s.nl, s.rpb)) * kMaxNorms <= op->partials_cap,
+            "partials workspace too small for the shifted-Laplace residual");
+    np += launch_sl2_res(op->const_c, a, op->ctx->stream);
+  }
+  HIPC(hipGetLastError());
+  reduce_norms(op, np, dst, 2);  // red[dst] = |r|^2, red[dst + 1] = |M r|^2
+}
+
 void residual(hh_op* op, const double2* b, const double2* x, double2* v0, int dst) {
   switch (op->pkind) {
     case HH_PREC_NONE: {
@@ -734,6 +785,10 @@ void residual(hh_op* op, const double2* b, const double2* x, double2* v0, int ds
       break;
     }
     case HH_PREC_SHIFTED_LAPLACE: {
+      if (sl_res_fused(op)) {  // one pass: v0 = M r with |r|^2 and |M r|^2
+        run_sl2_res(op, b, x, v0, dst);
+        break;
+      }
       ensure_scratch(op);
       // r must survive the sweeps: it lives in scrR, distinct from scrT/scrZ/v0.
       if (!op->scrR) op->scrR = dalloc<double2>(op->nloc);

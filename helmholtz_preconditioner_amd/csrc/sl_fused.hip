@@ -22,7 +22,9 @@
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
 #include "hh_stencil9.hpp"
+#include "hh_wave.hpp"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace hh {
@@ -50,6 +52,7 @@ struct RowTab {
 struct RowIn {
   double ic;
   double2 e;  // v at this strip's halo columns (lanes 0-31: i0-2, lanes 32-63: i0+TPB-1)
+  double2 b;  // (sl2_res_kernel) b at the lane's column
 };
 
 template <bool CONSTC, bool NTU, int TPB>
@@ -390,8 +393,12 @@ struct Sl2Lds {  // one LDS block shared by both instantiations of sl2_tile_v2
 };
 // PF: rows of prefetch distance of the v and 1/c^2 streams (1, or 2 with rings of 8 and the
 // row loop unrolled by 8): more bytes in flight per wave.
-template <bool CONSTC, bool NTU, bool EDGE, int PF>
-__device__ __forceinline__ void sl2_tile_v2(const StencilArgs& a, const int t, Sl2Lds& L) {
+// RES (sl2_res_kernel): the first sweep's input is the residual r = b - A x instead of s A v
+// (stencil.hip EPI_RES_SL's r, term for term), and acc[0] / acc[1] gather |r|^2 / |w|^2 of the
+// tile's output points.
+template <bool CONSTC, bool NTU, bool EDGE, int PF, bool RES = false>
+__device__ __forceinline__ void sl2_tile_v2(const StencilArgs& a, const int t, Sl2Lds& L,
+                                            double* acc = nullptr) {
   constexpr int RS = PF == 1 ? 4 : 8;  // ring slots: slot(row) = (row - rb + 2) % RS
   constexpr int TPB = kStencilThreads;
   constexpr int WO = TPB - 2;
@@ -437,6 +444,12 @@ __device__ __forceinline__ void sl2_tile_v2(const StencilArgs& a, const int t, S
       v.ic = a.invc2_const;
     }
     v.e = rowp(r)[ie];
+    if constexpr (RES) {
+      const double2* bp = r < 0 ? a.in1_lo + (size_t)(r + 2) * n
+                                : (r >= nl ? a.in1_hi + (size_t)(r - nl) * n
+                                           : a.in1 + (size_t)r * n);
+      v.b = bp[cc];
+    }
   };
   // PML row tables of the band (tab_j_ext rows rb-2 .. re+1) into LDS
   {
@@ -474,7 +487,8 @@ __device__ __forceinline__ void sl2_tile_v2(const StencilArgs& a, const int t, S
     Au = cfma(D, uC, Au);
     Au = cfma(E, uE, Au);
     Au = cfma(N, uN, Au);
-    T = cscale(Au, sin);
+    if constexpr (RES) T = csub(in.b, Au);
+    else T = cscale(Au, sin);
     const double inv = 1.0 / fma(Db.x, Db.x, Db.y * Db.y);  // = cdiv(T, Db), split
     const double2 q = cscale(make_double2(fma(T.x, Db.x, T.y * Db.y) * inv,
                                           fma(T.y, Db.x, -T.x * Db.y) * inv), a.damping);
@@ -556,6 +570,10 @@ __device__ __forceinline__ void sl2_tile_v2(const StencilArgs& a, const int t, S
         double2* q = a.out0 + (size_t)r * n + c;
         __builtin_nontemporal_store(w.x, &q->x);
         __builtin_nontemporal_store(w.y, &q->y);
+        if constexpr (RES) {
+          acc[0] += cabs2(TT[s0]);
+          acc[1] += cabs2(w);
+        }
       }
     });
   }
@@ -1235,6 +1253,33 @@ __global__ __launch_bounds__(TPB, (S9 && SHAPE == 4) ? 3 : 1) void sl2_kernel(co
   }
 }
 
+// v0 = M (b - A x) in one pass: sl2_tile_v2 with the residual as the first sweep's input (the
+// unfused form is EPI_RES_SL's stencil launch writing r and z1, the second sweep's stencil
+// launch reading them back and a norm pass over v0: 16 + 16 + 8 + 16 + 16 B, then 16 + 16 +
+// 8 + 16 and 16 per unknown -- here x 16 + b 16 + 1/c^2 8 + v0 16).  v0 bit-identical to the
+// unfused form; the two norms summed in another order (per block, then reduce_kernel).
+template <bool CONSTC, int PF>
+__global__ __launch_bounds__(kStencilThreads) void sl2_res_kernel(const StencilArgs a) {
+  double acc[2] = {0.0, 0.0};
+  const int L = blockIdx.x;
+  const int q = L >> 3, Q = gridDim.x >> 3;
+  const int ntiles = a.tiles_x * a.tiles_y;
+  __shared__ Sl2Lds lds;
+  for (int tt = q; tt < a.tiles_per_xcd; tt += Q) {
+    const int t = (L & 7) * a.tiles_per_xcd + tt;
+    if (t >= ntiles) break;  // uniform per block
+    const int tx = t % a.tiles_x, ty = t / a.tiles_x;
+    const int i0 = tx * (kStencilThreads - 2);
+    const int rb = a.row_begin + ty * a.row_step;
+    const int re = min(rb + a.rows_per_block, a.row_end);
+    const bool interior = i0 - 2 >= 0 && i0 + kStencilThreads - 1 < a.n && a.j0 + rb - 1 >= 0 &&
+                          a.j0 + re < a.n;
+    if (interior) sl2_tile_v2<CONSTC, false, false, PF, true>(a, t, lds, acc);
+    else sl2_tile_v2<CONSTC, false, true, PF, true>(a, t, lds, acc);
+  }
+  block_reduce_vec<2>(acc, a.partials, kMaxNorms);
+}
+
 template <int TPB, bool NTU, int SHAPE = 0, int PF = 1>
 void launch_t(bool const_c, const StencilArgs& a, int blocks, hipStream_t s) {
   const bool s9 = a.tab_r2x != nullptr;  // 9-point operator (the tables themselves are unused)
@@ -1326,6 +1371,26 @@ void launch_sl2(bool const_c, const StencilArgs& a_in, hipStream_t stream, int v
     if (ntu) launch_t<512, true>(const_c, a, blocks, stream);
     else launch_t<512, false>(const_c, a, blocks, stream);
   }
+}
+
+int sl2_res_blocks(int n, int rows, int rows_per_block) {
+  const int tiles_x = (n + kStencilThreads - 3) / (kStencilThreads - 2);
+  const int tiles = tiles_x * stencil_bands(rows, std::min(rows_per_block, kSl2MaxBand), 0);
+  return (tiles + 7) / 8 * 8;
+}
+
+int launch_sl2_res(bool const_c, const StencilArgs& a_in, hipStream_t stream) {
+  StencilArgs a = a_in;
+  const int rows = a.row_end - a.row_begin;
+  a.rows_per_block = std::min(a.rows_per_block, kSl2MaxBand);  // (the LDS row-table capacity)
+  a.row_step = a.rows_per_block;
+  a.tiles_x = (a.n + kStencilThreads - 3) / (kStencilThreads - 2);
+  a.tiles_y = stencil_bands(rows, a.rows_per_block, 0);
+  a.tiles_per_xcd = (a.tiles_x * a.tiles_y + 7) / 8;
+  const int blocks = a.tiles_per_xcd * 8;
+  if (const_c) hipLaunchKernelGGL((sl2_res_kernel<true, 2>), dim3(blocks), dim3(kStencilThreads), 0, stream, a);
+  else hipLaunchKernelGGL((sl2_res_kernel<false, 2>), dim3(blocks), dim3(kStencilThreads), 0, stream, a);
+  return blocks;
 }
 
 }  // namespace hh
