@@ -730,7 +730,8 @@ bool sl_res_fused(const hh_op* op) {
     const char* e = std::getenv("HH_SL_RES");
     return !(e && e[0] == '0');
   }();
-  return on && op->ctx->world == 1 && op->points == 5 && sl_fused_applies(op);
+  // (independent of the M A fusion switch, hh_op_set_sl_fusion: that A/B stays bit-identical)
+  return on && op->ctx->world == 1 && op->points == 5 && op->sweeps == 2 && op->sl_ext_ok;
 }
 
 void run_sl2_res(hh_op* op, const double2* b, const double2* x, double2* v0, int dst) {

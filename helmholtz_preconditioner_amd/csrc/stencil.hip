@@ -902,6 +902,10 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_
   }
   if (v >= kTileVariant && a.row_step > 0)  // spaced bands (halo rows): marching shape
     v = stencil_resolve_variant(epi, kVariantInSolve, a.n);
+  // constant medium (no 1/c^2 stream, 32 B per unknown): 6-row tiles -- the halo rows' share of
+  // the u loads falls from 6/4 to 8/6 (4096^2: 97.2 vs 97.9 us, 8192^2: 366.4 vs 381.7 us;
+  // Marmousi-like: 4096^2 118.1 vs 117.5, so 4 rows stay; profiles/r05/r05s_tune_ntu_*.log)
+  if (variant == -1 && const_c && v == kTileDefault && !a.tab_r2x) v = kTileVariant + 6;
   if (v >= kTileVariant) {  // non-marching tiles (plain / Jacobi 5-point apply, tile_kernel)
     const int w = v - kTileVariant, R = w % 16;
     const bool ntu = (w / 16) % 2 == 1 && w < 64, nt = w < 32 || w >= 64;
