@@ -1,0 +1,6 @@
+set -u
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r05x; mkdir -p $O
+fatal() { case $1 in 124|137|134|139) echo "FATAL rc=$1 in $2"; exit $1;; esac; }
+# run-to-run spread on one box, the final tree: 5 runs each of config 2 and the default (config 3) line
+bash tools/ab_env.sh 5 "HH_NOTHING=0" -- python bench.py --config 2 --no-cpu-baseline > $O/spread_c2.log 2>&1; rc=$?; echo "c2 rc=$rc"; cat $O/spread_c2.log; fatal $rc c2
+bash tools/ab_env.sh 5 "HH_NOTHING=0" -- python bench.py --no-cpu-baseline --const-steps 0 > $O/spread_c3.log 2>&1; rc=$?; echo "c3 rc=$rc"; cat $O/spread_c3.log; fatal $rc c3
