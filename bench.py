@@ -329,16 +329,26 @@ def make_precond(H, A, kind, sweeps):
 
 
 def timed_gmres(H, A, ctx, f_host, args, iters, wd=None):
-    """Warm-up (one full restart cycle: first allreduces, and tens of ms of load so the clocks
-    have ramped), then `iters` timed legacy-counted inner iterations: (iterations, wall s max
-    over ranks, history)."""
+    """Warm-up (full restart cycles, at least 0.1 s of them: first allreduces, and enough load
+    that the clocks have ramped), then `iters` timed legacy-counted inner iterations:
+    (iterations, wall s max over ranks, history)."""
     f = A.vector(f_host)
     M = make_precond(H, A, args.precond, args.sl_sweeps)
     if wd:
         wd.phase("gmres warm-up (first restart cycle, first in-solve allreduces)", 180)
-    H.gmres(A, f, rtol=1e-14, restart=args.restart, maxiter=max(2, args.restart), M=M,
-            callback=lambda r: None, callback_type="legacy")
-    ctx.barrier()
+    # one full restart cycle, repeated until >= 0.1 s of warm-up (a cycle of a small grid is ~1
+    # ms: the clocks would still be ramping in the timed solve -- config 2's first run read 10 %
+    # low, profiles/r05/r05x_spread_c2_5runs.log); the repeat count from the slowest rank, so
+    # every rank runs the same collectives
+    def warm():
+        t = time.perf_counter()
+        H.gmres(A, f, rtol=1e-14, restart=args.restart, maxiter=max(2, args.restart), M=M,
+                callback=lambda r: None, callback_type="legacy")
+        ctx.barrier()
+        return float(ctx.allreduce_max([time.perf_counter() - t])[0])
+    dt = warm()
+    for _ in range(min(20, max(0, int(0.1 / max(dt, 1e-6))))):
+        warm()
     if wd:
         wd.phase("timed gmres", 120 + 0.5 * iters)
     t0 = time.perf_counter()
