@@ -197,6 +197,8 @@ struct hh_op {
   double2* scrT = nullptr;
   double2* scrZ = nullptr;
   double2* scrR = nullptr;
+  double2* res_bh_lo = nullptr;  // b's two rows beyond the rank's slab, per side (run_sl2_res)
+  double2* res_bh_hi = nullptr;
   // GMRES workspace
   double2* V = nullptr;
   int V_cols = 0;
@@ -722,34 +724,61 @@ void norm2(hh_op* op, const double2* v, int dst) {
 
 // v0 = M (b - A x); red[dst] = |b - A x|^2, red[dst+1] = |v0|^2
 // The shifted-Laplace residual v0 = M (b - A x) in one pass (sl_fused.hip sl2_res_kernel) where
-// it applies: one rank (b's rows beyond a slab are the neighbouring slab's or off the grid), the
-// 5-point operator, the two-sweep M; HH_SL_RES=0 keeps the three launches (r and z1, the second
-// sweep, |M r|^2).  v0 is bit-identical either way; the norms are summed in another order.
+// it applies: the 5-point operator, the two-sweep M with the medium known two layers beyond
+// every slab (as for the fused M A, run_sl2); HH_SL_RES=0 keeps the three launches (r and z1,
+// the second sweep, |M r|^2).  v0 is bit-identical either way; the norms are summed in another
+// order.  Independent of the M A fusion switch (hh_op_set_sl_fusion: that A/B stays
+// bit-identical).
 bool sl_res_fused(const hh_op* op) {
   static const bool on = [] {
     const char* e = std::getenv("HH_SL_RES");
     return !(e && e[0] == '0');
   }();
-  // (independent of the M A fusion switch, hh_op_set_sl_fusion: that A/B stays bit-identical)
-  return on && op->ctx->world == 1 && op->points == 5 && op->sweeps == 2 && op->sl_ext_ok;
+  return on && op->points == 5 && op->sweeps == 2 && op->sl_ext_ok;
 }
 
+// run_sl2's structure: a band reads x AND b two rows beyond itself -- in place from a
+// neighbouring slab of the rank, from the two-row halo buffers across ranks (b's exchanged
+// beside x's, every call: b may change between solves), zero rows off the grid; the rows next
+// to a cross-rank boundary run on the halo stream after the exchange.
 void run_sl2_res(hh_op* op, const double2* b, const double2* x, double2* v0, int dst) {
+  hh_ctx* c = op->ctx;
   const int n = op->n;
   const int S = (int)op->slabs.size();
+  const bool lo_x = c->world > 1 && c->rank > 0;
+  const bool hi_x = c->world > 1 && c->rank < c->world - 1;
+  const Slab& s0 = op->slabs[0];
+  const Slab& sl = op->slabs[S - 1];
+  if (lo_x || hi_x) {
+    const size_t two = 2 * (size_t)n;
+    if (!op->res_bh_lo) {
+      op->res_bh_lo = dalloc<double2>(two);
+      op->res_bh_hi = dalloc<double2>(two);
+      HIPC(hipMemsetAsync(op->res_bh_lo, 0, two * sizeof(double2), c->stream));
+      HIPC(hipMemsetAsync(op->res_bh_hi, 0, two * sizeof(double2), c->stream));
+    }
+    const size_t bytes = two * sizeof(double2);
+    c->comm->halo(lo_x ? b + s0.off : nullptr, lo_x ? op->res_bh_lo : nullptr,
+                  hi_x ? b + sl.off + (size_t)(sl.nl - 2) * n : nullptr,
+                  hi_x ? op->res_bh_hi : nullptr, bytes, c->stream, c->cstream, c->ev_in);
+    c->comm->halo(lo_x ? x + s0.off : nullptr, lo_x ? s0.halo2_lo : nullptr,
+                  hi_x ? x + sl.off + (size_t)(sl.nl - 2) * n : nullptr,
+                  hi_x ? sl.halo2_hi : nullptr, bytes, c->stream, c->cstream, c->ev_in);
+  }
   int np = 0;
-  for (int si = 0; si < S; ++si) {
+  auto launch_rows = [&](int si, int r0, int r1, int rpb, hipStream_t st) {
+    if (r1 <= r0) return;
     const Slab& s = op->slabs[si];
-    if (s.nl <= 0) continue;
-    StencilArgs a{};
-    const size_t prev_tail = si > 0 ? op->slabs[si - 1].off + (size_t)(op->slabs[si - 1].nl - 2) * n : 0;
+    const size_t prev_tail =
+        si > 0 ? op->slabs[si - 1].off + (size_t)(op->slabs[si - 1].nl - 2) * n : 0;
     const size_t next_head = si < S - 1 ? op->slabs[si + 1].off : 0;
+    StencilArgs a{};
     a.u = x + s.off;
-    a.halo_lo = si > 0 ? x + prev_tail : op->zero_row;
-    a.halo_hi = si < S - 1 ? x + next_head : op->zero_row;
+    a.halo_lo = si > 0 ? x + prev_tail : (lo_x ? s.halo2_lo : op->zero_row);
+    a.halo_hi = si < S - 1 ? x + next_head : (hi_x ? s.halo2_hi : op->zero_row);
     a.in1 = b + s.off;
-    a.in1_lo = si > 0 ? b + prev_tail : op->zero_row;
-    a.in1_hi = si < S - 1 ? b + next_head : op->zero_row;
+    a.in1_lo = si > 0 ? b + prev_tail : (lo_x ? op->res_bh_lo : op->zero_row);
+    a.in1_hi = si < S - 1 ? b + next_head : (hi_x ? op->res_bh_hi : op->zero_row);
     a.invc2 = op->const_c ? nullptr : s.invc2;
     a.invc2_halo = s.invc2_halo;
     a.invc2_const = op->invc2_const;
@@ -758,16 +787,35 @@ void run_sl2_res(hh_op* op, const double2* b, const double2* x, double2* v0, int
     a.j0 = s.j0;
     a.n = n;
     a.nl = s.nl;
-    a.row_begin = 0;
-    a.row_end = s.nl;
-    a.rows_per_block = s.rpb;
+    a.row_begin = r0;
+    a.row_end = r1;
+    a.rows_per_block = rpb;
     a.mshift = op->mshift;
     a.damping = op->damping;
     a.out0 = v0 + s.off;
     a.partials = op->partials + (size_t)np * kMaxNorms;
-    REQUIRE((size_t)(np + sl2_res_blocks(n, s.nl, s.rpb)) * kMaxNorms <= op->partials_cap,
+    REQUIRE((size_t)(np + sl2_res_blocks(n, r1 - r0, rpb)) * kMaxNorms <= op->partials_cap,
             "partials workspace too small for the shifted-Laplace residual");
-    np += launch_sl2_res(op->const_c, a, op->ctx->stream);
+    np += launch_sl2_res(op->const_c, a, st);
+  };
+  // interior rows (no cross-rank halo needed) first
+  for (int si = 0; si < S; ++si) {
+    const Slab& s = op->slabs[si];
+    const int r0 = (si == 0 && lo_x) ? std::min(2, s.nl) : 0;
+    const int r1 = (si == S - 1 && hi_x) ? std::max(r0, s.nl - 2) : s.nl;
+    launch_rows(si, r0, r1, s.rpb, c->stream);
+  }
+  if (lo_x || hi_x) {
+    // the two rows next to each cross-rank boundary, on the halo stream behind the exchange
+    hipStream_t hs = c->cstream;
+    if (S == 1 && lo_x && hi_x && s0.nl < 4) {
+      launch_rows(0, 0, s0.nl, s0.nl, hs);  // (no interior rows)
+    } else {
+      if (lo_x) launch_rows(0, 0, std::min(2, s0.nl), 2, hs);
+      if (hi_x) launch_rows(S - 1, std::max(0, sl.nl - 2), sl.nl, 2, hs);
+    }
+    HIPC(hipEventRecord(c->ev_halo, hs));
+    HIPC(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
   }
   HIPC(hipGetLastError());
   reduce_norms(op, np, dst, 2);  // red[dst] = |r|^2, red[dst + 1] = |M r|^2
@@ -1370,6 +1418,8 @@ static void op_release(hh_op* op) {
   dfree(op->scrT);
   dfree(op->scrZ);
   dfree(op->scrR);
+  dfree(op->res_bh_lo);
+  dfree(op->res_bh_hi);
   dfree(op->V);
   dfree(op->gbuf);
   dfree(op->npart);
