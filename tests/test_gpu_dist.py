@@ -223,12 +223,17 @@ def test_bench_two_ranks_rehearsal(tmp_path, transport):
 
 def test_bench_stalled_rank_exits_with_the_phase_named(tmp_path):
     """A rank that stalls (simulated: HH_BENCH_STALL makes rank 1 hang when its first applies
-    start) must end the job with a non-zero status and the stalled phase named, not hang."""
+    start) must end the job with a non-zero status and the stalled phase named, not hang.  The
+    stalled rank and the rank waiting for it in the first halo exchange enter the phase together
+    under the same bound, so either watchdog may fire first (rank 0's did once, in the final
+    round-5 suite): the phase must be named by one of them."""
+    import re
     out = _torchrun_bench(tmp_path, 2, BENCH_SMALL,
                           {"HH_TRANSPORT": "shm", "HH_WATCHDOG_SCALE": "0.1",
                            "HH_BENCH_STALL": "1:first applies"}, timeout=180)
     assert out.returncode != 0
-    assert "[bench watchdog] rank 1: phase 'first applies" in out.stderr, out.stderr[-3000:]
+    assert re.search(r"\[bench watchdog\] rank [01]: phase 'first applies", out.stderr), \
+        out.stderr[-3000:]
 
 
 @pytest.mark.parametrize("world", [2, 3])
