@@ -86,14 +86,23 @@ __device__ __forceinline__ Band band_of(const FusedArgs& a) {
 
 // u_K at row r (uniform), column col, given the value formed from the (clamped) row: rows inside
 // [rlo, rhi) are formed from memory; the others are zero (FROW_ZERO) or the neighbour rank's
-// received rows (FROW_HALO; H halo rows per side)
+// received rows (FROW_HALO; H halo rows per side: rows -H .. -1 and nl .. nl+H-1).
+// A march also asks for rows just beyond those (the shifted-Laplace pass's edge waves form u_K
+// one row behind the band's first ring row: row -3 in a band starting at row 0).  Those values
+// feed only rows the pass never outputs, and there is no received row to read: they are zero.
+// (Until round 6 row -3 was read at halo_lo - n -- one row BEFORE the receive buffer.  Where
+// that address was mapped by another allocation the value was discarded unnoticed; under
+// RCCL's allocation layout at 11584^2 / 8 ranks it was unmapped and every rank faulted in the
+// first pass's boundary rows.  DESIGN 4, tests/test_gpu_dist.py guarded-halo tests.)
 template <int H>
 __device__ __forceinline__ double2 row_value(const FusedArgs& a, int rlo, int rhi, int r, int col,
                                              double2 formed) {
   if (r >= rlo && r < rhi) return formed;
   if (r < 0)
-    return a.lo_mode == FROW_HALO ? a.halo_lo[(size_t)(r + H) * a.n + col] : make_double2(0.0, 0.0);
-  return a.hi_mode == FROW_HALO ? a.halo_hi[(size_t)(r - a.nl) * a.n + col] : make_double2(0.0, 0.0);
+    return (a.lo_mode == FROW_HALO && r >= -H) ? a.halo_lo[(size_t)(r + H) * a.n + col]
+                                               : make_double2(0.0, 0.0);
+  return (a.hi_mode == FROW_HALO && r < a.nl + H) ? a.halo_hi[(size_t)(r - a.nl) * a.n + col]
+                                                  : make_double2(0.0, 0.0);
 }
 
 // the update coefficients c_k = raw_k s_k^2 (update_kernel's expression), k < K, into LDS

@@ -261,6 +261,7 @@ struct FusedArgs {
 // rocprofiler-sdk has finalised (tools/exit_probe.py), so the grid-wide sweeps and
 // the small-grid cycle then launch plainly (their waits are bounded either way); logged once.
 bool under_profiler();
+int check_halo_level();  // HH_CHECK_HALO (runtime.cpp check_site)
 constexpr int kFusedMaxK = 20;  // K <= this (restart <= kFusedMaxK + 1)
 // basis vectors whose projection re-read is served from the pass's own LDS copy (HH_FUSED_KEEP:
 // 0 = every re-read from the memory system, for A/B)

@@ -40,8 +40,77 @@ static T* dalloc(size_t count) {
   return static_cast<T*>(p);
 }
 
+// Guarded allocations (HH_GUARD_HALO=1, diagnostic): each cross-rank halo receive buffer gets
+// its own reserved address range, [unmapped granule][mapped granules][unmapped granule], and
+// sits against the guard on the side a stray read would cross: the rows BELOW the slab (rows
+// -H .. -1) start where the mapping starts, so a read of row -H-1 faults; the rows ABOVE it
+// (nl .. nl+H-1) end where the mapping ends (`at_end`), so a read of row nl+H faults.  A kernel
+// that reads one row beyond a received halo then faults at that access on every transport and
+// grid size, instead of only where the allocator happened to leave the neighbouring address
+// unmapped (the round-5 RCCL fault at 11584^2 / 8 ranks: DESIGN 4).
+namespace {
+struct GuardMap {
+  char* va;        // reserved range: [guard][mapped][guard]
+  size_t total;    // reserved bytes
+  size_t mapped;   // mapped bytes (a multiple of the granule)
+  hipMemGenericAllocationHandle_t h;
+};
+std::vector<std::pair<void*, GuardMap>>& guard_registry() {
+  static std::vector<std::pair<void*, GuardMap>> r;
+  return r;
+}
+}  // namespace
+
+bool guard_halo() {
+  static const bool on = [] {
+    const char* e = std::getenv("HH_GUARD_HALO");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+template <class T>
+static T* dalloc_guarded(size_t count, int device, bool at_end) {
+  if (!guard_halo()) return dalloc<T>(count);
+  const size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+  hipMemAllocationProp prop{};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = device;
+  size_t gran = 0;
+  HIPC(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum));
+  GuardMap g{};
+  g.mapped = (bytes + gran - 1) / gran * gran;
+  g.total = g.mapped + 2 * gran;
+  void* va = nullptr;
+  HIPC(hipMemAddressReserve(&va, g.total, gran, nullptr, 0));
+  g.va = static_cast<char*>(va);
+  HIPC(hipMemCreate(&g.h, g.mapped, &prop, 0));
+  HIPC(hipMemMap(g.va + gran, g.mapped, 0, g.h, 0));
+  hipMemAccessDesc acc{};
+  acc.location = prop.location;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  HIPC(hipMemSetAccess(g.va + gran, g.mapped, &acc, 1));
+  char* p = g.va + gran + (at_end ? g.mapped - bytes : 0);
+  guard_registry().push_back({p, g});
+  return reinterpret_cast<T*>(p);
+}
+
 static void dfree(void* p) {
-  if (p) (void)hipFree(p);
+  if (!p) return;
+  auto& reg = guard_registry();
+  for (size_t k = 0; k < reg.size(); ++k) {
+    if (reg[k].first != p) continue;
+    const GuardMap g = reg[k].second;
+    reg.erase(reg.begin() + (ptrdiff_t)k);
+    const size_t gran = (g.total - g.mapped) / 2;
+    (void)hipDeviceSynchronize();
+    (void)hipMemUnmap(g.va + gran, g.mapped);
+    (void)hipMemRelease(g.h);
+    (void)hipMemAddressFree(g.va, g.total);
+    return;
+  }
+  (void)hipFree(p);
 }
 
 // --------------------------------------------------------------- PML profiles
@@ -62,6 +131,16 @@ static cd s2(double x, double C, double eta, cd om) {
   return 1.0 / (1.0 + cd(0, 1) * sigma2(x, C, eta) / om);
 }
 static double2 d2(cd z) { return make_double2(z.real(), z.imag()); }
+
+// HH_CHECK_HALO: 0 (default) off, 1 synchronise + attribute at every multi-rank site
+// (runtime.cpp check_site), 2 also trace each site
+int check_halo_level() {
+  static const int lvl = [] {
+    const char* e = std::getenv("HH_CHECK_HALO");
+    return e ? std::atoi(e) : 0;
+  }();
+  return lvl;
+}
 
 bool under_profiler() {
   static const bool on = [] {
@@ -294,12 +373,40 @@ void tspan(hh_op* op, int cat, hipEvent_t a, hipEvent_t b, bool clamp = false) {
   if (op->timer.on) op->timer.span(cat, a, b, clamp);
 }
 
+// HH_CHECK_HALO (diagnostic, off by default): after every halo exchange, launch group and
+// collective of the multi-rank paths, synchronise the stream it was queued on and attribute a
+// device fault to that site (rank, site, running check number) instead of to the next host sync
+// far behind it.  1: check; 2: also trace every site to stderr.  The streams are serialised by
+// it, so it also tells a hazard between the halo and compute streams (passes when checked) from
+// a fault of one launch (reported at its own site).
+void check_site(const hh_ctx* c, const char* site, hipStream_t s) {
+  const int lvl = check_halo_level();
+  if (lvl == 0) return;
+  static thread_local long count = 0;
+  ++count;
+  const hipError_t e = hipStreamSynchronize(s);
+  const char* sname = s == c->cstream ? "halo" : "compute";
+  if (e != hipSuccess) {
+    std::fprintf(stderr, "[HH_CHECK_HALO] rank %d/%d: FAULT at %s (check #%ld, %s stream): %s\n",
+                 c->rank, c->world, site, count, sname, hipGetErrorString(e));
+    std::fflush(stderr);
+    fail(HH_ERR_HIP, "[HH_CHECK_HALO] rank %d: %s (check #%ld, %s stream) -> %s", c->rank, site,
+         count, sname, hipGetErrorString(e));
+  }
+  if (lvl >= 2) {
+    std::fprintf(stderr, "[HH_CHECK_HALO] rank %d: ok %s (#%ld, %s)\n", c->rank, site, count, sname);
+    std::fflush(stderr);
+  }
+}
+
 void allreduce_sum_dev(hh_op* op, double* d, int count) {
   hh_ctx* c = op->ctx;
   if (c->world > 1) {
+    check_site(c, "before allreduce", c->stream);
     hipEvent_t a = tmark(op, c->stream);
     c->comm->allreduce(d, count, false, c->stream);
     tspan(op, HH_SPAN_ALLREDUCE, a, tmark(op, c->stream));
+    check_site(c, "allreduce (RCCL kernel)", c->stream);
   }
 }
 
@@ -317,12 +424,14 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
     const Slab& s0 = op->slabs[0];
     const Slab& sl = op->slabs[S - 1];
     t_ready = tmark(op, c->stream);  // (the input is complete: the exchange may start)
+    check_site(c, "stencil: work before the exchange", c->stream);
     c->comm->halo(lo_x ? in + s0.off : nullptr, lo_x ? s0.halo_lo_buf : nullptr,
                   hi_x ? in + sl.off + (size_t)(sl.nl - 1) * n : nullptr,
                   hi_x ? sl.halo_hi_buf : nullptr, 2 * sizeof(double) * (size_t)n, c->stream,
                   c->cstream, c->ev_in);
     t_halo = tmark(op, c->cstream);
     tspan(op, HH_SPAN_HALO, t_ready, t_halo);
+    check_site(c, "stencil: one-row halo exchange", c->cstream);
   }
 
   auto make_args = [&](int si) {
@@ -387,6 +496,7 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
   }
   t_int1 = tmark(op, c->stream);
   tspan(op, HH_SPAN_INTERIOR, t_int0, t_int1);
+  if (lo_x || hi_x) check_site(c, "stencil: interior rows", c->stream);
   if (lo_x || hi_x) {
     // The boundary rows run on the halo stream, right behind the exchange (which it ordered
     // after everything the compute stream had queued), concurrently with the interior launch;
@@ -403,6 +513,7 @@ int run_stencil(hh_op* op, int epi, const double2* in, const double* in_scale,
       if (lo_x) launch_rows(0, 0, 1, 1, 0, hs);
       if (hi_x) launch_rows(S - 1, sl.nl - 1, sl.nl, 1, 0, hs);
     }
+    check_site(c, "stencil: boundary rows", hs);
     hipEvent_t t_bnd = tmark(op, hs);
     tspan(op, HH_SPAN_BOUNDARY, t_halo, t_bnd);
     tspan(op, HH_SPAN_HALO_WAIT, t_int1, t_bnd, true);  // compute stream idle behind the halo
@@ -433,12 +544,14 @@ void run_sl2(hh_op* op, const double2* v, const double* vs, double2* out) {
     const Slab& s0 = op->slabs[0];
     const Slab& sl = op->slabs[S - 1];
     hipEvent_t t_ready = tmark(op, c->stream);
+    check_site(c, "sl2 (fused M A): work before the exchange", c->stream);
     c->comm->halo(lo_x ? v + s0.off : nullptr, lo_x ? s0.halo2_lo : nullptr,
                   hi_x ? v + sl.off + (size_t)(sl.nl - 2) * n : nullptr,
                   hi_x ? sl.halo2_hi : nullptr, 2 * 2 * sizeof(double) * (size_t)n, c->stream,
                   c->cstream, c->ev_in);
     t_halo = tmark(op, c->cstream);
     tspan(op, HH_SPAN_HALO, t_ready, t_halo);
+    check_site(c, "sl2 (fused M A): two-row halo exchange", c->cstream);
   }
   auto launch_rows = [&](int si, int r0, int r1, int rpb, int step, hipStream_t st) {
     if (r1 <= r0) return;
@@ -481,6 +594,7 @@ void run_sl2(hh_op* op, const double2* v, const double* vs, double2* out) {
   }
   hipEvent_t t_int1 = tmark(op, c->stream);
   tspan(op, HH_SPAN_INTERIOR, t_int0, t_int1);
+  if (lo_x || hi_x) check_site(c, "sl2 (fused M A): interior rows", c->stream);
   if (lo_x || hi_x) {
     // the two rows next to each cross-rank boundary, on the halo stream behind the exchange
     hipStream_t hs = c->cstream;
@@ -493,6 +607,7 @@ void run_sl2(hh_op* op, const double2* v, const double* vs, double2* out) {
       if (lo_x) launch_rows(0, 0, std::min(2, s0.nl), 2, 0, hs);
       if (hi_x) launch_rows(S - 1, std::max(0, sl.nl - 2), sl.nl, 2, 0, hs);
     }
+    check_site(c, "sl2 (fused M A): boundary rows", hs);
     hipEvent_t t_bnd = tmark(op, hs);
     tspan(op, HH_SPAN_BOUNDARY, t_halo, t_bnd);
     tspan(op, HH_SPAN_HALO_WAIT, t_int1, t_bnd, true);
@@ -537,6 +652,7 @@ int run_point(hh_op* op, int pt, const double2* in0, double2* out0, bool shifted
 // op->red[dst..dst+cols), then allreduce across ranks
 void reduce_norms(hh_op* op, int nparts, int dst, int cols) {
   launch_reduce(op->partials, nparts, kMaxNorms, cols, op->red + dst, op->ctx->stream);
+  check_site(op->ctx, "norm reduce", op->ctx->stream);
   allreduce_sum_dev(op, op->red + dst, cols);
 }
 
@@ -752,18 +868,21 @@ void run_sl2_res(hh_op* op, const double2* b, const double2* x, double2* v0, int
   if (lo_x || hi_x) {
     const size_t two = 2 * (size_t)n;
     if (!op->res_bh_lo) {
-      op->res_bh_lo = dalloc<double2>(two);
-      op->res_bh_hi = dalloc<double2>(two);
+      op->res_bh_lo = dalloc_guarded<double2>(two, c->device, false);
+      op->res_bh_hi = dalloc_guarded<double2>(two, c->device, true);
       HIPC(hipMemsetAsync(op->res_bh_lo, 0, two * sizeof(double2), c->stream));
       HIPC(hipMemsetAsync(op->res_bh_hi, 0, two * sizeof(double2), c->stream));
     }
     const size_t bytes = two * sizeof(double2);
+    check_site(c, "sl2_res: work before the exchanges", c->stream);
     c->comm->halo(lo_x ? b + s0.off : nullptr, lo_x ? op->res_bh_lo : nullptr,
                   hi_x ? b + sl.off + (size_t)(sl.nl - 2) * n : nullptr,
                   hi_x ? op->res_bh_hi : nullptr, bytes, c->stream, c->cstream, c->ev_in);
+    check_site(c, "sl2_res: b's two-row halo exchange", c->cstream);
     c->comm->halo(lo_x ? x + s0.off : nullptr, lo_x ? s0.halo2_lo : nullptr,
                   hi_x ? x + sl.off + (size_t)(sl.nl - 2) * n : nullptr,
                   hi_x ? sl.halo2_hi : nullptr, bytes, c->stream, c->cstream, c->ev_in);
+    check_site(c, "sl2_res: x's two-row halo exchange", c->cstream);
   }
   int np = 0;
   auto launch_rows = [&](int si, int r0, int r1, int rpb, hipStream_t st) {
@@ -805,6 +924,7 @@ void run_sl2_res(hh_op* op, const double2* b, const double2* x, double2* v0, int
     const int r1 = (si == S - 1 && hi_x) ? std::max(r0, s.nl - 2) : s.nl;
     launch_rows(si, r0, r1, s.rpb, c->stream);
   }
+  if (lo_x || hi_x) check_site(c, "sl2_res: interior rows", c->stream);
   if (lo_x || hi_x) {
     // the two rows next to each cross-rank boundary, on the halo stream behind the exchange
     hipStream_t hs = c->cstream;
@@ -814,6 +934,7 @@ void run_sl2_res(hh_op* op, const double2* b, const double2* x, double2* v0, int
       if (lo_x) launch_rows(0, 0, std::min(2, s0.nl), 2, hs);
       if (hi_x) launch_rows(S - 1, std::max(0, sl.nl - 2), sl.nl, 2, hs);
     }
+    check_site(c, "sl2_res: boundary rows", hs);
     HIPC(hipEventRecord(c->ev_halo, hs));
     HIPC(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
   }
@@ -870,6 +991,7 @@ int device_cus(hh_ctx* c) {
 int mnorm_slot(const hh_op* op, int dst) { return op->pkind == HH_PREC_NONE ? dst : dst + 1; }
 
 void read_dev(hh_op* op, const double* dsrc, double* hdst, int count) {
+  check_site(op->ctx, "queued work before a host read", op->ctx->stream);
   HIPC(hipMemcpyAsync(op->status_h, dsrc, count * sizeof(double), hipMemcpyDeviceToHost,
                       op->ctx->stream));
   HIPC(hipStreamSynchronize(op->ctx->stream));
@@ -964,6 +1086,7 @@ int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double*
       launch_fused_edge(K, e, 0, rows_rank, 0, 0, c->stream);
     else
       launch_fused_edge(K, e, 0, lo_x ? H : 0, rows_rank - H, hi_x ? H : 0, c->stream);
+    check_site(c, "one-pass: edge rows of u_K", c->stream);
     const Slab& s0 = op->slabs[0];
     const Slab& sL = op->slabs[S - 1];
     hipEvent_t t_ready = tmark(op, c->stream);
@@ -973,6 +1096,7 @@ int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double*
                   (size_t)H * n * sizeof(double2), c->stream, c->cstream, c->ev_in);
     t_halo = tmark(op, c->cstream);
     tspan(op, HH_SPAN_HALO, t_ready, t_halo);
+    check_site(c, "one-pass: u_K halo exchange", c->cstream);
   }
   hipEvent_t t_int0 = tmark(op, c->stream);
   for (int si = 0; si < S; ++si) {
@@ -983,6 +1107,8 @@ int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double*
   }
   hipEvent_t t_int1 = tmark(op, c->stream);
   tspan(op, HH_SPAN_INTERIOR, t_int0, t_int1);
+  if (lo_x || hi_x) check_site(c, slk ? "one-pass (slk): interior rows" : "one-pass: interior rows",
+                               c->stream);
   if (lo_x || hi_x) {
     hipStream_t hs = c->cstream;
     const Slab& s0 = op->slabs[0];
@@ -994,6 +1120,7 @@ int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double*
       if (lo_x) launch(0, 0, std::min(H, s0.nl), H, 0, hs);
       if (hi_x) launch(S - 1, std::max(0, sL.nl - H), sL.nl, H, 0, hs);
     }
+    check_site(c, slk ? "one-pass (slk): boundary rows" : "one-pass: boundary rows", hs);
     hipEvent_t t_bnd = tmark(op, hs);
     tspan(op, HH_SPAN_BOUNDARY, t_halo, t_bnd);
     tspan(op, HH_SPAN_HALO_WAIT, t_int1, t_bnd, true);
@@ -1347,12 +1474,12 @@ HH_API int hh_op_create(hh_ctx* c, int n, int b, double cconst, double eta, doub
         sl.invc2_halo = dalloc<double>(hb.size());
         HIPC(hipMemcpy(sl.invc2_halo, hb.data(), hb.size() * sizeof(double), hipMemcpyHostToDevice));
       }
-      sl.halo2_lo = dalloc<double2>(2 * (size_t)n);
-      sl.halo2_hi = dalloc<double2>(2 * (size_t)n);
+      sl.halo2_lo = dalloc_guarded<double2>(2 * (size_t)n, c->device, false);
+      sl.halo2_hi = dalloc_guarded<double2>(2 * (size_t)n, c->device, true);
       HIPC(hipMemsetAsync(sl.halo2_lo, 0, 2 * n * sizeof(double2), c->stream));
       HIPC(hipMemsetAsync(sl.halo2_hi, 0, 2 * n * sizeof(double2), c->stream));
-      sl.halo_lo_buf = dalloc<double2>(n);
-      sl.halo_hi_buf = dalloc<double2>(n);
+      sl.halo_lo_buf = dalloc_guarded<double2>(n, c->device, false);
+      sl.halo_hi_buf = dalloc_guarded<double2>(n, c->device, true);
       HIPC(hipMemsetAsync(sl.halo_lo_buf, 0, n * sizeof(double2), c->stream));
       HIPC(hipMemsetAsync(sl.halo_hi_buf, 0, n * sizeof(double2), c->stream));
       op->slabs.push_back(sl);
@@ -2541,6 +2668,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       launch_reduce(op->partials, blocks, 4, 3, op->red + 16, s, stp);
       allreduce_sum_dev(op, op->red + 16, 3);
       launch_gmres_lag(g, 0, op->red + 16, op->red + 16 + 3, false, eps, ptol, stop_col, s);
+      check_site(c, "one-pass: first projection + column", s);
       for (int c2 = 0; c2 < stop_col; ++c2) {
         const int K = c2 + 1, K2 = K + 1;
         const int np = run_fused(op, K, Wb[c2 & 1], Wb[(c2 + 1) & 1], op->red + 16, g.sscale + K);
@@ -2562,6 +2690,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
           tspan(op, HH_SPAN_COLUMN, k1, tmark(op, s));
         }
         HIPC(hipGetLastError());
+        check_site(c, "one-pass: reduce + allreduce + column", s);
       }
       {  // the last column's update and the norm that completes it
         const int K = stop_col + 1;
@@ -2579,6 +2708,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         allreduce_sum_dev(op, op->red + 8, 1);
         launch_gmres_lag(g, stop_col + 1, nullptr, op->red + 8, true, eps, ptol, stop_col, s);
         HIPC(hipGetLastError());
+        check_site(c, "one-pass: cycle end", s);
       }
     }
     for (int c2 = 0; c2 <= stop_col && lagged; ++c2) {
@@ -2688,6 +2818,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       launch_cycle_finish(g, stop_col, V + (size_t)(stop_col + 1) * ldv, x, L, blocks, s);
     launch_gmres_solve(g, stop_col, merge_end, s);
     launch_xupdate(V, ldv, stop_col + 1, g.ycoef, x, L, blocks, s, g.ctrl);
+    check_site(c, "cycle finish + triangular solve + x update", s);
     residual(op, b, x, V, 4);  // r = b - A x; V[0] = M r for the next cycle
     read_dev(op, op->red + 4, st, 1);
     const double* sth = op->status_h + kRedStatus;

@@ -35,27 +35,42 @@ def rccl_rank_env(rank):
                 HH_FORCE_DEVICE="0")
 
 
-def _run_workers(tmp_path, world, n, extra=(), transport="shm", timeout=240):
+def _run_workers(tmp_path, world, n, extra=(), transport="shm", timeout=240, env_extra=None):
     tok = os.urandom(128).hex()
     procs = []
     for r in range(world):
         out = tmp_path / f"r{r}.npz"
         env = dict(os.environ, **(rccl_rank_env(r) if transport == "rccl" else {}),
-                   TMPDIR=str(tmp_path))
+                   TMPDIR=str(tmp_path), **(env_extra or {}))
         procs.append((subprocess.Popen([sys.executable, WORKER, "--rank", str(r), "--world",
                                         str(world), "--id", tok, "--out", str(out), "--n", str(n),
                                         "--transport", transport] + list(extra),
                                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env),
                       out))
+    # poll: the first rank that fails ends the run at once (its peers would otherwise wait for
+    # it in a collective until their own transport timeout) and its output is reported
+    import time
+    t0 = time.monotonic()
     try:
-        for p, _ in procs:
-            p.wait(timeout=timeout)
-    except subprocess.TimeoutExpired:
+        while True:
+            codes = [p.poll() for p, _ in procs]
+            bad = [r for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r = bad[0]
+                for q, _ in procs:
+                    if q.poll() is None:
+                        q.kill()
+                out = procs[r][0].stdout.read().decode(errors="replace")
+                raise AssertionError(f"rank {r} of {world} exited with {codes[r]}:\n{out[-3000:]}")
+            if all(c == 0 for c in codes):
+                break
+            if time.monotonic() - t0 > timeout:
+                raise subprocess.TimeoutExpired("dist_worker", timeout)
+            time.sleep(0.05)
+    finally:
         for q, _ in procs:
-            q.kill()
-        raise
-    for p, _ in procs:
-        assert p.returncode == 0, p.stdout.read().decode()[-3000:]
+            if q.poll() is None:
+                q.kill()
     return [np.load(o) for _, o in procs]
 
 
@@ -158,6 +173,26 @@ def test_fused_pass_ranks_match_single_domain(tmp_path, world, slabs, transport)
     # f (1 + 1e-15) by 7.7e-6 (tools/slab_drift.py --n 150 --slabs 16 --restart 20 --iters 50,
     # profiles/r05/r05_slab_drift_cpu_150_16slabs_jacobi.log)
     _check_against_single_domain(parts, ref, world, n, tol=1e-7 if world * slabs >= 16 else 1e-8)
+
+
+@pytest.mark.parametrize("world,transport", [(3, "shm"), (3, "rccl"), (8, "shm")])
+def test_fused_pass_guarded_halo_buffers(tmp_path, world, transport):
+    """The round-5 8-rank RCCL fault: the shifted-Laplace pass's boundary rows read
+    u_K of row -3 -- one row BEFORE the received halo -- at halo_lo - n.  The value was never
+    used, so every parity test passed; whether the read faulted depended on what the allocator
+    had mapped there (it did at 11584^2 / 8 ranks under RCCL's layout, in every rank).  Here
+    every halo receive buffer sits against an unmapped guard granule (HH_GUARD_HALO=1,
+    runtime.cpp dalloc_guarded): a read one row beyond a received halo on either side faults
+    at the smallest shape, on either transport.  The one-pass path (none / Jacobi / the
+    two-sweep shifted Laplace), the fused M A and the apply then run clean and still match the
+    single domain."""
+    n = 150
+    parts = _run_workers(tmp_path, world, n, ["--krylov", "fused"], transport=transport,
+                         timeout=240, env_extra={"HH_GUARD_HALO": "1", "HH_CHECK_HALO": "1"})
+    ref = _single_domain(n, krylov="fused")
+    for name in ("none", "jacobi", "sl"):
+        assert all(str(p[f"path_{name}"]) == "one-pass" for p in parts), name
+    _check_against_single_domain(parts, ref, world, n)
 
 
 @pytest.mark.parametrize("world", [2, 3])

@@ -4,12 +4,12 @@
 # RCCL over loopback (one NCCL_HOSTID per rank) if it accepts 8 ranks on one device, else the
 # host-staged SHM transport; the line's `parallelism` names the one used.  ARGS are passed to
 # bench.py (e.g. --grid 4096 --same-n 2048 for a reduced grid).  Rates are one card shared by 8
-# processes, not scaling.
+# processes, not scaling.  TRANSPORTS limits the transports tried (default "rccl shm").
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/rehearse8}; mkdir -p $OUT
 TAG=${TAG:-n8}
-for tr in rccl shm; do
+for tr in ${TRANSPORTS:-rccl shm}; do
   extra=""; [ $tr = rccl ] && extra="HH_RCCL_HOSTID_PER_RANK=1 NCCL_SOCKET_IFNAME=lo NCCL_IB_DISABLE=1"
   env HH_TRANSPORT=$tr HH_FORCE_DEVICE=0 $extra timeout -k 10 ${SECS:-600} python bench.py --gpus 8 "$@" \
     > $OUT/bench_${TAG}_$tr.log 2>&1
@@ -21,5 +21,7 @@ for tr in rccl shm; do
   fi
   tail -20 $OUT/bench_${TAG}_$tr.log
   case $rc in 124|137|134|139) exit $rc;; esac
+  # a device fault reported as an error (HH_CHECK_HALO attributes it): nothing more on the GPU
+  grep -q "illegal memory access\|FAULT at" $OUT/bench_${TAG}_$tr.log && exit 5
 done
 exit 1
