@@ -159,10 +159,8 @@ def relaunch_distributed(args):
 
 def local_f1(omega, n, j0, j1, r1=.5, r2=.125):
     """rows [j0, j1) of init_f1_mat(r1, r2, omega, n) (code.py:53-58), flattened."""
-    import numpy as np
-    x = np.linspace(0, 1, n + 2)[1:-1]
-    yy = x[j0:j1, None]
-    return np.exp(-(4 * omega / np.pi) ** 2 * ((x[None, :] - r1) ** 2 + (yy - r2) ** 2)).ravel()
+    import helmholtz_preconditioner_amd as H
+    return H.init_f1_rows(r1, r2, omega, n, j0, j1).ravel()
 
 
 TRAFFIC_DB = "profiles/r05_pmc_traffic.json"

@@ -58,7 +58,7 @@ def main():
         yref = np.load(os.path.join(a.ref_dir, "y.npy"), mmap_mode="r")[j0 * n:j1 * n]
         out["y_mismatch"] = int(np.count_nonzero(yl != yref))
         del yl, yref
-    f = H.init_f1_mat(.5, .125, om, n)[j0:j1].ravel()
+    f = H.init_f1_rows(.5, .125, om, n, j0, j1).ravel()  # (rows j0 .. j1 of init_f1_mat)
     xs, info, hist = H.gmres(A, f, rtol=1e-3, restart=20, maxiter=a.iters, M="jacobi",
                              callback=lambda r: None, callback_type="legacy",
                              return_history=True)

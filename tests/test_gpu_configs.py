@@ -100,7 +100,7 @@ N4, WN4, K4 = 8192, 256.0, 20
 # K = 20 (profiles/r03_gmres_sensitivity_config4.log) -- so the oracle comparison stops at 10
 K4_ORACLE = 10
 N5, WN5, K5 = 16384, 800.0, 5
-from test_gpu_dist import rccl_rank_env  # noqa: E402  (one NCCL host id per rank on one GPU)
+from test_gpu_dist import rccl_rank_env, wait_ranks  # noqa: E402  (one NCCL host id per rank)
 
 
 def _single_domain_solve(ctx, d, n, wn, K, with_apply, K_oracle=None):
@@ -188,7 +188,7 @@ def test_config4_jacobi_gmres_vs_oracle(config4_reference):
     _oracle_parity(d, N4, K4_ORACLE, info, hist, params, f, name="x_oracle.npy")
 
 
-def _run_large_ranks(tmp_path, d, world, transport, n, wn, K, apply_check=True):
+def _run_large_ranks(tmp_path, d, world, transport, n, wn, K, apply_check=True, timeout=300):
     tok = os.urandom(128).hex()
     procs = []
     for r in range(world):
@@ -201,15 +201,7 @@ def _run_large_ranks(tmp_path, d, world, transport, n, wn, K, apply_check=True):
                transport] + ([] if apply_check else ["--no-apply"])
         procs.append((subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                                        env=env), out))
-    try:
-        for p, _ in procs:
-            p.wait(timeout=300)
-    except subprocess.TimeoutExpired:
-        for q, _ in procs:
-            q.kill()
-        raise
-    for p, _ in procs:
-        assert p.returncode == 0, p.stdout.read().decode()[-3000:]
+    wait_ranks([p for p, _ in procs], timeout)
     parts = [np.load(o) for _, o in procs]
     assert parts[0]["j0"] == 0 and parts[-1]["j1"] == n
     return parts
@@ -249,8 +241,14 @@ def test_config5_jacobi_gmres_vs_oracle(config5_reference):
     _oracle_parity(d, N5, K5, info, hist, params, f)
 
 
-def test_config5_two_ranks_match_single_domain(config5_reference, tmp_path):
-    """The same solve split over 2 ranks (shared-memory transport, both on device 0)."""
+@pytest.mark.parametrize("world,transport", [(2, "shm"), (8, "shm"), (8, "rccl")])
+def test_config5_ranks_match_single_domain(config5_reference, tmp_path, world, transport):
+    """The same solve split over `world` ranks, all on device 0 -- config 5's own 8-rank split
+    (2048 rows a rank: the one-pass iteration's interior, edge and boundary launches, u_K's edge
+    rows exchanged every pass) over the shared-memory transport and over RCCL: every rank on the
+    one-pass path, history and field to 1e-8 of the single domain."""
     d, info, hist, _, _ = config5_reference
-    parts = _run_large_ranks(tmp_path, d, 2, "shm", N5, WN5, K5, apply_check=False)
+    parts = _run_large_ranks(tmp_path, d, world, transport, N5, WN5, K5, apply_check=False,
+                             timeout=600)
+    assert all(str(p["transport"]) == transport for p in parts)
     _assert_ranks_match(parts, info, hist)

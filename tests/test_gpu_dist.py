@@ -35,6 +35,35 @@ def rccl_rank_env(rank):
                 HH_FORCE_DEVICE="0")
 
 
+def wait_ranks(procs, timeout):
+    """Wait for the rank processes (stdout piped): the first rank that fails ends the run at
+    once -- its peers would otherwise wait for it in a collective until their own transport
+    timeout -- and its output is reported."""
+    import time
+    t0 = time.monotonic()
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [r for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r = bad[0]
+                for q in procs:
+                    if q.poll() is None:
+                        q.kill()
+                out = procs[r].stdout.read().decode(errors="replace")
+                raise AssertionError(f"rank {r} of {len(procs)} exited with {codes[r]}:\n"
+                                     f"{out[-3000:]}")
+            if all(c == 0 for c in codes):
+                return
+            if time.monotonic() - t0 > timeout:
+                raise subprocess.TimeoutExpired("rank processes", timeout)
+            time.sleep(0.05)
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+
+
 def _run_workers(tmp_path, world, n, extra=(), transport="shm", timeout=240, env_extra=None):
     tok = os.urandom(128).hex()
     procs = []
@@ -47,30 +76,7 @@ def _run_workers(tmp_path, world, n, extra=(), transport="shm", timeout=240, env
                                         "--transport", transport] + list(extra),
                                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env),
                       out))
-    # poll: the first rank that fails ends the run at once (its peers would otherwise wait for
-    # it in a collective until their own transport timeout) and its output is reported
-    import time
-    t0 = time.monotonic()
-    try:
-        while True:
-            codes = [p.poll() for p, _ in procs]
-            bad = [r for r, c in enumerate(codes) if c not in (None, 0)]
-            if bad:
-                r = bad[0]
-                for q, _ in procs:
-                    if q.poll() is None:
-                        q.kill()
-                out = procs[r][0].stdout.read().decode(errors="replace")
-                raise AssertionError(f"rank {r} of {world} exited with {codes[r]}:\n{out[-3000:]}")
-            if all(c == 0 for c in codes):
-                break
-            if time.monotonic() - t0 > timeout:
-                raise subprocess.TimeoutExpired("dist_worker", timeout)
-            time.sleep(0.05)
-    finally:
-        for q, _ in procs:
-            if q.poll() is None:
-                q.kill()
+    wait_ranks([p for p, _ in procs], timeout)
     return [np.load(o) for _, o in procs]
 
 

@@ -35,6 +35,16 @@ def test_inputs_match_reference():
                                    z["f2"], rtol=1e-13, atol=1e-300)
 
 
+@pytest.mark.parametrize("n,j0,j1", [(33, 0, 33), (150, 37, 101), (257, 250, 257)])
+def test_f1_rows_are_the_slab_of_init_f1_mat(n, j0, j1):
+    """A rank's rows of the source (media.init_f1_rows: bench.py and the multi-rank workers,
+    which must not form the whole n x n grid at 16384^2) are bit for bit rows j0 .. j1 of
+    init_f1_mat, the golden-pinned reference input."""
+    om = complex(n / 3.0, 0.25)
+    np.testing.assert_array_equal(media.init_f1_rows(.5, .125, om, n, j0, j1),
+                                  media.init_f1_mat(.5, .125, om, n)[j0:j1])
+
+
 @pytest.mark.parametrize("name", COEF)
 def test_csr_matches_reference(name):
     z = load_golden(name)
