@@ -46,26 +46,45 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 class Watchdog:
     """Per-rank phase timer: `phase(name, bound_s)` starts a phase; a
     daemon thread ends the process with status 3 (os._exit: no re-exec, no cleanup that could
-    block on the stalled collective) when the current phase overruns its bound, after
-    printing the phase and rank.  ctypes releases the GIL inside the native calls, so the
-    thread runs while the main thread is blocked in RCCL or a stream synchronize.
+    block on the stalled collective) when the current phase overruns its bound.  ctypes releases
+    the GIL inside the native calls, so the thread runs while the main thread is blocked in RCCL
+    or a stream synchronize.
+
+    Naming the stalled rank: the rank that stops and the ranks that wait for
+    it in its next collective enter the phase together and overrun its bound together, so the
+    first watchdog to fire may well be a waiting one.  Every rank's thread therefore publishes,
+    twice a second, its phase and the collectives it has entered (hh_ctx_progress: halo
+    exchanges + allreduces, the same sequence on every rank) to a node-local file next to the
+    rendezvous file; the watchdog that fires reads all of them and names the rank(s) with the
+    fewest collectives entered -- the one(s) the others are waiting for -- or, with equal counts,
+    the earliest phase; a rank with no state file never started.
     HH_WATCHDOG_SCALE multiplies every bound (tests shorten them); HH_BENCH_STALL=rank:phase
     makes that rank hang at the start of the phase whose name starts with `phase` (the
     stalled-rank rehearsal)."""
 
-    def __init__(self, rank):
-        self.rank = rank
+    def __init__(self, rank, world=1):
+        from helmholtz_preconditioner_amd import dist
+        self.rank, self.world = rank, world
         self.scale = float(os.environ.get("HH_WATCHDOG_SCALE", "1"))
         self.name, self.deadline, self.t0 = "startup", None, time.monotonic()
+        self.seq = 0  # phases entered
+        self.ctx = None
         self.lock = threading.Lock()
+        self.paths = [dist.job_file("wd", f"_r{r}.json") for r in range(world)]
         stall = os.environ.get("HH_BENCH_STALL", "")
         self.stall = tuple(stall.split(":", 1)) if ":" in stall else None
         threading.Thread(target=self._run, daemon=True).start()
+
+    def attach(self, ctx):
+        """the context whose collectives count as this rank's progress"""
+        self.ctx = ctx
 
     def phase(self, name, bound_s):
         with self.lock:
             self.name, self.t0 = name, time.monotonic()
             self.deadline = self.t0 + bound_s * self.scale
+            self.seq += 1
+        self._publish()
         if self.stall and int(self.stall[0]) == self.rank and name.startswith(self.stall[1]):
             while True:  # simulated stalled rank: only the watchdog ends it
                 time.sleep(1)
@@ -73,16 +92,71 @@ class Watchdog:
     def done(self):
         with self.lock:
             self.name, self.deadline = "done", None
+        try:
+            os.unlink(self.paths[self.rank])
+        except OSError:
+            pass
+
+    def _collectives(self):
+        try:
+            return self.ctx.collectives() if self.ctx is not None else -1
+        except Exception:  # (a closed context)
+            return -1
+
+    def _publish(self):
+        if self.world == 1:
+            return
+        with self.lock:
+            st = {"rank": self.rank, "phase": self.name, "seq": self.seq,
+                  "in_phase_s": round(time.monotonic() - self.t0, 1)}
+        st["collectives"] = self._collectives()
+        path = self.paths[self.rank]
+        try:
+            with open(path + ".tmp", "w") as fh:
+                json.dump(st, fh)
+            os.replace(path + ".tmp", path)
+        except OSError:
+            pass
+
+    def stalled_ranks(self):
+        """(stalled ranks, per-rank states) from the ranks' published states"""
+        states = {}
+        for r, path in enumerate(self.paths):
+            try:
+                with open(path) as fh:
+                    states[r] = json.load(fh)
+            except (OSError, ValueError):
+                pass
+        missing = [r for r in range(self.world) if r not in states]
+        if missing:
+            return missing, states
+        calls = {r: s["collectives"] for r, s in states.items() if s["collectives"] >= 0}
+        if calls and min(calls.values()) < max(calls.values()):
+            lo = min(calls.values())
+            return sorted(r for r, c in calls.items() if c == lo), states
+        seqs = {r: s["seq"] for r, s in states.items()}
+        if min(seqs.values()) < max(seqs.values()):
+            lo = min(seqs.values())
+            return sorted(r for r, q in seqs.items() if q == lo), states
+        return [], states
 
     def _run(self):
         while True:
             time.sleep(0.5)
+            self._publish()
             with self.lock:
                 late = self.deadline is not None and time.monotonic() > self.deadline
                 name, el = self.name, time.monotonic() - self.t0
             if late:
-                print(f"[bench watchdog] rank {self.rank}: phase '{name}' stalled for {el:.0f} s "
-                      f"(bound exceeded); exiting with status 3", file=sys.stderr, flush=True)
+                msg = (f"[bench watchdog] rank {self.rank}: phase '{name}' stalled for {el:.0f} s "
+                       f"(bound exceeded); exiting with status 3")
+                if self.world > 1:
+                    stalled, states = self.stalled_ranks()
+                    rows = "; ".join(f"rank {r}: '{s['phase'][:40]}' {s['in_phase_s']} s, "
+                                     f"{s['collectives']} collectives" for r, s in sorted(states.items()))
+                    who = ",".join(map(str, stalled)) if stalled else "undetermined"
+                    msg += f"\n[bench watchdog] stalled rank(s): {who} -- {rows}"
+                print(msg, file=sys.stderr, flush=True)
                 os._exit(3)
 
 
@@ -544,10 +618,11 @@ def main():
     from helmholtz_preconditioner_amd import dist
 
     rank, world, _ = dist.env_rank_world()
-    wd = Watchdog(rank)
+    wd = Watchdog(rank, world)
     transport = os.environ.get("HH_TRANSPORT", "rccl") if world > 1 else "none"
     wd.phase("context + communicator init (ncclCommInitRank)", 240)
     ctx = dist.init_from_env(virtual_slabs=args.virtual_slabs)
+    wd.attach(ctx)
     H.set_default_context(ctx)
 
     n = args.grid or int(round(4096 * math.sqrt(world) / 32) * 32)

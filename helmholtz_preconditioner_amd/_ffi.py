@@ -88,6 +88,7 @@ SIGNATURES = [
     ("hh_ctx_allreduce_sum", c_int, [c_void_p, c_dp, c_int]),
     ("hh_ctx_barrier", c_int, [c_void_p]),
     ("hh_ctx_synchronize", c_int, [c_void_p]),
+    ("hh_ctx_progress", c_int, [c_void_p, c_lp]),
     ("hh_op_create", c_int, [c_void_p, c_int, c_int, c_double, c_double, c_double, c_double,
                              c_double, c_dp, c_double, c_double, c_double, PP]),
     ("hh_op_destroy", c_int, [c_void_p]),

@@ -63,6 +63,13 @@ class Context:
     def synchronize(self):
         check(lib.hh_ctx_synchronize(self.handle))
 
+    def collectives(self) -> int:
+        """Collectives (halo exchanges + allreduces) this rank has entered (hh_ctx_progress);
+        safe to call from another thread while this one is blocked inside a collective."""
+        n = ctypes.c_long()
+        check(lib.hh_ctx_progress(self.handle, ctypes.byref(n)))
+        return n.value
+
     def close(self):
         if getattr(self, "_h", None) is not None:
             lib.hh_ctx_destroy(self._h)

@@ -36,11 +36,11 @@ class RcclComm final : public Comm {
   ~RcclComm() override {
     if (comm_) ncclCommDestroy(comm_);
   }
-  void allreduce(double* d, int count, bool max, hipStream_t s) override {
+  void do_allreduce(double* d, int count, bool max, hipStream_t s) override {
     NCCLC(ncclAllReduce(d, d, count, ncclFloat64, max ? ncclMax : ncclSum, comm_, s));
   }
-  void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi, size_t bytes,
-            hipStream_t compute, hipStream_t hs, hipEvent_t ready) override {
+  void do_halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi,
+               size_t bytes, hipStream_t compute, hipStream_t hs, hipEvent_t ready) override {
     // the halo stream starts once the input vector is complete on the compute stream
     HIPC(hipEventRecord(ready, compute));
     HIPC(hipStreamWaitEvent(hs, ready, 0));
@@ -135,7 +135,7 @@ class ShmComm final : public Comm {
     if (hpin_) (void)hipHostFree(hpin_);
     if (base_) munmap(base_, size_);
   }
-  void allreduce(double* d, int count, bool max, hipStream_t s) override {
+  void do_allreduce(double* d, int count, bool max, hipStream_t s) override {
     REQUIRE(count <= (int)kShmSlotDoubles, "shm allreduce too large");
     HIPC(hipMemcpyAsync(pin_, d, count * sizeof(double), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
@@ -153,8 +153,8 @@ class ShmComm final : public Comm {
     HIPC(hipMemcpyAsync(d, pin_, count * sizeof(double), hipMemcpyHostToDevice, s));
     HIPC(hipStreamSynchronize(s));
   }
-  void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi, size_t bytes,
-            hipStream_t compute, hipStream_t, hipEvent_t) override {
+  void do_halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi,
+               size_t bytes, hipStream_t compute, hipStream_t, hipEvent_t) override {
     REQUIRE(bytes <= kShmHaloBytes, "shm halo of %zu bytes exceeds the slot (two rows of n <= %zu)",
             bytes, kShmMaxRow);
     // Device <-> shared memory goes through this rank's pinned staging rows: DMA copies to /

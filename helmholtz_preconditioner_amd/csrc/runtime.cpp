@@ -1359,6 +1359,13 @@ HH_API int hh_ctx_barrier(hh_ctx* c) {
   GUARD_END
 }
 
+HH_API int hh_ctx_progress(hh_ctx* c, long* collectives) {
+  GUARD_BEGIN
+  REQUIRE(c && collectives, "null argument");
+  *collectives = c->comm ? c->comm->entered() : 0;
+  GUARD_END
+}
+
 HH_API int hh_ctx_synchronize(hh_ctx* c) {
   GUARD_BEGIN
   REQUIRE(c, "null ctx");

@@ -29,11 +29,20 @@ def env_rank_world():
             int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0"))))
 
 
+def job_key() -> str:
+    """A key every rank of this launch computes alike (the launcher's PID, MASTER_PORT and run
+    id): names the node-local files the ranks share (rendezvous id, watchdog state)."""
+    return f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}_" \
+           f"{os.environ.get('TORCHELASTIC_RUN_ID', 'none')}"
+
+
+def job_file(kind: str, suffix: str, key: str | None = None) -> str:
+    return os.path.join(os.environ.get("TMPDIR", tempfile.gettempdir()),
+                        f"hh_{kind}_{key or job_key()}{suffix}")
+
+
 def _rdzv_path(key: str | None):
-    if key is None:
-        key = f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}_" \
-              f"{os.environ.get('TORCHELASTIC_RUN_ID', 'none')}"
-    return os.path.join(os.environ.get("TMPDIR", tempfile.gettempdir()), f"hh_rdzv_{key}.id")
+    return job_file("rdzv", ".id", key)
 
 
 def exchange_unique_id(rank: int, world: int, key: str | None = None, timeout: float = 300.0,

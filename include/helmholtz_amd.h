@@ -101,6 +101,11 @@ int hh_ctx_allreduce_max(hh_ctx* ctx, double* values, int count);
 int hh_ctx_allreduce_sum(hh_ctx* ctx, double* values, int count);
 int hh_ctx_barrier(hh_ctx* ctx);
 int hh_ctx_synchronize(hh_ctx* ctx);
+/* Collectives (halo exchanges + allreduces) this rank has entered so far, 0 at world 1.  Every
+ * rank of a job enters the same sequence, so when a job stalls the rank with the fewest is the
+ * one that stopped (bench.py's watchdog reads it from its own thread while the main thread may
+ * be blocked inside a collective: the read takes no lock and touches no device). */
+int hh_ctx_progress(hh_ctx* ctx, long* collectives);
 
 /* --------------------------------------------------------------- operator */
 /* Replaces build_A_matrix(b, const, eta, omega, h, n, c_mat), code.py:202-219

@@ -262,19 +262,24 @@ def test_bench_two_ranks_rehearsal(tmp_path, transport):
     assert 1 <= gi["allreduces"] <= 3  # one per inner iteration (+ per-cycle extras)
 
 
-def test_bench_stalled_rank_exits_with_the_phase_named(tmp_path):
-    """A rank that stalls (simulated: HH_BENCH_STALL makes rank 1 hang when its first applies
-    start) must end the job with a non-zero status and the stalled phase named, not hang.  The
-    stalled rank and the rank waiting for it in the first halo exchange enter the phase together
-    under the same bound, so either watchdog may fire first (rank 0's did once, in the final
-    round-5 suite): the phase must be named by one of them."""
+@pytest.mark.parametrize("world,stall", [(2, 1), (3, 2)])
+def test_bench_stalled_rank_exits_with_the_phase_named(tmp_path, world, stall):
+    """A rank that stalls (simulated: HH_BENCH_STALL makes it hang when its first applies start)
+    must end the job with a non-zero status, the stalled phase named and the STALLED rank named
+    -- not the rank waiting for it.  Both enter the phase together under the same bound, so
+    either watchdog may fire first (the waiting rank's did once, round 5); whichever fires reads
+    every rank's published progress (collectives entered, bench.py Watchdog) and names the rank
+    with the fewest."""
     import re
-    out = _torchrun_bench(tmp_path, 2, BENCH_SMALL,
+    out = _torchrun_bench(tmp_path, world, BENCH_SMALL,
                           {"HH_TRANSPORT": "shm", "HH_WATCHDOG_SCALE": "0.1",
-                           "HH_BENCH_STALL": "1:first applies"}, timeout=180)
+                           "HH_BENCH_STALL": f"{stall}:first applies"}, timeout=180)
     assert out.returncode != 0
-    assert re.search(r"\[bench watchdog\] rank [01]: phase 'first applies", out.stderr), \
+    assert re.search(r"\[bench watchdog\] rank \d: phase 'first applies", out.stderr), \
         out.stderr[-3000:]
+    named = re.findall(r"\[bench watchdog\] stalled rank\(s\): ([0-9,]+|undetermined)",
+                       out.stderr)
+    assert named and all(n == str(stall) for n in named), out.stderr[-3000:]
 
 
 @pytest.mark.parametrize("world", [2, 3])
