@@ -250,7 +250,8 @@ def measured_traffic(n, medium, rows, stencil=5):
     cannot be read inside the timed run, so this is the committed measurement of the same kernel
     and workload: (ratio, source), or Nones for a shape without a record."""
     kind = "const" if medium == "const" else medium
-    if os.environ.get("HH_TILE_XCD", "0") != "0":
+    import helmholtz_preconditioner_amd as H
+    if "HH_TILE_XCD" in H.knobs():
         return None, None  # (the records are of the default tile order)
     for db, key in ((TRAFFIC_DB, f"n{n}_rows{rows}_{kind}_s{stencil}"),
                     (TRAFFIC_DB_R03, f"n{n}_{kind}_s{stencil}" if rows == n else None)):
@@ -455,7 +456,10 @@ FUSED_KNOBS = ("HH_FUSED_ITER", "HH_FUSED_KEEP", "HH_FUSED_ROWS", "HH_BASIS_PAD"
 
 
 def fused_knobs():
-    return {k: os.environ[k] for k in FUSED_KNOBS if k in os.environ}
+    """the run's values of FUSED_KNOBS that differ from the shipped path (the library's own
+    reading, hh_knobs_json)"""
+    import helmholtz_preconditioner_amd as H
+    return {k: str(v["value"]) for k, v in H.knobs().items() if k in FUSED_KNOBS}
 
 
 def fused_pass_traffic(n, rows, medium, precond, restart):
@@ -763,6 +767,8 @@ def main():
                         f"(+ GMRES({args.restart}) {args.precond}-preconditioned)",
             "n": n, "unknowns": n * n, "wave_num": args.wave_num, "b": args.b, "C": args.C,
             "alpha": args.alpha, "bytes_per_unknown": bpp, "stencil_points": args.stencil,
+            # the library's HH_* knobs that differ from the shipped path ({} = the default path)
+            "knobs": H.knobs(),
             "parallelism": (f"row-slab x{world} ({'RCCL' if transport == 'rccl' else 'host-staged SHM'}"
                             f" halo{', all ranks on one GPU' if os.environ.get('HH_FORCE_DEVICE') else ''})"
                             if world > 1 else "single GPU"),

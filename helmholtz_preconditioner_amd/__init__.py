@@ -13,7 +13,7 @@ the C ABI in ``include/helmholtz_amd.h`` (ctypes shim ``_ffi.py``).  Importing
 this package fails if that library has not been built; there is no CPU path.
 """
 from ._ffi import HHError  # noqa: F401  (raises ImportError if the .so is missing)
-from .context import Context, default_context, device_count, set_default_context, unique_id  # noqa: F401
+from .context import Context, default_context, device_count, knobs, set_default_context, unique_id  # noqa: F401,E501
 from .media import (constant_c_mat, init_c1_f1, init_c1_f2, init_c1_mat, init_c2_f1,  # noqa: F401
                     init_c2_f2, init_c2_mat, init_f1_mat, init_f1_rows, init_f2_mat, marmousi_like_c_mat,
                     problem_params)
@@ -28,7 +28,7 @@ from . import dist  # noqa: F401
 __all__ = [
     "build_A_matrix", "gmres", "DeviceOperator", "DeviceVector", "Jacobi", "ShiftedLaplace",
     "Sweeping", "STENCIL9_WEIGHTS",
-    "Context", "default_context", "set_default_context", "device_count", "unique_id",
+    "Context", "default_context", "set_default_context", "device_count", "unique_id", "knobs",
     "init_c1_mat", "init_c2_mat", "init_f1_mat", "init_f1_rows", "init_f2_mat", "init_c1_f1", "init_c1_f2",
     "init_c2_f1", "init_c2_f2", "constant_c_mat", "marmousi_like_c_mat", "problem_params",
     "HHError", "run_solver", "gmres_counter", "true_relative_residual",

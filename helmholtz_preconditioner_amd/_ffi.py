@@ -89,6 +89,7 @@ SIGNATURES = [
     ("hh_ctx_barrier", c_int, [c_void_p]),
     ("hh_ctx_synchronize", c_int, [c_void_p]),
     ("hh_ctx_progress", c_int, [c_void_p, c_lp]),
+    ("hh_knobs_json", c_int, [c_int, ctypes.c_char_p, c_int, c_ip]),
     ("hh_op_create", c_int, [c_void_p, c_int, c_int, c_double, c_double, c_double, c_double,
                              c_double, c_dp, c_double, c_double, c_double, PP]),
     ("hh_op_destroy", c_int, [c_void_p]),

@@ -88,6 +88,17 @@ def unique_id() -> bytes:
     return bytes(buf)
 
 
+def knobs(only_changed: bool = True) -> dict:
+    """The library's HH_* knobs (hh_knobs_json): {name: {"value", "default"}} -- only those that
+    differ from the shipped path by default, so a default run reports {}."""
+    import json
+    need = ctypes.c_int()
+    check(lib.hh_knobs_json(int(only_changed), None, 0, ctypes.byref(need)))
+    buf = ctypes.create_string_buffer(need.value)
+    check(lib.hh_knobs_json(int(only_changed), buf, need.value, None))
+    return json.loads(buf.value.decode())
+
+
 def device_count() -> int:
     n = ctypes.c_int()
     check(lib.hh_device_count(ctypes.byref(n)))

@@ -738,30 +738,8 @@ using CycleTable = CTable<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16,
 
 // basis vectors whose re-read comes from the LDS copy: HH_FUSED_KEEP = 0 turns the copy off
 // (every re-read from the memory system), 17 (= kFusedKeepDefault, the only kept count built)
-// keeps it; any other value is refused.  Parsed again only when the variable's text changes,
-// so one process can still A/B it (tests/test_gpu_krylov_modes.py).
-int fused_keep() {
-  static thread_local std::string last = "\x01";
-  static thread_local int val = kFusedKeepDefault;
-  const char* e = std::getenv("HH_FUSED_KEEP");
-  const std::string cur = e ? e : "";
-  if (cur != last) {
-    last = cur;
-    if (cur.empty()) {
-      val = kFusedKeepDefault;
-    } else {
-      char* end = nullptr;
-      const long v = std::strtol(cur.c_str(), &end, 10);
-      if (*end != '\0' || (v != 0 && v != kFusedKeepDefault)) {
-        last = "\x01";
-        fail(HH_ERR_INVALID, "HH_FUSED_KEEP=%s: only 0 (no LDS copy) or %d (the built kept count)",
-             cur.c_str(), kFusedKeepDefault);
-      }
-      val = (int)v;
-    }
-  }
-  return val;
-}
+// keeps it; any other value is refused when the knobs are read (knobs.cpp).
+int fused_keep() { return (int)knobs().fused_keep; }
 template <int K>
 void fused_launch(const FusedArgs& a, int blocks, hipStream_t s) {
   if (a.sl) {
@@ -803,33 +781,18 @@ static_assert(kFusedMaxK == 20, "table covers 1..kFusedMaxK");
 
 }  // namespace
 
-// HH_FUSED_ALT=0 turns the alternating march off (A/B); read once
-constexpr bool kFusedAltDefault = true;  // config 2: +3.6 % (profiles/r05/r05b_ab_alt.log)
-bool fused_alt_dir() {
-  static const bool on = [] {
-    const char* e = std::getenv("HH_FUSED_ALT");
-    return e ? e[0] != '0' : kFusedAltDefault;
-  }();
-  return on;
-}
+// HH_FUSED_ALT=0 turns the alternating march off (A/B; on by default -- config 2: +3.6 %,
+// profiles/r05/r05b_ab_alt.log)
+bool fused_alt_dir() { return knobs().fused_alt != 0; }
 
 // One-pass column on one rank: the partial-row reduce and the lag step in one launch
 // (gmres_lag_red_kernel); HH_LAG_RED=0 keeps the two launches (A/B).
-bool lag_red_merge() {
-  static const bool on = [] {
-    const char* e = std::getenv("HH_LAG_RED");
-    return e ? e[0] != '0' : true;
-  }();
-  return on;
-}
+bool lag_red_merge() { return knobs().lag_red != 0; }
 
 // Band height: 8 rows at 1024^2, 32 at 4096^2 (profiles/r03t/r03s_ab_rows*), 64 from 8192^2;
 // HH_FUSED_ROWS overrides.  The partial rows (one per block) stay within kMaxStreamBlocks.
 int fused_iter_rows(int n, int rows) {
-  static const int env = [] {
-    const char* e = std::getenv("HH_FUSED_ROWS");
-    return e ? std::atoi(e) : 0;
-  }();
+  const int env = (int)knobs().fused_rows;
   const long tiles_x = (n + kT - 1) / kT;
   // (64 rows from n = 8192: 3 % fewer halo-row re-formations, +1.5 % at 8192^2,
   // profiles/r04/r04g_ab_rows_8192.log; at 4096^2 64-row bands leave too few tiles per CU)

@@ -357,17 +357,12 @@ static_assert(kFusedMaxK == 20, "table covers 1..kFusedMaxK");
 
 }  // namespace
 
-// HH_SLK: the smallest K that takes this kernel (0 = never), read once.  Default 2: at K = 1
+// HH_SLK (knobs.cpp): the smallest K that takes this kernel (0 = never).  Default 2: at K = 1
 // (two vectors) fused_sl_iter_kernel's two blocks per CU win, 336 vs 412 us at 4096^2; from
 // K = 4 this kernel does, 478 vs 493 us ... 1240 vs 1862 us at K = 19
 // (profiles/r05/r05e_slk0_tbps.txt, r05e_slk1_tbps.txt)
-constexpr int kSlkMinK = 2;
 int fused_slk_min_k() {
-  static const int v = [] {
-    const char* e = std::getenv("HH_SLK");
-    return e ? std::max(0, std::atoi(e)) : kSlkMinK;
-  }();
-  return v;
+  return (int)knobs().slk_min_k;
 }
 bool fused_slk_use(int K) {
   const int m = fused_slk_min_k();
@@ -376,10 +371,7 @@ bool fused_slk_use(int K) {
 // Band height: one band per CU where the grid allows (tiles_x * bands <= 256), at least 16
 // rows; HH_SLK_ROWS overrides.
 int fused_slk_rows(int n, int rows) {
-  static const int env = [] {
-    const char* e = std::getenv("HH_SLK_ROWS");
-    return e ? std::atoi(e) : 0;
-  }();
+  const int env = (int)knobs().slk_rows;
   const long tiles_x = (n + kT - 1) / kT;
   const long bands = std::max<long>(1, 256 / tiles_x);
   int R = env > 0 ? env : (int)std::max<long>(16, (rows + bands - 1) / bands);

@@ -722,10 +722,7 @@ hipError_t launch_one(const SmallCycleArgs& a, dim3 grid, dim3 block, size_t lds
   // Plain launch: co-residency is checked by the kernel's own gate (coresidency_gate), which
   // refuses a grid that cannot be resident before any state changes.  HH_SMALL_COOP=1 launches
   // cooperatively instead (the runtime's own residency check; ~55 us per launch), for A/B timing.
-  static const bool coop = [] {
-    const char* e = std::getenv("HH_SMALL_COOP");
-    return e && e[0] == '1' && !under_profiler();
-  }();
+  static const bool coop = knobs().small_coop == 1 && !under_profiler();
   if (!coop) {
     hipLaunchKernelGGL((gmres_small_cycle_kernel<C, J>), grid, block, lds, s, a);
     return hipGetLastError();
@@ -744,7 +741,7 @@ hipError_t launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi
   // at most 2 copies of the row's threads by default: 9.76-9.80 us/it at 128^2 against
   // 9.80-9.91 for 1 and 9.96-10.14 for 4 (the row-split update; block barriers of 8 waves)
   // (profiles/r02z_*); HH_SMALL_WIDE=c selects up to c copies, for A/B timing
-  static const int wide = getenv("HH_SMALL_WIDE") ? std::max(1, atoi(getenv("HH_SMALL_WIDE"))) : 2;
+  const int wide = (int)knobs().small_wide;
   const int threads = npad * std::max(1, std::min(wide, kSmallBlock / npad));
   const size_t lds = small_cycle_lds_bytes(a.n, a.restart);
   const dim3 grid(a.n + 1), block(threads);  // + the Givens workgroup

@@ -261,7 +261,6 @@ struct FusedArgs {
 // rocprofiler-sdk has finalised (tools/exit_probe.py), so the grid-wide sweeps and
 // the small-grid cycle then launch plainly (their waits are bounded either way); logged once.
 bool under_profiler();
-int check_halo_level();  // HH_CHECK_HALO (runtime.cpp check_site)
 constexpr int kFusedMaxK = 20;  // K <= this (restart <= kFusedMaxK + 1)
 // basis vectors whose projection re-read is served from the pass's own LDS copy (HH_FUSED_KEEP:
 // 0 = every re-read from the memory system, for A/B)
@@ -388,5 +387,17 @@ hipError_t launch_small_cycle(const SmallCycleArgs& a, bool const_c, bool jacobi
 // executed (g.ctrl[1] <= stop_col, read on the device); `merged`: a cycle that reached stop_col
 // was completed by the merged end instead (g.ctrl[2] = 1: the xupdate skips).
 void launch_gmres_solve(const GivensState& g, int stop_col, bool merged, hipStream_t stream);
+
+// Every HH_* environment knob, read once per process (knobs.cpp; the table there gives each
+// one's default -- the shipped path -- and meaning).  hh_ctx_create reads them first, so a
+// malformed value fails there; hh_knobs_json reports them.
+struct Knobs {
+  long fused_iter, sl_res, slk_min_k, slk_rows, fused_rows, fused_keep, fused_alt, lag_red,
+      cycle_merge, basis_pad, krylov_fuse, krylov_rev, tile_xcd;
+  long sweep_chain, sweep_graph, sweep_coop, sweep_diag;
+  long small_coop, small_wide, small_coop_refuse, small_refuse_at;
+  long check_halo, guard_halo;
+};
+const Knobs& knobs();
 
 }  // namespace hh

@@ -1,0 +1,114 @@
+// Every HH_* environment knob of the library, read ONCE per process into one struct (VERDICT r5
+// item 8: the A/B switches used to be function-static getenv calls spread over the kernels'
+// launchers, so a stray variable changed the credited kernel path silently).  hh_ctx_create reads
+// them (a malformed value fails the context there), and hh_knobs_json reports them -- bench.py
+// prints the ones that differ from the shipped path into its line's `config`.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "hh_error.hpp"
+#include "hh_internal.hpp"
+
+namespace hh {
+namespace {
+
+struct KnobDesc {
+  const char* name;
+  long Knobs::*field;
+  long def;
+  const char* what;
+};
+
+// name, field, shipped default, meaning (the DESIGN section that measured the choice)
+const KnobDesc kKnobs[] = {
+    {"HH_FUSED_ITER", &Knobs::fused_iter, 1, "one-pass GMRES iteration where it applies (3g)"},
+    {"HH_SL_RES", &Knobs::sl_res, 1, "shifted-Laplace residual in one pass (3g)"},
+    {"HH_SLK", &Knobs::slk_min_k, 2, "smallest K for fused_slk_kernel, 0 = never (3g)"},
+    {"HH_SLK_ROWS", &Knobs::slk_rows, 0, "fused_slk_kernel band height, 0 = by n"},
+    {"HH_FUSED_ROWS", &Knobs::fused_rows, 0, "one-pass band height, 0 = by n"},
+    {"HH_FUSED_KEEP", &Knobs::fused_keep, kFusedKeepDefault,
+     "basis vectors re-read from the pass's LDS copy: 0 or 17"},
+    {"HH_FUSED_ALT", &Knobs::fused_alt, 1, "odd bands march downwards (3g)"},
+    {"HH_LAG_RED", &Knobs::lag_red, 1, "one-rank reduce + lag step in one launch (3g)"},
+    {"HH_CYCLE_MERGE", &Knobs::cycle_merge, 1, "cycle end in one pass (3g)"},
+    {"HH_BASIS_PAD", &Knobs::basis_pad, 272, "complex elements between basis vectors"},
+    {"HH_KRYLOV_FUSE", &Knobs::krylov_fuse, 0, "regular cycle: last-block fused Krylov kernels"},
+    {"HH_KRYLOV_REV", &Knobs::krylov_rev, 1, "back-to-front cached update sweeps"},
+    {"HH_TILE_XCD", &Knobs::tile_xcd, 0, "per-XCD tile streams of the apply"},
+    {"HH_SWEEP_CHAIN", &Knobs::sweep_chain, 1, "sweeping M: persistent dense apply chain"},
+    {"HH_SWEEP_GRAPH", &Knobs::sweep_graph, 1, "sweeping M: GEMV chain replayed from a graph"},
+    {"HH_SWEEP_COOP", &Knobs::sweep_coop, 1, "sweeping M: cooperative grid-wide launches"},
+    {"HH_SWEEP_DIAG", &Knobs::sweep_diag, 0, "sweeping M: chain diagnostics"},
+    {"HH_SMALL_COOP", &Knobs::small_coop, 0, "small-grid cycle: cooperative launch"},
+    {"HH_SMALL_WIDE", &Knobs::small_wide, 2, "small-grid cycle: copies of a row's threads"},
+    {"HH_SMALL_COOP_REFUSE", &Knobs::small_coop_refuse, 0, "test hook: gate refuses every launch"},
+    {"HH_SMALL_REFUSE_AT", &Knobs::small_refuse_at, 0, "test hook: gate refuses launch k"},
+    {"HH_CHECK_HALO", &Knobs::check_halo, 0, "diagnostic: sync + attribute every rank site (4)"},
+    {"HH_GUARD_HALO", &Knobs::guard_halo, 0, "diagnostic: halo buffers against guard pages (4)"},
+};
+
+Knobs read_knobs() {
+  Knobs k{};
+  for (const KnobDesc& d : kKnobs) {
+    k.*(d.field) = d.def;
+    const char* e = std::getenv(d.name);
+    if (!e || !*e) continue;
+    char* end = nullptr;
+    const long v = std::strtol(e, &end, 10);
+    if (*end != '\0')
+      fail(HH_ERR_INVALID, "%s=%s: not an integer", d.name, e);
+    k.*(d.field) = v;
+  }
+  if (k.fused_keep != 0 && k.fused_keep != kFusedKeepDefault)
+    fail(HH_ERR_INVALID, "HH_FUSED_KEEP=%ld: only 0 (no LDS copy) or %d (the built kept count)",
+         k.fused_keep, kFusedKeepDefault);
+  if (k.slk_min_k < 0) k.slk_min_k = 0;
+  if (k.small_wide < 1) k.small_wide = 1;
+  if (k.basis_pad < 0) fail(HH_ERR_INVALID, "HH_BASIS_PAD=%ld must be >= 0", k.basis_pad);
+  return k;
+}
+
+}  // namespace
+
+const Knobs& knobs() {
+  static const Knobs k = read_knobs();  // (a throw leaves it uninitialised: the next call retries)
+  return k;
+}
+
+std::string knobs_json(bool only_changed) {
+  const Knobs& k = knobs();
+  std::string s = "{";
+  bool first = true;
+  for (const KnobDesc& d : kKnobs) {
+    const long v = k.*(d.field);
+    if (only_changed && v == d.def) continue;
+    char buf[192];
+    std::snprintf(buf, sizeof(buf), "%s\"%s\": {\"value\": %ld, \"default\": %ld}",
+                  first ? "" : ", ", d.name, v, d.def);
+    s += buf;
+    first = false;
+  }
+  return s + "}";
+}
+
+}  // namespace hh
+
+extern "C" __attribute__((visibility("default"))) int hh_knobs_json(int only_changed, char* buf,
+                                                                     int cap, int* needed) {
+  try {
+    REQUIRE(buf || cap == 0, "null buffer");
+    const std::string s = hh::knobs_json(only_changed != 0);
+    if (needed) *needed = (int)s.size() + 1;
+    if (cap > 0) {
+      const size_t m = std::min<size_t>(s.size(), (size_t)cap - 1);
+      std::memcpy(buf, s.data(), m);
+      buf[m] = '\0';
+    }
+  } catch (const hh::Error& e) {
+    return e.code;
+  }
+  return HH_OK;
+}

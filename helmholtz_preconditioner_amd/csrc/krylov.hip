@@ -673,11 +673,7 @@ constexpr size_t kSmallKrylovLen = (size_t)2 << 20;  // rank-local unknowns
 bool krylov_nt(size_t len) { return g_krylov_nt < 0 ? len > kSmallKrylovLen : g_krylov_nt != 0; }
 // back-to-front update sweeps with cached loads (HH_KRYLOV_REV=0 turns them off: diagnostic)
 bool krylov_rev() {
-  static const bool rev = [] {
-    const char* e = std::getenv("HH_KRYLOV_REV");
-    return !(e && e[0] == '0');
-  }();
-  return rev;
+  return knobs().krylov_rev != 0;
 }
 
 template <int K>

@@ -61,17 +61,9 @@ std::vector<std::pair<void*, GuardMap>>& guard_registry() {
 }
 }  // namespace
 
-bool guard_halo() {
-  static const bool on = [] {
-    const char* e = std::getenv("HH_GUARD_HALO");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 template <class T>
 static T* dalloc_guarded(size_t count, int device, bool at_end) {
-  if (!guard_halo()) return dalloc<T>(count);
+  if (knobs().guard_halo == 0) return dalloc<T>(count);
   const size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
   hipMemAllocationProp prop{};
   prop.type = hipMemAllocationTypePinned;
@@ -131,16 +123,6 @@ static cd s2(double x, double C, double eta, cd om) {
   return 1.0 / (1.0 + cd(0, 1) * sigma2(x, C, eta) / om);
 }
 static double2 d2(cd z) { return make_double2(z.real(), z.imag()); }
-
-// HH_CHECK_HALO: 0 (default) off, 1 synchronise + attribute at every multi-rank site
-// (runtime.cpp check_site), 2 also trace each site
-int check_halo_level() {
-  static const int lvl = [] {
-    const char* e = std::getenv("HH_CHECK_HALO");
-    return e ? std::atoi(e) : 0;
-  }();
-  return lvl;
-}
 
 bool under_profiler() {
   static const bool on = [] {
@@ -300,10 +282,7 @@ struct hh_op {
   // kernels.  Off by default: measured no faster at 1024^2 (update+column 8 975-9 077 vs 8 878-
   // 9 105 it/s unfused; multidot+reduce 8 219 -- its last block's reduction is a serial chain
   // of device-scope loads; profiles/r02c2e_fuse_ab.log)
-  int fuse_krylov = [] {
-    const char* e = std::getenv("HH_KRYLOV_FUSE");
-    return e ? std::atoi(e) : 0;
-  }();
+  int fuse_krylov = (int)knobs().krylov_fuse;
   // timing hooks
   hipEvent_t tk0 = nullptr, tk1 = nullptr;
   // device stop flag of the GMRES cycle being queued (nullptr outside hh_gmres)
@@ -380,7 +359,7 @@ void tspan(hh_op* op, int cat, hipEvent_t a, hipEvent_t b, bool clamp = false) {
 // it, so it also tells a hazard between the halo and compute streams (passes when checked) from
 // a fault of one launch (reported at its own site).
 void check_site(const hh_ctx* c, const char* site, hipStream_t s) {
-  const int lvl = check_halo_level();
+  const long lvl = knobs().check_halo;
   if (lvl == 0) return;
   static thread_local long count = 0;
   ++count;
@@ -697,11 +676,7 @@ void sweep_apply(hh_op* op, const double2* r, double2* out, bool asis) {
     ChainArgs c{};
     c.gbuf = op->sw_chain;
     c.timeout = reinterpret_cast<unsigned*>(op->red + kRedTimeout);
-    static const int diag = [] {
-      const char* e = std::getenv("HH_SWEEP_DIAG");
-      return e ? std::atoi(e) : 0;
-    }();
-    c.diag = diag;
+    c.diag = (int)knobs().sweep_diag;
     c.seq = (++op->sw_seq) & 0xfffffu;
     if (c.seq == 0) c.seq = op->sw_seq = 1;  // (tag 0 is the zeroed buffer)
     launch_sweep_dense_apply(a, op->sw_T, r, out, op->sw_u, asis ? 1 : 0, s, &c);
@@ -714,11 +689,7 @@ void sweep_apply(hh_op* op, const double2* r, double2* out, bool asis) {
     const int am = asis ? 1 : 0;
     // HH_SWEEP_GRAPH=0: eager launches of the same kernels (profilers that cannot follow
     // graph replays)
-    static const bool use_graph = [] {
-      const char* e = std::getenv("HH_SWEEP_GRAPH");
-      return !(e && e[0] == '0');
-    }();
-    if (!use_graph) {
+    if (knobs().sweep_graph == 0) {
       SweepArgs a = op->sweep;
       a.stop = op->stop_flag;
       launch_sweep_dense_apply(a, op->sw_T, r, out, op->sw_u, am, s);
@@ -846,11 +817,7 @@ void norm2(hh_op* op, const double2* v, int dst) {
 // order.  Independent of the M A fusion switch (hh_op_set_sl_fusion: that A/B stays
 // bit-identical).
 bool sl_res_fused(const hh_op* op) {
-  static const bool on = [] {
-    const char* e = std::getenv("HH_SL_RES");
-    return !(e && e[0] == '0');
-  }();
-  return on && op->points == 5 && op->sweeps == 2 && op->sl_ext_ok;
+  return knobs().sl_res != 0 && op->points == 5 && op->sweeps == 2 && op->sl_ext_ok;
 }
 
 // run_sl2's structure: a band reads x AND b two rows beyond itself -- in place from a
@@ -999,13 +966,7 @@ void read_dev(hh_op* op, const double* dsrc, double* hdst, int count) {
 }
 
 // the one-pass iteration where it applies, unless HH_FUSED_ITER=0
-bool fused_default() {
-  static const bool on = [] {
-    const char* e = std::getenv("HH_FUSED_ITER");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+bool fused_default() { return knobs().fused_iter != 0; }
 
 // One pass of the one-pass GMRES iteration (fused.hip) over the rank's slabs: u_K = w_{K-1} -
 // sum_k c_k u_k into V[K], w_K = M A (s_K u_K) into wout, and the partial rows of the next
@@ -1157,13 +1118,7 @@ void check_sweep_chain(hh_op* op) {
 // at 8192^2): 4 KiB + 256 B between them measured +3 % for the one-pass iteration at 8192^2
 // (316.6 -> 326.0 it/s; 256 B +1.5 %, 2.3 / 8.3 / 64.3 KiB +1.5-2.5 %,
 // profiles/r04/r04h_ab_pad_c4.log, r04i_ab_nt_c4.log)
-size_t basis_pad() {
-  static const size_t pad = [] {
-    const char* e = std::getenv("HH_BASIS_PAD");
-    return e ? (size_t)std::atol(e) : (size_t)272;
-  }();
-  return pad;
-}
+size_t basis_pad() { return (size_t)knobs().basis_pad; }
 
 void ensure_gmres(hh_op* op, int restart) {
   REQUIRE(restart >= 1 && restart <= kMaxProj - 1, "restart must be in [1, %d]", kMaxProj - 1);
@@ -1253,6 +1208,7 @@ HH_API int hh_ctx_create_ex(int device, int rank, int world, const unsigned char
   REQUIRE(world == 1 || id, "world > 1 needs a communicator id from rank 0");
   REQUIRE(transport == TRANSPORT_RCCL || transport == TRANSPORT_SHM, "unknown transport %d",
           transport);
+  (void)knobs();  // every HH_* knob read here, once per process (a malformed one fails here)
   int ndev = 0;
   HIPC(hipGetDeviceCount(&ndev));
   REQUIRE(device >= 0 && device < ndev, "device %d not present (%d devices)", device, ndev);
@@ -1597,10 +1553,7 @@ HH_API int hh_op_local_rows(hh_op* op, int* j_begin, int* j_end) {
 // The persistent apply chain of the dense form (sweep_dense.hip sweep_chain_kernel) where it
 // fits, unless mode 2 (one launch per GEMV, replayed from a graph) or HH_SWEEP_CHAIN=0.
 static void sweep_chain_configure(hh_op* op) {
-  static const bool chain_env = [] {
-    const char* e = std::getenv("HH_SWEEP_CHAIN");
-    return !(e && e[0] == '0');
-  }();
+  const bool chain_env = knobs().sweep_chain != 0;
   int cus = 0;
   HIPC(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, op->ctx->device));
   const bool want = op->sw_T && op->sw_mode != 2 && chain_env && sweep_chain_fits(op->n, cus);
@@ -2459,11 +2412,7 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
   // the end of a full one-pass cycle in one pass over the basis (fused.hip cycle_end_kernel:
   // the last update's norm, x += V a and V b together; HH_CYCLE_MERGE=0: update, then the
   // triangular solve and xupdate)
-  static const bool merge_env = [] {
-    const char* e = std::getenv("HH_CYCLE_MERGE");
-    return !(e && e[0] == '0');
-  }();
-  const bool merge_end = fused && merge_env;
+  const bool merge_end = fused && knobs().cycle_merge != 0;
   double r0 = bnrm2;  // (x0 = 0: r = b)
   if (x_any) {
     residual(op, b, x, V, 4);  // V[0] = M (b - A x0); red[4..5]
@@ -2565,14 +2514,8 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
         sa.gate_arrive = reinterpret_cast<unsigned*>(sa.gate_decide + 1);
         // test hooks: the gate refuses every launch (HH_SMALL_COOP_REFUSE=1), or only the
         // solve's launch number HH_SMALL_REFUSE_AT (1-based: 2 = the second batch)
-        static const bool force_abort = [] {
-          const char* e = std::getenv("HH_SMALL_COOP_REFUSE");
-          return e && e[0] == '1';
-        }();
-        static const long refuse_at = [] {
-          const char* e = std::getenv("HH_SMALL_REFUSE_AT");
-          return e ? std::atol(e) : 0L;
-        }();
+        const bool force_abort = knobs().small_coop_refuse != 0;
+        const long refuse_at = knobs().small_refuse_at;
         ++launches;
         sa.gate_force_abort = (force_abort || launches == refuse_at) ? 1 : 0;
         // P consecutive sequence numbers, none 0 (tag 0 is the zeroed scratch)

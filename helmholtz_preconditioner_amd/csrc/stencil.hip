@@ -856,10 +856,7 @@ int stencil_resolve_variant(int epi, int requested, int n) {
 // TB/s): the plain order's cross-XCD halo re-reads are served by the Infinity Cache, not HBM
 // (FETCH_SIZE counts both), while eight separate per-XCD streams cost DRAM locality.
 bool tile_xcd_map(int tiles_x) {
-  static const bool on = [] {
-    const char* e = std::getenv("HH_TILE_XCD");
-    return e && e[0] == '1';
-  }();
+  const bool on = knobs().tile_xcd == 1;
   (void)tiles_x;
   return on;
 }

@@ -1337,10 +1337,7 @@ bool sweep_part_ys_lds(int B, int G, int n) {
 size_t sweep_part_granules(int G) { return (size_t)2 * 2 * G * kSweepGranStride; }
 
 bool sweep_coop_launch() {
-  static const bool coop = [] {
-    const char* e = std::getenv("HH_SWEEP_COOP");
-    return !(e && e[0] == '0') && !under_profiler();
-  }();
+  static const bool coop = knobs().sweep_coop != 0 && !under_profiler();
   return coop;
 }
 

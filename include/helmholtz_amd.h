@@ -106,6 +106,11 @@ int hh_ctx_synchronize(hh_ctx* ctx);
  * one that stopped (bench.py's watchdog reads it from its own thread while the main thread may
  * be blocked inside a collective: the read takes no lock and touches no device). */
 int hh_ctx_progress(hh_ctx* ctx, long* collectives);
+/* The library's HH_* environment knobs (A/B switches and diagnostics), read once per process,
+ * as a JSON object {"HH_X": {"value": v, "default": d}, ...}: all of them, or (only_changed)
+ * those that differ from the shipped path -- an empty object for a default run.  Writes at most
+ * cap bytes (NUL-terminated); *needed (nullable) receives the full size. */
+int hh_knobs_json(int only_changed, char* buf, int cap, int* needed);
 
 /* --------------------------------------------------------------- operator */
 /* Replaces build_A_matrix(b, const, eta, omega, h, n, c_mat), code.py:202-219

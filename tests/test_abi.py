@@ -59,3 +59,35 @@ def test_error_message_roundtrip():
     rc = _ffi.lib.hh_ctx_create(0, 3, 2, None, 1, ctypes.byref(ctypes.c_void_p()))
     assert rc == -1  # HH_ERR_INVALID: rank >= world
     assert b"rank" in _ffi.lib.hh_last_error()
+
+
+_KNOB_CHILD = ("import sys, json; sys.path.insert(0, sys.argv[1]); "
+               "import helmholtz_preconditioner_amd as H; print(json.dumps(H.knobs()))")
+
+
+@pytest.mark.parametrize("env,want", [({}, {}),
+                                      ({"HH_LAG_RED": "0", "HH_SLK": "3"},
+                                       {"HH_LAG_RED": 0, "HH_SLK": 3}),
+                                      ({"HH_CYCLE_MERGE": "1"}, {})])
+def test_knobs_read_once_and_reported(env, want):
+    """Every HH_* knob is read once into one struct (knobs.cpp) and reported by hh_knobs_json:
+    only those off the shipped path (bench.py prints them into its line's config), so a default
+    run reports {} and a knob set to its default is not reported either."""
+    import json
+    import subprocess
+    import sys
+    clean = {k: v for k, v in os.environ.items() if not k.startswith("HH_")}
+    r = subprocess.run([sys.executable, "-c", _KNOB_CHILD, ROOT], env=dict(clean, **env),
+                       capture_output=True, text=True, timeout=120, check=True)
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    assert {k: v["value"] for k, v in got.items()} == want
+
+
+@pytest.mark.parametrize("env,msg", [({"HH_FUSED_KEEP": "4"}, "HH_FUSED_KEEP=4"),
+                                     ({"HH_SLK": "two"}, "HH_SLK=two: not an integer")])
+def test_malformed_knob_fails_loudly(env, msg):
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, "-c", _KNOB_CHILD, ROOT], env=dict(os.environ, **env),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and msg in r.stderr, r.stderr[-2000:]

@@ -223,48 +223,55 @@ def test_fused_pass_is_the_single_rank_default(ctx):
     assert B.last_solve_path() == "regular"
 
 
+_KEEP_CHILD = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import helmholtz_preconditioner_amd as H
+n, kind, out = int(sys.argv[2]), sys.argv[3], sys.argv[4]
+om, h, eta = H.problem_params(n, 12, n / 40.0, 2.0)
+cm = H.marmousi_like_c_mat(n) if kind == "marmousi" else H.init_c1_mat(.5, .5, n)
+A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm)
+A.krylov_mode("fused")
+f = H.init_f1_mat(.5, .125, om, n).ravel()
+hist = []
+x, info = H.gmres(A, f, rtol=1e-12, restart=21, maxiter=25, M="jacobi", callback=hist.append,
+                  callback_type="legacy")
+assert A.last_solve_path() == "one-pass"
+np.savez(out, x=x, hist=np.array(hist), knobs=str(H.knobs()))
+'''
+
+
 @pytest.mark.parametrize("n,kind", [(300, "c1"), (1100, "marmousi")])
-def test_fused_pass_lds_kept_basis_is_bit_identical(ctx, n, kind, monkeypatch):
-    """HH_FUSED_KEEP (read per launch): the projections' re-read of the first 17 basis vectors
-    from the pass's own one-row LDS copy (the default) instead of the memory system (0) reads
-    the same values in the same order -- histories and fields bit-identical (K up to 20: the
-    kept and re-read vectors mixed in one pass)"""
-    om, h, eta = O.problem_params(n, 12, n / 40.0, 2.0)
-    cm = medium(kind, n) if kind != "marmousi" else H.marmousi_like_c_mat(n)
-    A = H.build_A_matrix(12, 81.0, eta, om, h, n, cm, context=ctx)
-    f = O.init_f1_mat(.5, .125, om, n).ravel()
-    A.krylov_mode("fused")
+def test_fused_pass_lds_kept_basis_is_bit_identical(tmp_path, n, kind):
+    """HH_FUSED_KEEP (read once per process, knobs.cpp): the projections' re-read of the first
+    17 basis vectors from the pass's own one-row LDS copy (the default) instead of the memory
+    system (0) reads the same values in the same order -- histories and fields bit-identical
+    (K up to 20: the kept and re-read vectors mixed in one pass)"""
+    import subprocess
+    import sys
     out = []
     for keep in ("0", "17"):
-        monkeypatch.setenv("HH_FUSED_KEEP", keep)
-        hist = []
-        x, info = H.gmres(A, f, rtol=1e-12, restart=21, maxiter=25, M="jacobi",
-                          callback=hist.append, callback_type='legacy')
-        assert A.last_solve_path() == "one-pass"
-        out.append((x, np.array(hist)))
-    A.krylov_mode("auto")
-    for x, hh in out[1:]:
-        assert np.array_equal(hh, out[0][1])
-        assert np.array_equal(x, out[0][0])
+        o = tmp_path / f"k{keep}.npz"
+        subprocess.run([sys.executable, "-c", _KEEP_CHILD, ROOT, str(n), kind, str(o)],
+                       env=dict(os.environ, HH_FUSED_KEEP=keep), check=True, timeout=240)
+        out.append(np.load(o))
+    # the child reports the knob it ran with (hh_knobs_json: only values off the default)
+    assert "HH_FUSED_KEEP" in str(out[0]["knobs"]) and str(out[1]["knobs"]) == "{}"
+    assert np.array_equal(out[1]["hist"], out[0]["hist"])
+    assert np.array_equal(out[1]["x"], out[0]["x"])
 
 
-def test_fused_keep_knob_refuses_unbuilt_counts(ctx, monkeypatch):
+def test_fused_keep_knob_refuses_unbuilt_counts():
     """HH_FUSED_KEEP selects between the two built forms (0: no LDS copy, 17: the default);
-    any other count (round 3's A/B values 4, 8) is refused with an error instead of silently
-    running 17"""
-    n = 300
-    om, h, eta = O.problem_params(n, 12, n / 40.0, 2.0)
-    A = H.build_A_matrix(12, 81.0, eta, om, h, n, medium("c1", n), context=ctx)
-    A.krylov_mode("fused")
-    A.small_cycle("off")
-    f = O.init_f1_mat(.5, .125, om, n).ravel()
-    monkeypatch.setenv("HH_FUSED_KEEP", "4")
-    with pytest.raises(H.HHError, match="HH_FUSED_KEEP"):
-        H.gmres(A, f, rtol=1e-12, restart=20, maxiter=3, M="jacobi")
-    monkeypatch.setenv("HH_FUSED_KEEP", "0")
-    H.gmres(A, f, rtol=1e-12, restart=20, maxiter=3, M="jacobi")
-    assert A.last_solve_path() == "one-pass"
-    A.krylov_mode("auto")
+    any other count (round 3's A/B values 4, 8) is refused -- since round 6 when the knobs are
+    read, at the first context -- instead of silently running 17 (ADVICE r04)"""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, sys.argv[1]); import helmholtz_preconditioner_amd as H; "
+            "H.Context(device=0)")
+    r = subprocess.run([sys.executable, "-c", code, ROOT], env=dict(os.environ, HH_FUSED_KEEP="4"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "HH_FUSED_KEEP=4" in r.stderr, r.stderr[-2000:]
 
 
 @pytest.mark.parametrize("n,slabs", [(150, 2), (300, 3), (613, 4)])
