@@ -277,6 +277,12 @@ bool fused_alt_dir();
 bool lag_red_merge();  // HH_LAG_RED (default on)
 int fused_slk_rows(int n, int rows);
 void launch_fused_slk(int K, const FusedArgs& a, int blocks, hipStream_t stream);
+// the shifted-Laplace pass in the standalone fused M A's shape (fused_slv.hip: overlapping
+// strips, no edge waves, four waves per SIMD, the projections' basis rows re-read from L2): used
+// for K <= HH_SLV; its grid (252 output columns per strip)
+bool fused_slv_use(int K);
+int fused_slv_blocks(int n, int bands);
+void launch_fused_slv(int K, const FusedArgs& a, int blocks, hipStream_t stream);
 // u_K on rows [r0, r0 + c0) and [r1, r1 + c1) of a.V / a.win (rank-local), written to a.uout:
 // the rows a neighbouring rank's pass reads as its halo (fused_iter_kernel's arithmetic)
 void launch_fused_edge(int K, const FusedArgs& a, int r0, int c0, int r1, int c1,
@@ -392,7 +398,7 @@ void launch_gmres_solve(const GivensState& g, int stop_col, bool merged, hipStre
 // one's default -- the shipped path -- and meaning).  hh_ctx_create reads them first, so a
 // malformed value fails there; hh_knobs_json reports them.
 struct Knobs {
-  long fused_iter, sl_res, slk_min_k, slk_rows, fused_rows, fused_keep, fused_alt, lag_red,
+  long fused_iter, sl_res, slk_min_k, slv_max_k, slk_rows, fused_rows, fused_keep, fused_alt, lag_red,
       cycle_merge, basis_pad, krylov_fuse, krylov_rev, tile_xcd;
   long sweep_chain, sweep_graph, sweep_coop, sweep_diag;
   long small_coop, small_wide, small_coop_refuse, small_refuse_at;

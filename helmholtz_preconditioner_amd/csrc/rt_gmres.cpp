@@ -29,7 +29,8 @@ int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double*
   double2* uout = op->V + (size_t)K * ldv;
   const int width = 2 * (K + 1) + 2;
   const int rows_rank = op->je - op->jb;
-  const bool slk = sl && fused_slk_use(K);
+  const bool slv = sl && fused_slv_use(K);
+  const bool slk = sl && !slv && fused_slk_use(K);
   const int R = slk ? fused_slk_rows(n, rows_rank) : fused_iter_rows(n, rows_rank);
   FusedArgs base{};
   base.ldv = ldv;
@@ -68,10 +69,12 @@ int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double*
     a.row_step = step;
     a.bands = step > 0 ? (r1 - r0 - 1) / step + 1 : (r1 - r0 + rows - 1) / rows;
     a.partials = op->partials + (size_t)nparts * width;
-    const int blocks = fused_iter_blocks(n, a.bands);
+    const int blocks = slv ? fused_slv_blocks(n, a.bands) : fused_iter_blocks(n, a.bands);
     REQUIRE((size_t)(nparts + blocks) * width <= op->partials_cap,
             "partials workspace too small for the one-pass iteration (%d blocks)", nparts + blocks);
-    if (slk)
+    if (slv)
+      launch_fused_slv(K, a, blocks, st);
+    else if (slk)
       launch_fused_slk(K, a, blocks, st);
     else
       launch_fused_iter(K, a, blocks, st);
