@@ -452,14 +452,21 @@ FUSED_TRAFFIC_DB = "profiles/r05_pmc_fused.json"
 # the environment knobs that change the one-pass kernels' traffic: a record applies only to a run
 # with the same values (unset = the build's default)
 FUSED_KNOBS = ("HH_FUSED_ITER", "HH_FUSED_KEEP", "HH_FUSED_ROWS", "HH_BASIS_PAD", "HH_SLK",
-               "HH_SLK_ROWS", "HH_CYCLE_MERGE", "HH_FUSED_ALT")
+               "HH_SLV", "HH_SLK_ROWS", "HH_CYCLE_MERGE", "HH_FUSED_ALT")
+SL_ONLY_KNOBS = ("HH_SLK", "HH_SLV", "HH_SLK_ROWS")
 
 
-def fused_knobs():
-    """the run's values of FUSED_KNOBS that differ from the shipped path (the library's own
-    reading, hh_knobs_json)"""
+def fused_knobs(rec_knobs=None, precond="sl"):
+    """FUSED_KNOBS with their effective values (the library's reading, hh_knobs_json): this
+    run's, or -- rec_knobs given -- a record's (knobs it does not name at their default); the
+    shifted-Laplace-only knobs are dropped for the other preconditioners"""
     import helmholtz_preconditioner_amd as H
-    return {k: str(v["value"]) for k, v in H.knobs().items() if k in FUSED_KNOBS}
+    allk = H.knobs(only_changed=False)
+    if rec_knobs is None:
+        eff = {k: str(allk[k]["value"]) for k in FUSED_KNOBS}
+    else:
+        eff = {k: str(rec_knobs.get(k, allk[k]["default"])) for k in FUSED_KNOBS}
+    return {k: v for k, v in eff.items() if precond == "sl" or k not in SL_ONLY_KNOBS}
 
 
 def fused_pass_traffic(n, rows, medium, precond, restart):
@@ -474,7 +481,7 @@ def fused_pass_traffic(n, rows, medium, precond, restart):
         return None, None, None
     key = f"n{n}_rows{rows}_{medium}_{precond}_r{restart}"
     rec = json.load(open(path)).get(key)
-    if not rec or rec.get("knobs", {}) != fused_knobs():
+    if not rec or fused_knobs(rec.get("knobs", {}), precond) != fused_knobs(None, precond):
         return None, None, None
     return rec["ratio"], rec["per_K"], f"{FUSED_TRAFFIC_DB}[{key}]: {rec['source']}"
 

@@ -227,6 +227,8 @@ __device__ __forceinline__ void slv_band(const FusedArgs& a, const BandV bd, dou
   }
 }
 
+// (Holding the allocation to four waves per SIMD at K <= 2 -- 128 VGPRs, 10-16 of them spilled
+// -- measured slower: K = 1 291 vs 242 us, K = 2 479 vs 331 us; profiles/r06/r06i_*)
 template <int K, bool CONSTC>
 __global__ __launch_bounds__(kT) void fused_slv_kernel(const FusedArgs a) {
   if (a.stop && *a.stop) return;

@@ -27,7 +27,7 @@ const KnobDesc kKnobs[] = {
     {"HH_FUSED_ITER", &Knobs::fused_iter, 1, "one-pass GMRES iteration where it applies (3g)"},
     {"HH_SL_RES", &Knobs::sl_res, 1, "shifted-Laplace residual in one pass (3g)"},
     {"HH_SLK", &Knobs::slk_min_k, 2, "smallest K for fused_slk_kernel, 0 = never (3g)"},
-    {"HH_SLV", &Knobs::slv_max_k, 0, "largest K for fused_slv_kernel, 0 = never (3g)"},
+    {"HH_SLV", &Knobs::slv_max_k, 4, "largest K for fused_slv_kernel, 0 = never (3g)"},
     {"HH_SLK_ROWS", &Knobs::slk_rows, 0, "fused_slk_kernel band height, 0 = by n"},
     {"HH_FUSED_ROWS", &Knobs::fused_rows, 0, "one-pass band height, 0 = by n"},
     {"HH_FUSED_KEEP", &Knobs::fused_keep, kFusedKeepDefault,

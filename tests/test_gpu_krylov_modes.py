@@ -484,3 +484,29 @@ def test_fused_pass_alternating_march_matches(tmp_path, n, kind, pc):
     assert np.max(np.abs(a["hist"][:5] - b["hist"][:5]) / a["hist"][:5]) < 1e-10
     assert np.max(np.abs(a["hist"] - b["hist"]) / a["hist"]) < TOL
     assert relerr(b["x"], a["x"]) < TOL
+
+
+@pytest.mark.parametrize("n,kind,slabs", [(300, "c1", 1), (257, "marmousi", 3), (1100, "marmousi", 1),
+                                          (613, "c1", 2)])
+def test_fused_sl_overlapping_strip_kernel_matches(tmp_path, n, kind, slabs):
+    """fused_slv.hip (the shifted-Laplace pass in the standalone fused M A's shape: overlapping
+    252-column strips, no edge waves; HH_SLV = the largest K it takes) against the edge-wave
+    kernels (HH_SLV=0: fused_sl_iter_kernel / fused_slk_kernel) on the same problem: the same
+    operator and preconditioner arithmetic, only the strip-edge columns' u_K (k order here, a
+    shuffle tree there) and the projections' summation order differ -- the first iterations to
+    rounding, the 25-iteration history (K = 1 .. 20: both kernels in one cycle, then a second
+    cycle) and the field within the parity contract; ragged strips, virtual slabs."""
+    import subprocess
+    import sys
+    res = []
+    for slv in ("0", "6"):
+        out = tmp_path / f"slv{slv}.npz"
+        env = dict(os.environ, HH_SLV=slv)
+        subprocess.run([sys.executable, "-c", _SLK_CHILD, ROOT, str(n), kind, str(slabs), "21",
+                        "25", str(out)], env=env, check=True, timeout=240)
+        res.append(np.load(out))
+    a, b = res
+    assert int(a["info"]) == int(b["info"]) and len(a["hist"]) == len(b["hist"]) == 25
+    assert np.max(np.abs(a["hist"][:5] - b["hist"][:5]) / a["hist"][:5]) < 1e-10
+    assert np.max(np.abs(a["hist"] - b["hist"]) / a["hist"]) < TOL
+    assert relerr(b["x"], a["x"]) < TOL

@@ -11,7 +11,7 @@ N = n * n
 rows = []
 with open(path) as fh:
     for r in csv.DictReader(fh):
-        m = re.search(r"fused_(sl_iter|slk|iter)_kernel<(\d+)", r["Name"])
+        m = re.search(r"fused_(sl_iter|slk|slv|iter)_kernel<(\d+)", r["Name"])
         if m:
             K = int(m.group(2))
             ns = float(r["AverageNs"])

@@ -20,9 +20,9 @@ from collections import defaultdict
 def load(path):
     acc = defaultdict(list)
     for r in csv.DictReader(open(path)):
-        m = re.search(r"fused_(sl_iter|slk|iter)_kernel<(\d+)", r["Kernel_Name"])
+        m = re.search(r"fused_(sl_iter|slk|slv|iter)_kernel<(\d+)", r["Kernel_Name"])
         if m:
-            tag = "" if m.group(1) == "iter" else "sl_"  # (both shifted-Laplace kernels: "sl")
+            tag = "" if m.group(1) == "iter" else "sl_"  # (every shifted-Laplace kernel: "sl")
             acc[(tag, int(m.group(2)))].append(float(r["Counter_Value"]) * 1024.0)
     return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
