@@ -150,7 +150,8 @@ int stencil_bands(int rows, int rows_per_block, int row_step);  // tiles along j
 // rows per side and the extended tables (StencilArgs, fused SL fields); a.tab_r2x != nullptr
 // selects the 9-point operator.
 void launch_sl2(bool const_c, const StencilArgs& a, hipStream_t stream, int variant = -1);
-// v0 = M (b - A x) for the two-sweep shifted Laplace in one pass (5-point, one rank): a.u = x,
+// v0 = M (b - A x) for the two-sweep shifted Laplace in one pass (5-point; one slab's rows -- across
+// slabs and ranks runtime's run_sl2_res supplies b's and x's two rows beyond it): a.u = x,
 // a.in1 / in1_lo / in1_hi = b, a.out0 = v0; per block |r|^2 and |M r|^2 into a.partials
 // (width kMaxNorms).  Returns the blocks launched (the partial rows written).
 int launch_sl2_res(bool const_c, const StencilArgs& a, hipStream_t stream);
@@ -269,7 +270,8 @@ int fused_iter_rows(int n, int rows);  // band height for a slab of `rows` rows
 int fused_iter_blocks(int n, int bands);
 void launch_fused_iter(int K, const FusedArgs& a, int blocks, hipStream_t stream);
 // the shifted-Laplace pass with the whole basis window on chip (fused_slk.hip; one block per
-// CU): used for K >= HH_SLK (default 1; 0 = never), with its own band height
+// CU): used for K >= HH_SLK (default 2; 0 = never) above fused_slv's range, with its own band
+// height
 bool fused_slk_use(int K);
 // fused_iter_kernel's odd bands march downwards (HH_FUSED_ALT, read once), so the halo rows a
 // band re-forms are read while their owners read them too (fused.hip)

@@ -167,10 +167,11 @@ __global__ __launch_bounds__(kT) void update_kernel(const double2* __restrict__ 
 
 // x += sum_k y_k V_k (NT: the basis is dead after this pass; non-temporal loads at 4096^2).
 // ctl (the cycle's control words, nullable): ctl[2] != 0 skips the update (the merged cycle end
-// already applied it); otherwise only the ctl[1] + 1 vectors of the executed columns count --
-// the rest get coefficient 0 and re-read the last counted vector (finite, and cached: the
-// vectors past an early stop may never have been written), so the update of a cycle that
-// stopped early needs no host round trip for its length.  Full cycles: ctl[1] + 1 == K.
+// already applied it); otherwise only the ctl[1] + 1 vectors of the executed columns are read
+// (a block-uniform bound: the vectors past an early stop may never have been written, and
+// since round 6 they are not loaded at all -- ADVICE r05: the re-reads of the last counted
+// vector with coefficient 0 cost up to K / kc times the bytes under NT loads), so the update of
+// a cycle that stopped early needs no host round trip for its length.  Full cycles: kc == K.
 template <int K, bool NT>
 __global__ __launch_bounds__(kT) void xupdate_kernel(const double2* __restrict__ V, size_t ldv,
                                                      const double2* __restrict__ y,
@@ -179,17 +180,17 @@ __global__ __launch_bounds__(kT) void xupdate_kernel(const double2* __restrict__
   int kc = K;
   if (ctl) {
     if (ctl[2]) return;
-    kc = min(max(ctl[1] + 1, 1), K);
+    kc = __builtin_amdgcn_readfirstlane(min(max(ctl[1] + 1, 1), K));  // (uniform)
   }
   double2 c[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) c[k] = k < kc ? y[min(k, kc - 1)] : make_double2(0.0, 0.0);
+  for (int k = 0; k < K; ++k) c[k] = k < kc ? y[k] : make_double2(0.0, 0.0);
   const size_t stride = (size_t)gridDim.x * kT;
   for (size_t p = (size_t)blockIdx.x * kT + threadIdx.x; p < len; p += stride) {
     double2 t = make_double2(0.0, 0.0);
 #pragma unroll
     for (int k = 0; k < K; ++k)
-      t = cfma(c[k], ldnt<NT>(V + (size_t)min(k, kc - 1) * ldv + p), t);
+      if (k < kc) t = cfma(c[k], ldnt<NT>(V + (size_t)k * ldv + p), t);
     x[p] = cadd(x[p], t);
   }
 }

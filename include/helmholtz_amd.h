@@ -204,6 +204,10 @@ int hh_op_time_apply_set(hh_op* op, const hh_vec* const* xs, hh_vec* const* ys, 
  *         (hh_op_set_small_cycle) queues up to 16 restart cycles per host synchronisation, so
  *         x may be up to 15 cycles past the iteration the callback stopped at (scipy's callers
  *         never see x in that case either: the exception propagates).
+ *   x after HH_ERR_STATE is unspecified too: a cycle's end (the x update and the next
+ *         residual) is queued before the host reads the cycle's report, so a grid-wide wait of
+ *         the sweeping preconditioner that timed out (reported as HH_ERR_STATE) is detected
+ *         after x has been updated from that cycle's garbage.
  * On every exit path -- success, error or abort -- the operator is left ready for plain
  * applies (no stale in-solve state). */
 typedef int (*hh_gmres_callback)(void* user, long iteration, double rel_presid);

@@ -362,7 +362,7 @@ def test_fused_cycle_end_merge_matches_solve_and_xupdate(tmp_path, n, kind, rest
                                               (1024, "c1", 21, 25)])
 def test_fused_lag_reduce_merge_bit_identical(tmp_path, n, kind, restart, K):
     """One rank: the partial-row reduce and the lag step in one launch (krylov.hip
-    gmres_lag_red_kernel, reduce_kernel's 256-thread summation order played by 16 waves) against
+    gmres_lag_red_kernel, reduce_kernel's 256-thread summation order played by 8 waves) against
     the two launches (HH_LAG_RED=0): history and x bit for bit."""
     import subprocess
     import sys
@@ -403,8 +403,10 @@ np.savez(out, x=x, info=info, hist=hist)
 def test_sl_residual_one_pass_matches_three_launches(tmp_path, n, kind, slabs):
     """The shifted-Laplace residual v0 = M (b - A x) in one pass (sl_fused.hip sl2_res_kernel,
     with |r|^2 and |M r|^2) against the three launches (HH_SL_RES=0: r and z1, the second sweep,
-    the norm): v0 is bit-identical, the norms are summed in another order -- the histories agree
-    to rounding at the start and within the parity contract after (stagnating runs amplify)."""
+    the norm): v0 is formed by the same per-point arithmetic (not compared directly here: the
+    solve exposes only its history and x), the norms are summed in another order -- the
+    histories agree to rounding at the start and within the parity contract after (stagnating
+    runs amplify)."""
     import subprocess
     import sys
     res = []
