@@ -273,7 +273,7 @@ __global__ __launch_bounds__(kT) void fused_iter_kernel(const FusedArgs a) {
   }
   v[2 * (K + 1)] = nw;
   v[2 * (K + 1) + 1] = nu;
-  block_reduce_vec<2 * (K + 1) + 2>(v, a.partials, 2 * (K + 1) + 2);
+  pass_epilogue<2 * (K + 1) + 2>(v, a);
 }
 
 // ------------------------------------------------------- M = two-sweep shifted Laplace
@@ -565,7 +565,7 @@ __global__ __launch_bounds__(kT) void fused_sl_iter_kernel(const FusedArgs a) {
   }
   v[2 * (K + 1)] = nw;
   v[2 * (K + 1) + 1] = nu;
-  block_reduce_vec<2 * (K + 1) + 2>(v, a.partials, 2 * (K + 1) + 2);
+  pass_epilogue<2 * (K + 1) + 2>(v, a);
 }
 
 // ----------------------------------------------------------------- edge rows (across ranks)

@@ -337,7 +337,7 @@ void fused_slk_kernel(const FusedArgs a) {
   }
   v[2 * (K + 1)] = nw;
   v[2 * (K + 1) + 1] = nu;
-  block_reduce_vec<2 * (K + 1) + 2>(v, a.partials, 2 * (K + 1) + 2);
+  pass_epilogue<2 * (K + 1) + 2>(v, a);
 }
 
 template <int K>

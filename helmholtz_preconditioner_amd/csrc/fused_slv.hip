@@ -264,7 +264,7 @@ __global__ __launch_bounds__(kT) void fused_slv_kernel(const FusedArgs a) {
   }
   v[2 * (K + 1)] = nw;
   v[2 * (K + 1) + 1] = nu;
-  block_reduce_vec<2 * (K + 1) + 2>(v, a.partials, 2 * (K + 1) + 2);
+  pass_epilogue<2 * (K + 1) + 2>(v, a);
 }
 
 template <int K>

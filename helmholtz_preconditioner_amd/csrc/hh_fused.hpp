@@ -7,6 +7,7 @@
 #include "hh_internal.hpp"
 #include "hh_complex.hpp"
 #include "hh_wave.hpp"
+#include "hh_givens.hpp"
 
 namespace hh {
 namespace fusedk {
@@ -113,6 +114,87 @@ __device__ __forceinline__ void load_coef(const FusedArgs& a, double2* coef) {
     const double sk = a.vscale[t];
     const double2 hk = cscale(make_double2(a.raw[2 * t], a.raw[2 * t + 1]), sk);
     coef[t] = cscale(hk, sk);
+  }
+}
+
+// ---- the in-pass column (PassFold, HH_LAG_RED=2): after every block stored its partial row
+// write-through (block_reduce_vec<SC1>), the last block of each group of kFoldGroup blocks sums
+// the group's rows in block order into a group row, and the last group's reducer sums the group
+// rows in group order into red[] and runs the lag step (gmres_lag_kernel's arithmetic) on its
+// first wave.  A fixed summation order whatever the arrival order (so every run gives the same
+// bits; a different order than reduce_kernel's, so histories agree with HH_LAG_RED=0/1 to
+// rounding).  Hand-offs: sc1 stores drained, then one lane's agent-scope acq_rel ticket behind a
+// barrier (krylov.hip last_block's form); the reads agent-scope.  Counters re-armed by the block
+// that finished with them; the next launch starts after a kernel boundary.
+using gu32f = __attribute__((address_space(1))) unsigned;
+using gu64f = __attribute__((address_space(1))) unsigned long long;
+__device__ __forceinline__ double ld_agent(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load((gu64f*)p, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_agent(double* p, double v) {
+  __hip_atomic_store((gu64f*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool fold_ticket(unsigned* counter, unsigned last) {
+  __shared__ int is_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores landed
+  __syncthreads();
+  if (threadIdx.x == 0)
+    is_last = __hip_atomic_fetch_add((gu32f*)counter, 1u, __ATOMIC_ACQ_REL,
+                                     __HIP_MEMORY_SCOPE_AGENT) == last;
+  __syncthreads();
+  return is_last;
+}
+// sum of rows r0 .. r0 + cnt - 1 (stride width) of column c in row order, loads 16 at a time
+__device__ __forceinline__ double fold_rows(const double* base, int r0, int cnt, int width, int c) {
+  double s = 0.0;
+  for (int b0 = 0; b0 < cnt; b0 += 16) {
+    double v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = ld_agent(base + (size_t)(r0 + min(b0 + q, cnt - 1)) * width + c);
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (b0 + q < cnt) s += v[q];
+  }
+  return s;
+}
+__device__ __forceinline__ void pass_fold(const FusedArgs& a, int width) {
+  const PassFold& f = a.fold;
+  const int nb = gridDim.x, ng = (nb + kFoldGroup - 1) / kFoldGroup;
+  const int grp = blockIdx.x / kFoldGroup, gsz = min(kFoldGroup, nb - grp * kFoldGroup);
+  const int t = threadIdx.x;
+  if (!fold_ticket(f.tickets + 1 + grp, (unsigned)gsz - 1)) return;
+  if (t < width) st_agent(f.gpart + (size_t)grp * 64 + t, fold_rows(a.partials, grp * kFoldGroup,
+                                                                     gsz, width, t));
+  if (t == 0) f.tickets[1 + grp] = 0u;  // (re-armed: every block of the group has arrived)
+  if (!fold_ticket(f.tickets, (unsigned)ng - 1)) return;
+  __shared__ double sred[64];
+  if (t < width) {
+    const double s = fold_rows(f.gpart, 0, ng, 64, t);
+    sred[t] = s;
+    f.red[t] = s;
+  }
+  if (t == 0) f.tickets[0] = 0u;
+  __syncthreads();
+  if (t < kWave) {  // the lag step, one wave (gmres_lag_red_kernel's second half)
+    using namespace givens;
+    const LagIn L = lag_load(f.g, f.j);
+    if (!L.stopped) {
+      const int kj = min(t, f.j);
+      lag_compute(f.g, f.j, L, make_double2(sred[2 * kj], sred[2 * kj + 1]), sred[2 * (f.j + 1)],
+                  sred[2 * (f.j + 1) + 1], 0, f.eps, f.ptol, f.stop_col);
+    }
+  }
+}
+// the pass's partial row: plain stores, or write-through stores + the in-pass column
+template <int NV>
+__device__ __forceinline__ void pass_epilogue(double (&v)[NV], const FusedArgs& a) {
+  if (a.fold.tickets) {
+    block_reduce_vec<NV, true>(v, a.partials, NV);
+    pass_fold(a, NV);
+  } else {
+    block_reduce_vec<NV>(v, a.partials, NV);
   }
 }
 

@@ -225,6 +225,20 @@ enum FusedRow : int {
   FROW_MEM = 1,   // a neighbouring slab of the same rank, contiguous in memory: formed in place
   FROW_HALO = 2,  // a neighbouring rank's rows of u_K, received into halo_lo / halo_hi
 };
+// The in-pass column of the one-pass iteration on one rank (HH_LAG_RED=2, round 6): the pass's
+// own blocks reduce its partial rows (groups of kFoldGroup blocks, then the groups: a fixed
+// order) and the last one runs the lag step (gmres_lag_kernel's arithmetic) -- no reduce / lag
+// launch, no launch boundary between two passes.  tickets == nullptr: off.
+constexpr int kFoldGroup = 16;
+constexpr int kFoldMaxGroups = kMaxStreamBlocks / kFoldGroup + 1;
+struct PassFold {
+  unsigned* tickets;  // [1 + kFoldMaxGroups] zeroed counters, re-armed by the kernel
+  double* gpart;      // [kFoldMaxGroups][64] the groups' partial rows
+  double* red;        // the reduced row (red + 16: gmres_lag_kernel's operands)
+  GivensState g;
+  int j, stop_col;
+  double eps, ptol;
+};
 struct FusedArgs {
   const double2* V;        // basis, at the slab's first row (negative row offsets: FROW_MEM)
   size_t ldv;
@@ -255,6 +269,7 @@ struct FusedArgs {
   double* partials;        // this launch's partial rows
   const int* stop;
   int alt;                 // fused_iter_kernel: odd bands march downwards (fused_alt_dir)
+  PassFold fold;           // the in-pass column (single rank), or fold.tickets == nullptr
 };
 // Running under rocprofv3 (its preloaded rocprofiler-sdk: ROCPROFILER_LIBRARY_CTOR /
 // ROCPROF_OUTPUT_PATH in the environment, or a rocprofiler library in LD_PRELOAD)?  ROCm 7.2:

@@ -186,6 +186,9 @@ struct hh_op {
   unsigned long long* small_ticks = nullptr;  // phase timing of the small cycle (diagnostic)
   // fused single-rank Krylov kernels (last-block reductions): their ticket counters
   unsigned* kcount = nullptr;
+  // the one-pass iteration's in-pass column (HH_LAG_RED=2): ticket counters and group rows
+  unsigned* fold_tickets = nullptr;
+  double* fold_gpart = nullptr;
   // HH_KRYLOV_FUSE bit 0: multidot + reduce, bit 1: update + Givens column as last-block fused
   // kernels.  Off by default: measured no faster at 1024^2 (update+column 8 975-9 077 vs 8 878-
   // 9 105 it/s unfused; multidot+reduce 8 219 -- its last block's reduction is a serial chain
@@ -290,7 +293,7 @@ int mnorm_slot(const hh_op* op, int dst);
 void read_dev(hh_op* op, const double* dsrc, double* hdst, int count);
 bool fused_default();
 int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double* raw,
-              const double* sin);
+              const double* sin, const PassFold* fold = nullptr);
 void check_sweep_chain(hh_op* op);
 size_t basis_pad();
 void ensure_gmres(hh_op* op, int restart);

@@ -17,7 +17,7 @@ bool fused_default() { return knobs().fused_iter != 0; }
 // interior rows run on the compute stream, and the H boundary rows run behind the exchange on
 // the halo stream (run_stencil's overlap).  Returns the number of partial rows written.
 int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double* raw,
-              const double* sin) {
+              const double* sin, const PassFold* fold) {
   hh_ctx* c = op->ctx;
   const int n = op->n;
   const int S = (int)op->slabs.size();
@@ -46,6 +46,10 @@ int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double*
   base.damping = op->damping;
   base.stop = op->stop_flag;
   base.alt = (!sl && fused_alt_dir()) ? 1 : 0;
+  if (fold) {  // (one launch covers every partial row: one slab of one rank)
+    REQUIRE(c->world == 1 && S == 1, "the in-pass column needs one slab of one rank");
+    base.fold = *fold;
+  }
   int nparts = 0;
   auto launch = [&](int si, int r0, int r1, int rows, int step, hipStream_t st) {
     if (r1 <= r0) return;
@@ -528,12 +532,34 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       allreduce_sum_dev(op, op->red + 16, 3);
       launch_gmres_lag(g, 0, op->red + 16, op->red + 16 + 3, false, eps, ptol, stop_col, s);
       check_site(c, "one-pass: first projection + column", s);
+      // HH_LAG_RED=2, one slab of one rank: the pass's own blocks reduce its partial rows and run
+      // the column (hh_fused.hpp pass_fold) -- no reduce / column launch between two passes
+      const bool fold = c->world == 1 && op->slabs.size() == 1 && knobs().lag_red == 2;
+      if (fold && !op->fold_tickets) {
+        op->fold_tickets = dalloc<unsigned>(1 + kFoldMaxGroups);
+        op->fold_gpart = dalloc<double>((size_t)kFoldMaxGroups * 64);
+        HIPC(hipMemsetAsync(op->fold_tickets, 0, (1 + kFoldMaxGroups) * sizeof(unsigned), s));
+      }
       for (int c2 = 0; c2 < stop_col; ++c2) {
         const int K = c2 + 1, K2 = K + 1;
-        const int np = run_fused(op, K, Wb[c2 & 1], Wb[(c2 + 1) & 1], op->red + 16, g.sscale + K);
+        PassFold pf{};
+        if (fold) {
+          pf.tickets = op->fold_tickets;
+          pf.gpart = op->fold_gpart;
+          pf.red = op->red + 16;
+          pf.g = g;
+          pf.j = c2 + 1;
+          pf.stop_col = stop_col;
+          pf.eps = eps;
+          pf.ptol = ptol;
+        }
+        const int np = run_fused(op, K, Wb[c2 & 1], Wb[(c2 + 1) & 1], op->red + 16, g.sscale + K,
+                                 fold ? &pf : nullptr);
         // (dots, |w|^2 and |u|^2 in one partial row: one reduce, one allreduce; on one rank the
-        // reduce and the column in one launch)
-        if (c->world == 1 && 2 * K2 + 2 <= 64 && lag_red_merge()) {
+        // reduce and the column in one launch, or in the pass itself)
+        if (fold) {
+          // (the pass ran the column)
+        } else if (c->world == 1 && 2 * K2 + 2 <= 64 && lag_red_merge()) {
           hipEvent_t k1 = tmark(op, s);
           launch_gmres_lag_red(g, c2 + 1, op->partials, np, 2 * K2 + 2, 2 * K2 + 2, op->red + 16,
                                eps, ptol, stop_col, s);

@@ -394,6 +394,8 @@ static void op_release(hh_op* op) {
   dfree(op->small_scr);
   dfree(op->small_ticks);
   dfree(op->kcount);
+  dfree(op->fold_tickets);
+  dfree(op->fold_gpart);
   dfree(op->sw_P);
   dfree(op->sw_Pf);
   dfree(op->sw_Pb);

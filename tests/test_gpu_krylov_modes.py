@@ -512,3 +512,35 @@ def test_fused_sl_overlapping_strip_kernel_matches(tmp_path, n, kind, slabs):
     assert np.max(np.abs(a["hist"][:5] - b["hist"][:5]) / a["hist"][:5]) < 1e-10
     assert np.max(np.abs(a["hist"] - b["hist"]) / a["hist"]) < TOL
     assert relerr(b["x"], a["x"]) < TOL
+
+
+@pytest.mark.parametrize("n,kind,restart,K,pc", [(300, "c1", 20, 45, "jacobi"),
+                                                 (1100, "marmousi", 7, 22, "jacobi"),
+                                                 (1024, "c1", 21, 25, "jacobi"),
+                                                 (613, "marmousi", 20, 30, "none"),
+                                                 (257, "c1", 1, 5, "jacobi"),
+                                                 (1100, "marmousi", 21, 25, "sl")])
+def test_in_pass_column_matches_separate_launches(tmp_path, n, kind, restart, K, pc):
+    """HH_LAG_RED=2 (one slab of one rank): the one-pass kernels' own blocks reduce their
+    partial rows -- groups of 16 blocks in block order, then the groups in group order -- and the
+    last one runs the lag step (hh_fused.hpp pass_fold), instead of the reduce + lag launches
+    (HH_LAG_RED=0).  Another summation order: the first iterations to rounding, the whole history
+    and the field within the parity contract; and a fixed order whatever the blocks' arrival
+    order -- two runs bit for bit."""
+    import subprocess
+    import sys
+    code = _ALT_CHILD.replace('restart=20, maxiter=30', f'restart={restart}, maxiter={K}')
+    res = []
+    for mode in ("0", "2", "2"):
+        out = tmp_path / f"m{mode}_{len(res)}.npz"
+        env = dict(os.environ, HH_LAG_RED=mode)
+        args = ([_SLK_CHILD, ROOT, str(n), kind, "1", str(restart), str(K), str(out)] if pc == "sl"
+                else [code, ROOT, str(n), kind, pc, str(out)])
+        subprocess.run([sys.executable, "-c"] + args, env=env, check=True, timeout=240)
+        res.append(np.load(out))
+    a, b, b2 = res
+    assert int(a["info"]) == int(b["info"]) and len(a["hist"]) == len(b["hist"]) == K
+    assert np.max(np.abs(a["hist"][:3] - b["hist"][:3]) / a["hist"][:3]) < 1e-11
+    assert np.max(np.abs(a["hist"] - b["hist"]) / a["hist"]) < TOL
+    assert relerr(b["x"], a["x"]) < TOL
+    assert np.array_equal(b["hist"], b2["hist"]) and np.array_equal(b["x"], b2["x"])
