@@ -51,10 +51,14 @@ __device__ __forceinline__ BandV band_v(const FusedArgs& a) {
   return b;
 }
 
-template <int K, bool CONSTC, bool EDGE>
+// KEEP: the projections' basis rows from a three-row LDS ring each thread writes for its own
+// column when it forms u_K (12 KiB per vector per block; no barrier: the same lane reads it two
+// steps later) instead of a re-read from L2 -- no registers for the re-read in flight
+template <int K, bool CONSTC, bool EDGE, bool KEEP>
 __device__ __forceinline__ void slv_band(const FusedArgs& a, const BandV bd, double2 (&acc)[K + 1],
                                          double& nw, double& nu, double2 (*lu)[kT + 2],
-                                         double2 (*lz)[kT + 2], const double2* coef) {
+                                         double2 (*lz)[kT + 2], const double2* coef,
+                                         double2 (*vk)[K][kT]) {
   const int n = a.n, nl = a.nl;
   const int t = threadIdx.x;
   const int c = bd.tx * kWO - 2 + t;  // this thread's column
@@ -87,7 +91,7 @@ __device__ __forceinline__ void slv_band(const FusedArgs& a, const BandV bd, dou
   };
   // ---- row L's loads (issued a step ahead): w_{K-1}, the K basis rows, the halo value, and
   // 1/c^2 of row L - 1
-  double2 pw, pv[K], ph = z, pr[K];  // pr: basis rows of the step's output row
+  double2 pw, pv[K], ph = z, pr[KEEP ? 1 : K];  // pr: basis rows of the step's output row
   double pic;
   auto issue = [&](int L) {
     const int Lc = min(L, re + 1);
@@ -109,11 +113,12 @@ __device__ __forceinline__ void slv_band(const FusedArgs& a, const BandV bd, dou
   // the projections' basis rows of output row L - 2 (a clamped in-band row otherwise), issued at
   // the end of step L - 1, after the step's own uses of the previous ones
   auto issue_proj = [&](int L) {
+    if constexpr (KEEP) return;
     const int rp = min(max(L - 2, rb), re - 1);
     gd2* prow = gptr(a.V + (ptrdiff_t)rp * n);
     asm volatile("" : "+s"(prow));
 #pragma unroll
-    for (int q = 0; q < K; ++q) pr[q] = ld_at(prow + (size_t)q * a.ldv, bo);
+    for (int q = 0; q < (KEEP ? 0 : K); ++q) pr[q] = ld_at(prow + (size_t)q * a.ldv, bo);
   };
   double2 uP = z, uC = z, Tm = z, z1a = z, z1b = z;
   double2 Dbm = make_double2(1.0, 0.0);
@@ -147,6 +152,11 @@ __device__ __forceinline__ void slv_band(const FusedArgs& a, const BandV bd, dou
       }
     }
     const double icv = pic;
+    if constexpr (KEEP) {  // basis row L for the projections of step L + 2
+      const int slot = (L % 3 + 3) % 3;
+#pragma unroll
+      for (int q = 0; q < K; ++q) vk[slot][q][t] = pv[q];
+    }
     // row L + 1's loads, in flight during the rest of the step
     issue(L + 1);
     __builtin_amdgcn_sched_barrier(0);
@@ -212,7 +222,8 @@ __device__ __forceinline__ void slv_band(const FusedArgs& a, const BandV bd, dou
       nu = fma(uo.x, uo.x, fma(uo.y, uo.y, nu));
       nw = fma(w.x, w.x, fma(w.y, w.y, nw));
 #pragma unroll
-      for (int k = 0; k < K; ++k) acc[k] = cfma_conj(pr[k], w, acc[k]);
+      for (int k = 0; k < K; ++k)
+        acc[k] = cfma_conj(KEEP ? vk[r % 3][k][t] : pr[KEEP ? 0 : k], w, acc[k]);
       acc[K] = cfma_conj(uo, w, acc[K]);
     }
     issue_proj(L + 1);  // (row L - 1's, for the next step)
@@ -229,11 +240,12 @@ __device__ __forceinline__ void slv_band(const FusedArgs& a, const BandV bd, dou
 
 // (Holding the allocation to four waves per SIMD at K <= 2 -- 128 VGPRs, 10-16 of them spilled
 // -- measured slower: K = 1 291 vs 242 us, K = 2 479 vs 331 us; profiles/r06/r06i_*)
-template <int K, bool CONSTC>
+template <int K, bool CONSTC, bool KEEP>
 __global__ __launch_bounds__(kT) void fused_slv_kernel(const FusedArgs a) {
   if (a.stop && *a.stop) return;
   __shared__ double2 coef[K];
   __shared__ double2 lu[2][kT + 2], lz[2][kT + 2];
+  __shared__ double2 vk[KEEP ? 3 : 1][K][kT];
   const BandV bd = band_v(a);
   load_coef<K>(a, coef);
   if (threadIdx.x < 2) {  // (the pads only feed columns that are never output)
@@ -252,9 +264,9 @@ __global__ __launch_bounds__(kT) void fused_slv_kernel(const FusedArgs a) {
     const int i0 = bd.tx * kWO;
     const bool interior = i0 - 2 >= 0 && i0 + kT - 2 <= a.n && bd.rb - 2 >= rlo && bd.re + 1 < rhi;
     if (interior)
-      slv_band<K, CONSTC, false>(a, bd, acc, nw, nu, lu, lz, coef);
+      slv_band<K, CONSTC, false, KEEP>(a, bd, acc, nw, nu, lu, lz, coef, vk);
     else
-      slv_band<K, CONSTC, true>(a, bd, acc, nw, nu, lu, lz, coef);
+      slv_band<K, CONSTC, true, KEEP>(a, bd, acc, nw, nu, lu, lz, coef, vk);
   }
   double v[2 * (K + 1) + 2];
 #pragma unroll
@@ -269,10 +281,14 @@ __global__ __launch_bounds__(kT) void fused_slv_kernel(const FusedArgs a) {
 
 template <int K>
 void slv_launch(const FusedArgs& a, int blocks, hipStream_t s) {
-  if (a.invc2)
-    hipLaunchKernelGGL((fused_slv_kernel<K, false>), dim3(blocks), dim3(kT), 0, s, a);
-  else
-    hipLaunchKernelGGL((fused_slv_kernel<K, true>), dim3(blocks), dim3(kT), 0, s, a);
+  const bool keep = K <= knobs().slv_keep_max;
+  if (a.invc2) {
+    if (keep) hipLaunchKernelGGL((fused_slv_kernel<K, false, true>), dim3(blocks), dim3(kT), 0, s, a);
+    else hipLaunchKernelGGL((fused_slv_kernel<K, false, false>), dim3(blocks), dim3(kT), 0, s, a);
+  } else {
+    if (keep) hipLaunchKernelGGL((fused_slv_kernel<K, true, true>), dim3(blocks), dim3(kT), 0, s, a);
+    else hipLaunchKernelGGL((fused_slv_kernel<K, true, false>), dim3(blocks), dim3(kT), 0, s, a);
+  }
 }
 template <int... Ks>
 struct VTable {

@@ -415,7 +415,7 @@ void launch_gmres_solve(const GivensState& g, int stop_col, bool merged, hipStre
 // one's default -- the shipped path -- and meaning).  hh_ctx_create reads them first, so a
 // malformed value fails there; hh_knobs_json reports them.
 struct Knobs {
-  long fused_iter, sl_res, slk_min_k, slv_max_k, slk_rows, fused_rows, fused_keep, fused_alt, lag_red,
+  long fused_iter, sl_res, slk_min_k, slv_max_k, slv_keep_max, slk_rows, fused_rows, fused_keep, fused_alt, lag_red,
       cycle_merge, basis_pad, krylov_fuse, krylov_rev, tile_xcd;
   long sweep_chain, sweep_graph, sweep_coop, sweep_diag;
   long small_coop, small_wide, small_coop_refuse, small_refuse_at;

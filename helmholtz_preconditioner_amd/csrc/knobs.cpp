@@ -28,6 +28,8 @@ const KnobDesc kKnobs[] = {
     {"HH_SL_RES", &Knobs::sl_res, 1, "shifted-Laplace residual in one pass (3g)"},
     {"HH_SLK", &Knobs::slk_min_k, 2, "smallest K for fused_slk_kernel, 0 = never (3g)"},
     {"HH_SLV", &Knobs::slv_max_k, 4, "largest K for fused_slv_kernel, 0 = never (3g)"},
+    {"HH_SLV_KEEP", &Knobs::slv_keep_max, 0,
+     "largest K whose fused_slv pass keeps its projection rows in LDS (else L2 re-reads)"},
     {"HH_SLK_ROWS", &Knobs::slk_rows, 0, "fused_slk_kernel band height, 0 = by n"},
     {"HH_FUSED_ROWS", &Knobs::fused_rows, 0, "one-pass band height, 0 = by n"},
     {"HH_FUSED_KEEP", &Knobs::fused_keep, kFusedKeepDefault,

@@ -5,7 +5,8 @@
 # bench.py's roofline.traffic and gmres.pass_traffic_vs_algorithmic look up by (n, slab rows).
 #   tools/pmc_shapes.sh [SHAPES...]   SHAPE = n:slabs, default: the weak-scaling grids of N = 1,
 #   2, 4, 8 (4096:1 5792:2 8192:4 11584:8) and the same-N 4096^2 legs (4096:2 4096:4 4096:8)
-# Env: KNOBS (comma list recorded with the pass records, e.g. HH_SLK=1) -- also exported.
+# Env: KNOBS (comma list recorded with the pass records, e.g. HH_SLK=1) -- also exported;
+# PASSES_ONLY=1 skips the apply records (the one-pass kernels changed, the apply did not).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/pmc_shapes}; mkdir -p $OUT
@@ -15,7 +16,7 @@ fatal() { case $1 in 124|137|134|139) echo "FATAL rc=$1 in $2"; exit $1;; esac; 
 SHAPES=("$@"); [ ${#SHAPES[@]} -eq 0 ] && SHAPES=(4096:1 5792:2 8192:4 11584:8 4096:2 4096:4 4096:8)
 for sh in "${SHAPES[@]}"; do
   n=${sh%%:*}; s=${sh##*:}; rows=$((n / s))
-  for med in marmousi const; do
+  for med in $([ "${PASSES_ONLY:-0}" = 1 ] || echo marmousi const); do
     nm="apply_${n}_${s}_${med}"
     for ctr in FETCH_SIZE WRITE_SIZE; do
       timeout -k 10 300 rocprofv3 --pmc $ctr -d $OUT/${nm}_$ctr -o run --output-format csv -- \
