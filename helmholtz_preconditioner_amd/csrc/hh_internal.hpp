@@ -230,7 +230,9 @@ enum FusedRow : int {
 // order) and the last one runs the lag step (gmres_lag_kernel's arithmetic) -- no reduce / lag
 // launch, no launch boundary between two passes.  tickets == nullptr: off.
 constexpr int kFoldGroup = 16;
-constexpr int kFoldMaxGroups = kMaxStreamBlocks / kFoldGroup + 1;
+// (a pass launch has at most ~kMaxStreamBlocks blocks; fused_slv's 252-column strips a few %
+// more: room for twice that)
+constexpr int kFoldMaxGroups = 2 * kMaxStreamBlocks / kFoldGroup;
 struct PassFold {
   unsigned* tickets;  // [1 + kFoldMaxGroups] zeroed counters, re-armed by the kernel
   double* gpart;      // [kFoldMaxGroups][64] the groups' partial rows

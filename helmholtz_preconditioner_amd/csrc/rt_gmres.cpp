@@ -74,6 +74,8 @@ int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double*
     a.bands = step > 0 ? (r1 - r0 - 1) / step + 1 : (r1 - r0 + rows - 1) / rows;
     a.partials = op->partials + (size_t)nparts * width;
     const int blocks = slv ? fused_slv_blocks(n, a.bands) : fused_iter_blocks(n, a.bands);
+    REQUIRE(!base.fold.tickets || blocks <= kFoldGroup * kFoldMaxGroups,
+            "in-pass column: %d blocks exceed its %d groups", blocks, kFoldMaxGroups);
     REQUIRE((size_t)(nparts + blocks) * width <= op->partials_cap,
             "partials workspace too small for the one-pass iteration (%d blocks)", nparts + blocks);
     if (slv)
