@@ -123,9 +123,17 @@ __device__ __forceinline__ void load_coef(const FusedArgs& a, double2* coef) {
 // rows in group order into red[] and runs the lag step (gmres_lag_kernel's arithmetic) on its
 // first wave.  A fixed summation order whatever the arrival order (so every run gives the same
 // bits; a different order than reduce_kernel's, so histories agree with HH_LAG_RED=0/1 to
-// rounding).  Hand-offs: sc1 stores drained, then one lane's agent-scope acq_rel ticket behind a
-// barrier (krylov.hip last_block's form); the reads agent-scope.  Counters re-armed by the block
-// that finished with them; the next launch starts after a kernel boundary.
+// rounding).  Hand-offs (MI355X_MICROARCH.md's sc1 hand-off table, first row): every byte
+// handed over is stored sc1 (write-through) and every storing wave drains its stores
+// (vmcnt(0)) before a workgroup barrier; then ONE lane adds to the group's counter with a RELAXED
+// agent-scope atomic; the block whose add returns the last ticket reads the bytes with sc1 loads
+// only (global_load sc1), after a barrier.  No release/acquire fence: an acq_rel ticket lowers to
+// buffer_wbl2 sc1 + buffer_inv sc1 in EVERY block -- a write-back of the XCD's L2, dirty with
+// the pass's w / u stores -- and made the in-pass column slower than the launches it replaces
+// (config 2 58.2 -> 67.8 us per iteration, profiles/r06/r06l_*).  Lines of the partial rows are
+// never read earlier in the launch, and a kernel start invalidates the L2s, so a reader's L2 has
+// no stale copy.  Counters re-armed by the block that finished with them; the next launch starts
+// after a kernel boundary.
 using gu32f = __attribute__((address_space(1))) unsigned;
 using gu64f = __attribute__((address_space(1))) unsigned long long;
 __device__ __forceinline__ double ld_agent(const double* p) {
@@ -141,7 +149,7 @@ __device__ __forceinline__ bool fold_ticket(unsigned* counter, unsigned last) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores landed
   __syncthreads();
   if (threadIdx.x == 0)
-    is_last = __hip_atomic_fetch_add((gu32f*)counter, 1u, __ATOMIC_ACQ_REL,
+    is_last = __hip_atomic_fetch_add((gu32f*)counter, 1u, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT) == last;
   __syncthreads();
   return is_last;
