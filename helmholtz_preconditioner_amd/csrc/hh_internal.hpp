@@ -293,7 +293,7 @@ bool fused_slk_use(int K);
 // fused_iter_kernel's odd bands march downwards (HH_FUSED_ALT, read once), so the halo rows a
 // band re-forms are read while their owners read them too (fused.hip)
 bool fused_alt_dir();
-bool lag_red_merge();  // HH_LAG_RED (default on)
+bool lag_red_merge();  // HH_LAG_RED != 0 (default 2: in the pass where it can, else merged)
 int fused_slk_rows(int n, int rows);
 void launch_fused_slk(int K, const FusedArgs& a, int blocks, hipStream_t stream);
 // the shifted-Laplace pass in the standalone fused M A's shape (fused_slv.hip: overlapping

@@ -35,8 +35,8 @@ const KnobDesc kKnobs[] = {
     {"HH_FUSED_KEEP", &Knobs::fused_keep, kFusedKeepDefault,
      "basis vectors re-read from the pass's LDS copy: 0 or 17"},
     {"HH_FUSED_ALT", &Knobs::fused_alt, 1, "odd bands march downwards (3g)"},
-    {"HH_LAG_RED", &Knobs::lag_red, 1,
-     "one rank: 0 reduce + lag launches, 1 one launch, 2 in the pass itself (3g)"},
+    {"HH_LAG_RED", &Knobs::lag_red, 2,
+     "one rank: 0 reduce + lag launches, 1 one launch, 2 in the pass itself (one slab; 3g)"},
     {"HH_CYCLE_MERGE", &Knobs::cycle_merge, 1, "cycle end in one pass (3g)"},
     {"HH_BASIS_PAD", &Knobs::basis_pad, 272, "complex elements between basis vectors"},
     {"HH_KRYLOV_FUSE", &Knobs::krylov_fuse, 0, "regular cycle: last-block fused Krylov kernels"},

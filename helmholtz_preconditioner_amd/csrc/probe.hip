@@ -90,6 +90,62 @@ __global__ __launch_bounds__(kT) void p6(const double2* __restrict__ u, const do
   }
 }
 
+// P15 / P16: the copy y = u (32 B per point, the constant medium's byte mix) with NT loads and
+// stores (P15) and with cached loads and NT stores (P16, the tile kernel's constant-medium form).
+template <bool NTL>
+__global__ __launch_bounds__(kT) void pcopy_nt(const double2* __restrict__ u,
+                                               double2* __restrict__ y, size_t len) {
+  const size_t stride = (size_t)gridDim.x * kT;
+  for (size_t p = (size_t)blockIdx.x * kT + threadIdx.x; p < len; p += stride) {
+    const double ux = NTL ? __builtin_nontemporal_load(&u[p].x) : u[p].x;
+    const double uy = NTL ? __builtin_nontemporal_load(&u[p].y) : u[p].y;
+    __builtin_nontemporal_store(ux, &y[p].x);
+    __builtin_nontemporal_store(uy, &y[p].y);
+  }
+}
+
+// P17 .. P21: the constant-medium tile kernel's access shape without its arithmetic (32 B per
+// point): a 256-thread block owns a 256-wide x R-row tile (plain tile order), loads its R rows
+// through the cache -- plus (HALO) the row above and below it, (EDGE) one broadcast load per row
+// for the wave's W/E edge column, (TAB) three per-column table loads -- and stores R rows NT.
+// Isolates what the tile shape itself costs against the streaming copy (P16).
+template <int R, bool HALO, bool EDGE, bool TAB>
+__global__ __launch_bounds__(kT) void ptile(const double2* __restrict__ u,
+                                            double2* __restrict__ y, int n) {
+  const int tiles_x = (n + kT - 1) / kT;
+  const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+  const int i = min(tx * kT + (int)threadIdx.x, n - 1), lane = threadIdx.x & 63;
+  const int rb = ty * R, re = min(rb + R, n);
+  if (rb >= n) return;
+  double2 U[R + 2], EG[R];
+  const double2 z = make_double2(0.0, 0.0);
+#pragma unroll
+  for (int m = 0; m < R + 2; ++m) {
+    const int r = rb - 1 + m;
+    const bool want = HALO ? (r >= 0 && r < n) : (m >= 1 && r < re);
+    U[m] = want ? u[(size_t)r * n + i] : z;
+  }
+  const int iw = min(max(lane < 32 ? i - lane - 1 : i - lane + 64, 0), n - 1);
+#pragma unroll
+  for (int m = 0; m < R; ++m) EG[m] = EDGE ? u[(size_t)min(rb + m, re - 1) * n + iw] : z;
+  double2 t0 = z, t1 = z, t2 = z;
+  if (TAB) {
+    t0 = u[i];
+    t1 = u[(size_t)n + i];
+    t2 = u[(size_t)2 * n + i];
+  }
+#pragma unroll
+  for (int m = 0; m < R; ++m) {
+    const int r = rb + m;
+    if (r < re) {
+      double vx = U[m + 1].x + 0.25 * (U[m].x + U[m + 2].x) + EG[m].x + t0.x + t1.x + t2.x;
+      double vy = U[m + 1].y + 0.25 * (U[m].y + U[m + 2].y) + EG[m].y + t0.y + t1.y + t2.y;
+      __builtin_nontemporal_store(vx, &y[(size_t)r * n + i].x);
+      __builtin_nontemporal_store(vy, &y[(size_t)r * n + i].y);
+    }
+  }
+}
+
 // P7/P8: the stencil's traversal without its arithmetic or neighbours.  A 512-thread block
 // owns a 512-wide strip x 32-row band and marches it with one row of prefetch (NT loads and
 // stores, 40 B/point).  P7 deals tiles to XCDs in contiguous ranges as the stencil does; P8
@@ -203,6 +259,22 @@ int launch_probe_kind(int kind, int blocks, const double2* u, const double* ic, 
       else hipLaunchKernelGGL(pnaive<true>, gn, bn, 0, s, u, ic, y, n);
       return 40;
     }
+    case 17: case 18: case 19: case 20: case 21: {
+      const int n = (int)llround(std::sqrt((double)len));
+      if ((size_t)n * n != len) return 0;
+      const int R = kind == 21 ? 12 : 6;
+      const dim3 gt((unsigned)(((n + kT - 1) / kT) * ((n + R - 1) / R))), bt(kT);
+      switch (kind) {
+        case 17: hipLaunchKernelGGL((ptile<6, false, false, false>), gt, bt, 0, s, u, y, n); break;
+        case 18: hipLaunchKernelGGL((ptile<6, true, false, false>), gt, bt, 0, s, u, y, n); break;
+        case 19: hipLaunchKernelGGL((ptile<6, true, true, false>), gt, bt, 0, s, u, y, n); break;
+        case 20: hipLaunchKernelGGL((ptile<6, true, true, true>), gt, bt, 0, s, u, y, n); break;
+        default: hipLaunchKernelGGL((ptile<12, false, false, false>), gt, bt, 0, s, u, y, n); break;
+      }
+      return 32;
+    }
+    case 15: hipLaunchKernelGGL(pcopy_nt<true>, g, b, 0, s, u, y, len); return 32;
+    case 16: hipLaunchKernelGGL(pcopy_nt<false>, g, b, 0, s, u, y, len); return 32;
     default: return 0;
   }
 }

@@ -461,7 +461,10 @@ __device__ __forceinline__ void stencil_tile(const StencilArgs& a, const int t) 
 // neighbour come mostly from L2 / the Infinity Cache.  Same per-point arithmetic as
 // stencil_tile: bit-identical results.
 // One tile t of tile_kernel (and of the persistent tile_persist_kernel, which loops over tiles)
-template <int EPI, bool CONSTC, int R, bool NT, bool NTU>
+// NTU: 0 u through the cache, 1 every u row non-temporal, 2 only the tile's private rows
+// non-temporal (rows rb+1 .. re-2: no other tile reads them; the four rows a tile shares with
+// its vertical neighbours stay cached for them)
+template <int EPI, bool CONSTC, int R, bool NT, int NTU>
 __device__ __forceinline__ void tile_do(const StencilArgs& a, const int t) {
   static_assert(EPI == EPI_AX || EPI == EPI_JAC, "tile shape: plain and Jacobi-fused apply");
   constexpr int TPB = kStencilThreads;
@@ -486,7 +489,10 @@ __device__ __forceinline__ void tile_do(const StencilArgs& a, const int t) {
   double2 U[R + 2], EG[R];
   double IC[R];
   #pragma unroll
-  for (int m = 0; m < R + 2; ++m) U[m] = ld2<NTU>(rowp(min(rb - 1 + m, re)) + ic_);
+  for (int m = 0; m < R + 2; ++m) {
+    const double2* q = rowp(min(rb - 1 + m, re)) + ic_;
+    U[m] = (NTU == 1 || (NTU == 2 && m >= 2 && m < R)) ? ld2<true>(q) : ld2<false>(q);
+  }
   #pragma unroll
   for (int m = 0; m < R; ++m) {
     const int r = min(rb + m, re - 1);
@@ -537,7 +543,7 @@ __device__ __forceinline__ void tile_do(const StencilArgs& a, const int t) {
 // slabs) every halo row goes to another XCD's L2: 1.23-1.29x the algorithmic fetch
 // (profiles/r05/r05n_pmc_shapes.log) against 1.03x -- from the Infinity Cache: the map is the
 // slower one (tile_xcd_map).
-template <int EPI, bool CONSTC, int R, bool NT, bool NTU>
+template <int EPI, bool CONSTC, int R, bool NT, int NTU>
 __global__ __launch_bounds__(kStencilThreads) void tile_kernel(const StencilArgs a) {
   if (a.stop && *a.stop) return;  // queued GMRES cycle already stopped
   int t = blockIdx.x;
@@ -552,7 +558,7 @@ __global__ __launch_bounds__(kStencilThreads) void tile_kernel(const StencilArgs
 // once): block b takes tiles b, b + G, b + 2 G, ... -- the resident blocks still sweep one
 // contiguous window of tiles, without the dispatch of tiles_x * tiles_y blocks and with a
 // tail of at most one tile per block (tuning variants kTilePersist + R).  Bit-identical.
-template <int EPI, bool CONSTC, int R, bool NT, bool NTU>
+template <int EPI, bool CONSTC, int R, bool NT, int NTU>
 __global__ __launch_bounds__(kStencilThreads) void tile_persist_kernel(const StencilArgs a,
                                                                        int tiles) {
   if (a.stop && *a.stop) return;
@@ -730,9 +736,16 @@ constexpr int kTileDefault = kTileVariant + 4;  // 4-row tiles, cached u, NT 1/c
 // + 64: the same tiles from a persistent grid (tile_persist_kernel; cached u, NT 1/c^2 and
 // stores; R rows per tile): kTilePersist + R
 [[maybe_unused]] constexpr int kTilePersist = kTileVariant + 64;
+// + 96: NT stores and 1/c^2, u non-temporal on the tile's private rows only (tile_do NTU = 2):
+// kTilePrivNT + R.  Not a default: 4096^2 constant medium R = 6 97.3 vs 97.4 us, Marmousi-like
+// R = 4 115.7 vs 114.8 (profiles/r06/r06o_tune_*_privnt.log).  (Also measured and not kept,
+// round 6: the two edge-column loads restricted to the two lanes that use them, and interior
+// strips taking the column tables as kernel arguments instead of three loads per lane -- each
+// 0-4 % SLOWER, profiles/r06/r06r_*; the access-shape probe behind them: r06p_probe_tile_shape.log)
+constexpr int kTilePrivNT = kTileVariant + 96;
 constexpr bool tile_variant_known(int v) {
   const int w = v - kTileVariant, R = w % 16;
-  return w >= 0 && (w < 64 || w < 80) && R >= 2 && R <= 8 && R != 7;
+  return w >= 0 && (w < 80 || (w >= 96 && w < 112)) && R >= 2 && R <= 8 && R != 7;
 }
 // The 9-point operator instantiates the four LDS-exchange shapes below and takes the 5-point
 // defaults: in its separable form (101-109 VGPRs, 4 waves per SIMD) it runs at the 5-point
@@ -878,7 +891,7 @@ int stencil_grid_blocks(int n, int rows, int rows_per_block, int row_step) {
 int stencil_default_variant() { return kDefaultVariant; }
 bool stencil_variant_valid(int v) {
   return (v >= 0 && v <= 27) || (v >= 30 && v <= 33) || (v >= 42 && v <= 45) || sl2_variant(v) ||
-         (v >= kTileVariant && v < kTileVariant + 80 && tile_variant_known(v));
+         (v >= kTileVariant && v < kTileVariant + 112 && tile_variant_known(v));
 }
 
 void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_out[1],
@@ -906,12 +919,13 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_
   if (v >= kTileVariant) {  // non-marching tiles (plain / Jacobi 5-point apply, tile_kernel)
     const int w = v - kTileVariant, R = w % 16;
     const bool ntu = (w / 16) % 2 == 1 && w < 64, nt = w < 32 || w >= 64;
+    const bool priv = v >= kTilePrivNT;  // (5-point only; the 9-point tiles take NT stores)
     // (padding tiles_x to a multiple of 8, which would put vertically adjacent tiles on one
     // XCD, measured 3-7 % SLOWER at n = 5792 and 11584: profiles/r01y_tune_tile_pad.log)
     a.tiles_x = (a.n + kStencilThreads - 1) / kStencilThreads;
     a.tiles_y = (rows + R - 1) / R;
     const int tiles = a.tiles_x * a.tiles_y;
-    const bool pers = w >= 64 && !a.tab_r2x;  // (5-point only)
+    const bool pers = w >= 64 && w < 80 && !a.tab_r2x;  // (5-point only)
     const bool xcd = !a.tab_r2x && !pers && tile_xcd_map(a.tiles_x);
     a.tiles_per_xcd = xcd ? (tiles + 7) / 8 : 0;
     nblocks_out[0] = 0;
@@ -951,10 +965,12 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_
         }
       } else if (const_c) {
         if (!nt) hipLaunchKernelGGL((tile_kernel<E, true, RR, false, false>), g, b, 0, stream, a);
+        else if (priv) hipLaunchKernelGGL((tile_kernel<E, true, RR, true, 2>), g, b, 0, stream, a);
         else if (ntu) hipLaunchKernelGGL((tile_kernel<E, true, RR, true, true>), g, b, 0, stream, a);
         else hipLaunchKernelGGL((tile_kernel<E, true, RR, true, false>), g, b, 0, stream, a);
       } else {
         if (!nt) hipLaunchKernelGGL((tile_kernel<E, false, RR, false, false>), g, b, 0, stream, a);
+        else if (priv) hipLaunchKernelGGL((tile_kernel<E, false, RR, true, 2>), g, b, 0, stream, a);
         else if (ntu) hipLaunchKernelGGL((tile_kernel<E, false, RR, true, true>), g, b, 0, stream, a);
         else hipLaunchKernelGGL((tile_kernel<E, false, RR, true, false>), g, b, 0, stream, a);
       }

@@ -25,11 +25,15 @@ names = ["1pt/lane u16 ic8 y16", "2pt/lane adjacent (ic16, u/y 32B stride)",
          "stencil traversal, blockIdx order", "stencil traversal, 8-row bands",
          "stencil traversal, 16-row bands", "stencil traversal, 64-row bands",
          "stencil traversal, 128-row bands", "naive 5-point gather, blockIdx order",
-         "naive 5-point gather, XCD row ranges"]
+         "naive 5-point gather, XCD row ranges", "copy, NT loads + NT stores",
+         "copy, cached loads + NT stores", "tile shape R6: own rows only",
+         "tile shape R6: + halo rows", "tile shape R6: + halo + edge loads",
+         "tile shape R6: + halo + edge + tables", "tile shape R12: own rows only"]
+kinds = [int(k) for k in os.environ.get("PROBE_KINDS", ",".join(map(str, range(22)))).split(",")]
 km, bpp = ctypes.c_double(), ctypes.c_int()
 for blocks in (2048, 8192, 32768):
-    for kind in range(15):
-        if kind >= 7 and blocks != 2048:
+    for kind in kinds:
+        if (7 <= kind <= 14 or kind >= 17) and blocks != 2048:
             continue  # the marching probes size their own grid
         best = 1e9
         for _ in range(3):

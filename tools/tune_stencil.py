@@ -29,6 +29,11 @@ grids = [int(v) for v in a.grids.replace("/", ",").split(",")]
 
 
 def vname(v):
+    if v >= 96:  # non-marching tiles (stencil.hip kTileVariant ...)
+        w = v - 96
+        kind = {0: "tile", 1: "tile ntu", 2: "tile st-cached", 3: "tile st-cached", 4: "tile persist",
+                6: "tile privnt"}.get(w // 16, "tile ?")
+        return f"{kind} R{w % 16}"
     w = v % 24
     return f"{['lds', 'direct', 'shfl'][w % 3]} pf{(w // 3) % 2 + 1}{' nt' if (w // 6) % 2 else ''}" \
            f"{' ntu' if w >= 12 else ''}{' w512' if v % 48 >= 24 else ''}{' occ6' if v >= 48 else ''}"
