@@ -118,16 +118,21 @@ __device__ __forceinline__ void load_coef(const FusedArgs& a, double2* coef) {
 }
 
 // ---- the in-pass column (PassFold, HH_LAG_RED=2): after every block stored its partial row
-// write-through (block_reduce_vec<SC1>), the last block of each group of kFoldGroup blocks sums
-// the group's rows in block order into a group row, and the last group's reducer sums the group
-// rows in group order into red[] and runs the lag step (gmres_lag_kernel's arithmetic) on its
-// first wave.  A fixed summation order whatever the arrival order (so every run gives the same
-// bits; a different order than reduce_kernel's, so histories agree with HH_LAG_RED=0/1 to
-// rounding).  Hand-offs (MI355X_MICROARCH.md's sc1 hand-off table, first row): every byte
-// handed over is stored sc1 (write-through) and every storing wave drains its stores
-// (vmcnt(0)) before a workgroup barrier; then ONE lane adds to the group's counter with a RELAXED
-// agent-scope atomic; the block whose add returns the last ticket reads the bytes with sc1 loads
-// only (global_load sc1), after a barrier.  No release/acquire fence: an acq_rel ticket lowers to
+// write-through (block_reduce_vec<SC1>), the pass's own blocks reduce the rows in EXACTLY
+// reduce_kernel's order -- so the sums, the column and the whole history are bit-identical to
+// HH_LAG_RED=1 / 0 (gmres_lag_red_kernel, reduce_kernel + gmres_lag_kernel):
+//   reduce_kernel's thread t (< 256) sums rows t, t + 256, ... ascending from 0.0 (S_t); its tree
+//   then forms U_r = (S_r + S_{r+128}) + (S_{r+64} + S_{r+192}) for r < 64 and sums the U_r by
+//   shuffles (off = 32 .. 1).
+//   Here the blocks b = r (mod 64) are one class: the last of them to arrive runs the four
+//   S_{r + 64 q} of its class (its rows ascending, row j of the class into S_{j mod 4}) and
+//   stores U_r; the last class to finish runs the shuffle tree of every column (one wave a
+//   column, U_r on lane r) and the lag step (gmres_lag_kernel's arithmetic) on its first wave.
+// Hand-offs (MI355X_MICROARCH.md's sc1 hand-off table, first row): every byte handed over is
+// stored sc1 (write-through) and every storing wave drains its stores (vmcnt(0)) before a
+// workgroup barrier; then ONE lane adds to the class's counter with a RELAXED agent-scope
+// atomic; the block whose add returns the last ticket reads the bytes with sc1 loads only
+// (global_load sc1), after a barrier.  No release/acquire fence: an acq_rel ticket lowers to
 // buffer_wbl2 sc1 + buffer_inv sc1 in EVERY block -- a write-back of the XCD's L2, dirty with
 // the pass's w / u stores -- and made the in-pass column slower than the launches it replaces
 // (config 2 58.2 -> 67.8 us per iteration, profiles/r06/r06l_*).  Lines of the partial rows are
@@ -154,34 +159,50 @@ __device__ __forceinline__ bool fold_ticket(unsigned* counter, unsigned last) {
   __syncthreads();
   return is_last;
 }
-// sum of rows r0 .. r0 + cnt - 1 (stride width) of column c in row order, loads 16 at a time
-__device__ __forceinline__ double fold_rows(const double* base, int r0, int cnt, int width, int c) {
-  double s = 0.0;
-  for (int b0 = 0; b0 < cnt; b0 += 16) {
-    double v[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = ld_agent(base + (size_t)(r0 + min(b0 + q, cnt - 1)) * width + c);
-#pragma unroll
-    for (int q = 0; q < 16; ++q)
-      if (b0 + q < cnt) s += v[q];
-  }
-  return s;
-}
 __device__ __forceinline__ void pass_fold(const FusedArgs& a, int width) {
   const PassFold& f = a.fold;
-  const int nb = gridDim.x, ng = (nb + kFoldGroup - 1) / kFoldGroup;
-  const int grp = blockIdx.x / kFoldGroup, gsz = min(kFoldGroup, nb - grp * kFoldGroup);
+  const int nb = gridDim.x, r = blockIdx.x % kFoldClasses;
+  const int ncls = min(nb, kFoldClasses);
+  const int cnt = (nb - r + kFoldClasses - 1) / kFoldClasses;  // blocks r, r + 64, ... < nb
   const int t = threadIdx.x;
-  if (!fold_ticket(f.tickets + 1 + grp, (unsigned)gsz - 1)) return;
-  if (t < width) st_agent(f.gpart + (size_t)grp * 64 + t, fold_rows(a.partials, grp * kFoldGroup,
-                                                                     gsz, width, t));
-  if (t == 0) f.tickets[1 + grp] = 0u;  // (re-armed: every block of the group has arrived)
-  if (!fold_ticket(f.tickets, (unsigned)ng - 1)) return;
+  if (!fold_ticket(f.tickets + 1 + r, (unsigned)cnt - 1)) return;
+  if (t < width) {  // U_r of column t
+    double S[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int j0 = 0; j0 < cnt; j0 += 16) {  // (16 row loads in flight)
+      double v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        v[q] = ld_agent(a.partials +
+                        (size_t)(r + kFoldClasses * min(j0 + q, cnt - 1)) * width + t);
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (j0 + q < cnt) S[q & 3] += v[q];  // (j0 a multiple of 4: row j0 + q into S_{q mod 4})
+    }
+    st_agent(f.gpart + (size_t)t * kFoldClasses + r, (S[0] + S[2]) + (S[1] + S[3]));
+  }
+  if (t == 0) f.tickets[1 + r] = 0u;  // (re-armed: every block of the class has arrived)
+  if (!fold_ticket(f.tickets, (unsigned)ncls - 1)) return;
   __shared__ double sred[64];
-  if (t < width) {
-    const double s = fold_rows(f.gpart, 0, ng, 64, t);
-    sred[t] = s;
-    f.red[t] = s;
+  const int lane = t & (kWave - 1), w = t / kWave;
+  constexpr int kCols = 64 / (kT / kWave);  // columns per wave
+  double u[kCols];
+#pragma unroll
+  for (int k = 0; k < kCols; ++k) {
+    const int c = w + (kT / kWave) * k;
+    u[k] = (c < width && lane < ncls) ? ld_agent(f.gpart + (size_t)c * kFoldClasses + lane) : 0.0;
+  }
+#pragma unroll
+  for (int k = 0; k < kCols; ++k) {
+    const int c = w + (kT / kWave) * k;
+    if (c < width) {  // (wave-uniform)
+      double x = u[k];
+#pragma unroll
+      for (int off = kWave / 2; off > 0; off >>= 1) x += __shfl_down(x, off);
+      if (lane == 0) {
+        sred[c] = x;
+        f.red[c] = x;
+      }
+    }
   }
   if (t == 0) f.tickets[0] = 0u;
   __syncthreads();

@@ -226,16 +226,14 @@ enum FusedRow : int {
   FROW_HALO = 2,  // a neighbouring rank's rows of u_K, received into halo_lo / halo_hi
 };
 // The in-pass column of the one-pass iteration on one rank (HH_LAG_RED=2, round 6): the pass's
-// own blocks reduce its partial rows (groups of kFoldGroup blocks, then the groups: a fixed
-// order) and the last one runs the lag step (gmres_lag_kernel's arithmetic) -- no reduce / lag
-// launch, no launch boundary between two passes.  tickets == nullptr: off.
-constexpr int kFoldGroup = 16;
-// (a pass launch has at most ~kMaxStreamBlocks blocks; fused_slv's 252-column strips a few %
-// more: room for twice that)
-constexpr int kFoldMaxGroups = 2 * kMaxStreamBlocks / kFoldGroup;
+// own blocks reduce its partial rows in reduce_kernel's exact order (the blocks of each residue
+// class mod kFoldClasses, then the classes: hh_fused.hpp pass_fold) and the last one runs the
+// lag step (gmres_lag_kernel's arithmetic) -- no reduce / lag launch, no launch boundary
+// between two passes; bit-identical to them.  tickets == nullptr: off.
+constexpr int kFoldClasses = 64;
 struct PassFold {
-  unsigned* tickets;  // [1 + kFoldMaxGroups] zeroed counters, re-armed by the kernel
-  double* gpart;      // [kFoldMaxGroups][64] the groups' partial rows
+  unsigned* tickets;  // [1 + kFoldClasses] zeroed counters, re-armed by the kernel
+  double* gpart;      // [64 columns][kFoldClasses] the classes' tree sums U_r
   double* red;        // the reduced row (red + 16: gmres_lag_kernel's operands)
   GivensState g;
   int j, stop_col;

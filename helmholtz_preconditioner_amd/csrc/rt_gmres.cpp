@@ -48,6 +48,7 @@ int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double*
   base.alt = (!sl && fused_alt_dir()) ? 1 : 0;
   if (fold) {  // (one launch covers every partial row: one slab of one rank)
     REQUIRE(c->world == 1 && S == 1, "the in-pass column needs one slab of one rank");
+    REQUIRE(width <= 64, "in-pass column: %d partial-row columns (at most 64)", width);
     base.fold = *fold;
   }
   int nparts = 0;
@@ -74,8 +75,6 @@ int run_fused(hh_op* op, int K, const double2* win, double2* wout, const double*
     a.bands = step > 0 ? (r1 - r0 - 1) / step + 1 : (r1 - r0 + rows - 1) / rows;
     a.partials = op->partials + (size_t)nparts * width;
     const int blocks = slv ? fused_slv_blocks(n, a.bands) : fused_iter_blocks(n, a.bands);
-    REQUIRE(!base.fold.tickets || blocks <= kFoldGroup * kFoldMaxGroups,
-            "in-pass column: %d blocks exceed its %d groups", blocks, kFoldMaxGroups);
     REQUIRE((size_t)(nparts + blocks) * width <= op->partials_cap,
             "partials workspace too small for the one-pass iteration (%d blocks)", nparts + blocks);
     if (slv)
@@ -534,13 +533,14 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       allreduce_sum_dev(op, op->red + 16, 3);
       launch_gmres_lag(g, 0, op->red + 16, op->red + 16 + 3, false, eps, ptol, stop_col, s);
       check_site(c, "one-pass: first projection + column", s);
-      // HH_LAG_RED=2, one slab of one rank: the pass's own blocks reduce its partial rows and run
-      // the column (hh_fused.hpp pass_fold) -- no reduce / column launch between two passes
+      // HH_LAG_RED=2, one slab of one rank: the pass's own blocks reduce its partial rows (in
+      // reduce_kernel's order) and run the column (hh_fused.hpp pass_fold) -- no reduce / column
+      // launch between two passes
       const bool fold = c->world == 1 && op->slabs.size() == 1 && knobs().lag_red == 2;
       if (fold && !op->fold_tickets) {
-        op->fold_tickets = dalloc<unsigned>(1 + kFoldMaxGroups);
-        op->fold_gpart = dalloc<double>((size_t)kFoldMaxGroups * 64);
-        HIPC(hipMemsetAsync(op->fold_tickets, 0, (1 + kFoldMaxGroups) * sizeof(unsigned), s));
+        op->fold_tickets = dalloc<unsigned>(1 + kFoldClasses);
+        op->fold_gpart = dalloc<double>((size_t)64 * kFoldClasses);
+        HIPC(hipMemsetAsync(op->fold_tickets, 0, (1 + kFoldClasses) * sizeof(unsigned), s));
       }
       for (int c2 = 0; c2 < stop_col; ++c2) {
         const int K = c2 + 1, K2 = K + 1;

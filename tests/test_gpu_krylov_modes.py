@@ -514,39 +514,37 @@ def test_fused_sl_overlapping_strip_kernel_matches(tmp_path, n, kind, slabs):
     assert relerr(b["x"], a["x"]) < TOL
 
 
-# (the 1024^2 case -- config 2's grid, 32 groups of 16 blocks -- runs 12 iterations, within the
-# first cycle: that solve stagnates from its first iteration (the host oracle's history falls
-# 1.84e-7 -> 1.06e-7 over 30) and past ~20 iterations moves 0.2-1.6e-6 in the field under EVERY
-# reordering the tests accept -- 16-row bands 4e-7 / 1.2e-6 in the history, the all-upward march
-# 2e-7, the in-pass column 1.6e-6 at (restart 21, 25 its), 1.35e-6 at (20, 30):
-# profiles/r06/r06m_order_sensitivity_1024_c1_r21_k25.log, r06l_tests_in_pass_1024_k30.log)
+# Grids: 130^2 (17 blocks: fewer than the 64 residue classes), 1024^2 (config 2's: 512 blocks,
+# 8 a class; a stagnating solve whose field moves 1e-6 under any reordering -- bit-identical
+# here), 2500^2 (3130 blocks: 49 a class, four rounds of row loads), ragged strips, restarts
+# and the shifted-Laplace passes (fused_slv / fused_slk).
 @pytest.mark.parametrize("n,kind,restart,K,pc", [(300, "c1", 20, 45, "jacobi"),
                                                  (1100, "marmousi", 7, 22, "jacobi"),
-                                                 (1024, "c1", 20, 12, "jacobi"),
+                                                 (1024, "c1", 20, 30, "jacobi"),
                                                  (613, "marmousi", 20, 30, "none"),
                                                  (257, "c1", 1, 5, "jacobi"),
+                                                 (130, "c1", 20, 25, "jacobi"),
+                                                 (2500, "marmousi", 20, 6, "jacobi"),
                                                  (1100, "marmousi", 21, 25, "sl")])
 def test_in_pass_column_matches_separate_launches(tmp_path, n, kind, restart, K, pc):
-    """HH_LAG_RED=2 (one slab of one rank): the one-pass kernels' own blocks reduce their
-    partial rows -- groups of 16 blocks in block order, then the groups in group order -- and the
-    last one runs the lag step (hh_fused.hpp pass_fold), instead of the reduce + lag launches
-    (HH_LAG_RED=0).  Another summation order: the first iterations to rounding, the whole history
-    and the field within the parity contract; and a fixed order whatever the blocks' arrival
-    order -- two runs bit for bit."""
+    """HH_LAG_RED=2 (the default on one slab of one rank): the one-pass kernels' own blocks
+    reduce their partial rows -- the blocks of each residue class mod 64 in block order, then the
+    classes by reduce_kernel's shuffle tree -- and the last one runs the lag step
+    (hh_fused.hpp pass_fold), instead of the reduce + lag launches (HH_LAG_RED=0) or the merged
+    launch (1): reduce_kernel's summation order exactly, so histories and fields are bit for bit
+    the launches' whatever order the blocks arrive in."""
     import subprocess
     import sys
     code = _ALT_CHILD.replace('restart=20, maxiter=30', f'restart={restart}, maxiter={K}')
     res = []
-    for mode in ("0", "2", "2"):
-        out = tmp_path / f"m{mode}_{len(res)}.npz"
+    for mode in ("0", "2", "1"):
+        out = tmp_path / f"m{mode}.npz"
         env = dict(os.environ, HH_LAG_RED=mode)
         args = ([_SLK_CHILD, ROOT, str(n), kind, "1", str(restart), str(K), str(out)] if pc == "sl"
                 else [code, ROOT, str(n), kind, pc, str(out)])
         subprocess.run([sys.executable, "-c"] + args, env=env, check=True, timeout=240)
         res.append(np.load(out))
-    a, b, b2 = res
+    a, b, c = res
     assert int(a["info"]) == int(b["info"]) and len(a["hist"]) == len(b["hist"]) == K
-    assert np.max(np.abs(a["hist"][:3] - b["hist"][:3]) / a["hist"][:3]) < 1e-11
-    assert np.max(np.abs(a["hist"] - b["hist"]) / a["hist"]) < TOL
-    assert relerr(b["x"], a["x"]) < TOL
-    assert np.array_equal(b["hist"], b2["hist"]) and np.array_equal(b["x"], b2["x"])
+    for o in (b, c):
+        assert np.array_equal(o["hist"], a["hist"]) and np.array_equal(o["x"], a["x"])
