@@ -68,4 +68,16 @@ __device__ __forceinline__ double2 smith_apply(double2 a, Smith f) {
   return make_double2(a.x / 0.0, a.y / 0.0);
 }
 
+
+// A 16-byte write-through store (global_store_dwordx4 sc1): the line leaves the XCD's L2 at once
+// instead of staying there dirty (plain and NT stores keep it, MI355X_MICROARCH.md's store
+// table), so a streaming kernel's outputs do not push out the lines it re-reads -- the apply's
+// halo rows, a pass's projection rows.  Vector store; the compiler does not count it in its
+// vmcnt bookkeeping, which only makes its later waits conservative.
+__device__ __forceinline__ void st_wt(double2* p, double2 v) {
+  typedef double d2wt __attribute__((ext_vector_type(2)));
+  const d2wt x = {v.x, v.y};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+}
+
 }  // namespace hh

@@ -530,8 +530,16 @@ __device__ __forceinline__ void tile_do(const StencilArgs& a, const int t) {
     Au = cfma(E, uE, Au);
     Au = cfma(N, uN, Au);
     if (act && r < re) {
-      if constexpr (EPI == EPI_AX) store2(a.out0 + (size_t)r * n + ic_, cscale(Au, sin), NT);
-      else store2(a.out0 + (size_t)r * n + ic_, cscale(cdiv(Au, D), sin), NT);
+      // NT tiles: write-through stores -- the outputs leave L2 at once, so the halo rows the
+      // next tiles re-read stay there (4096^2: 98.3-99.2 vs 100.8-100.9 us constant medium,
+      // 116.7-117.5 vs 118.6-118.7 Marmousi-like; profiles/r06/r06v_ab_tile_sc1_stores.log)
+      const double2 o = EPI == EPI_AX ? cscale(Au, sin) : cscale(cdiv(Au, D), sin);
+#ifndef HH_AB_NT_STORE
+      if constexpr (NT) st_wt(a.out0 + (size_t)r * n + ic_, o);
+      else store2(a.out0 + (size_t)r * n + ic_, o, false);
+#else
+      store2(a.out0 + (size_t)r * n + ic_, o, NT);
+#endif
     }
   }
 }
