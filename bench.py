@@ -797,7 +797,8 @@ def main():
         "traffic_vs_algorithmic": traffic_ratio,
         "traffic_source": traffic_src,
         "kernel": (f"tile_kernel<EPI_AX,{'true' if A.constant_medium else 'false'},"
-                   f"{6 if A.constant_medium else 4} rows> "
+                   f"{(8 if A.constant_medium else 6) if n > 4608 else (6 if A.constant_medium else 4)}"
+                   " rows> "
                    "(interior rows)") if (args.stencil == 5 and n >= 2048 and args.variant < 0) else
                   (f"stencil_kernel<EPI_AX,{'true' if A.constant_medium else 'false'},"
                    f"S9={'true' if args.stencil == 9 else 'false'}> (interior rows)"),

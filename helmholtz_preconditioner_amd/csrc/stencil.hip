@@ -920,10 +920,17 @@ void launch_stencil(int epi, bool const_c, const StencilArgs& a_in, int nblocks_
   }
   if (v >= kTileVariant && a.row_step > 0)  // spaced bands (halo rows): marching shape
     v = stencil_resolve_variant(epi, kVariantInSolve, a.n);
-  // constant medium (no 1/c^2 stream, 32 B per unknown): 6-row tiles -- the halo rows' share of
-  // the u loads falls from 6/4 to 8/6 (4096^2: 97.2 vs 97.9 us, 8192^2: 366.4 vs 381.7 us;
-  // Marmousi-like: 4096^2 118.1 vs 117.5, so 4 rows stay; profiles/r05/r05s_tune_ntu_*.log)
-  if (variant == -1 && const_c && v == kTileDefault && !a.tab_r2x) v = kTileVariant + 6;
+  // Taller tiles where they pay (the halo rows' share of the u loads (R + 2) / R): the constant
+  // medium (no 1/c^2 stream, 32 B per unknown) 6 rows, 8 on rows longer than kLongRow; the
+  // Marmousi-like medium 4 rows, 6 on rows longer than kLongRow.  With the write-through
+  // stores (round 6): constant 4096^2 R5 / R6 / R8 95.2 / 95.3-95.9 / 98.2 us, 8192^2 R6 / R8
+  // 358.5 / 354.5, 16384^2 1428 / 1380; Marmousi 4096^2 R4 / R6 113.7 / 114.7, 5792^2 232.2 /
+  // 229.9, 8192^2 443.0 / 442.8, 11584^2 948.7 / 926.2 (profiles/r06/r06x_*, r06y_*; round 5:
+  // r05s_tune_ntu_*.log)
+  if (variant == -1 && v == kTileDefault && !a.tab_r2x) {
+    if (const_c) v = kTileVariant + (a.n > kLongRow ? 8 : 6);
+    else if (a.n > kLongRow) v = kTileVariant + 6;
+  }
   if (v >= kTileVariant) {  // non-marching tiles (plain / Jacobi 5-point apply, tile_kernel)
     const int w = v - kTileVariant, R = w % 16;
     const bool ntu = (w / 16) % 2 == 1 && w < 64, nt = w < 32 || w >= 64;

@@ -6,7 +6,8 @@
 #   tools/pmc_shapes.sh [SHAPES...]   SHAPE = n:slabs, default: the weak-scaling grids of N = 1,
 #   2, 4, 8 (4096:1 5792:2 8192:4 11584:8) and the same-N 4096^2 legs (4096:2 4096:4 4096:8)
 # Env: KNOBS (comma list recorded with the pass records, e.g. HH_SLK=1) -- also exported;
-# PASSES_ONLY=1 skips the apply records (the one-pass kernels changed, the apply did not).
+# PASSES_ONLY=1 skips the apply records (the one-pass kernels changed, the apply did not);
+# APPLY_ONLY=1 the pass records.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/pmc_shapes}; mkdir -p $OUT
@@ -27,6 +28,7 @@ for sh in "${SHAPES[@]}"; do
       $OUT/${nm}_WRITE_SIZE/run_counter_collection.csv --n $n --medium $med --rows $rows \
       --merge $OUT/r05_pmc_traffic.json || true
   done
+  [ "${APPLY_ONLY:-0}" = 1 ] && continue
   nm="pass_${n}_${s}_sl"
   for ctr in FETCH_SIZE WRITE_SIZE; do
     PRECOND=sl MODES=fused VSLABS=$s timeout -k 10 400 rocprofv3 --pmc $ctr -d $OUT/${nm}_$ctr -o run \
