@@ -340,7 +340,7 @@ void launch_gmres_column(const GivensState& g, int col, const double* red_dots,
 // launch_reduce + launch_gmres_lag in one launch (single rank: no allreduce between them)
 void launch_gmres_lag_red(const GivensState& g, int j, const double* partials, int count,
                           int width, int cols, double* red, double eps, double ptol, int stop_col,
-                          hipStream_t stream);
+                          hipStream_t stream, int final_step = 0);
 void launch_gmres_lag(const GivensState& g, int j, const double* red_dots, const double* sig2,
                       bool final_step, double eps, double ptol, int stop_col, hipStream_t stream);
 // Start of a cycle: S[0] = ||Mr||, vscale[0] = 1/||Mr|| from red[idx_m]; status[4] = ||r||.

@@ -385,9 +385,12 @@ __global__ void gmres_lag_kernel(GivensState g, int j, const double* rd, const d
 constexpr int kLagRedWaves = 8;
 constexpr int kLagRedThreads = kLagRedWaves * kWave;
 constexpr int kLagRedQ = kT / kLagRedWaves;  // virtual threads per lane
+// final_step (the cycle end's norm, cols = 1): the reduced column is the subdiagonal's |w|^2 and
+// the lag step only completes column j - 1 (gmres_lag_kernel with final_step, whose rd / w2
+// operands that step never reads).
 __global__ __launch_bounds__(kLagRedThreads) void gmres_lag_red_kernel(
     GivensState g, int j, const double* partials, int count, int width, int cols, double* red,
-    double eps, double ptol, int stop_col) {
+    double eps, double ptol, int stop_col, int final_step) {
   __shared__ double wsum[kLagRedWaves][kWave];
   __shared__ double sred[kWave];
   const int w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
@@ -429,9 +432,13 @@ __global__ __launch_bounds__(kLagRedThreads) void gmres_lag_red_kernel(
   }
   __syncthreads();
   if (w == 0 && !L.stopped) {
-    const int kj = min(lane, j);
-    lag_compute(g, j, L, make_double2(sred[2 * kj], sred[2 * kj + 1]), sred[2 * (j + 1)],
-                sred[2 * (j + 1) + 1], 0, eps, ptol, stop_col);
+    if (final_step) {
+      lag_compute(g, j, L, make_double2(0.0, 0.0), 0.0, sred[0], 1, eps, ptol, stop_col);
+    } else {
+      const int kj = min(lane, j);
+      lag_compute(g, j, L, make_double2(sred[2 * kj], sred[2 * kj + 1]), sred[2 * (j + 1)],
+                  sred[2 * (j + 1) + 1], 0, eps, ptol, stop_col);
+    }
   }
 }
 
@@ -658,9 +665,9 @@ void launch_gmres_column(const GivensState& g, int col, const double* red_dots,
 
 void launch_gmres_lag_red(const GivensState& g, int j, const double* partials, int count,
                           int width, int cols, double* red, double eps, double ptol, int stop_col,
-                          hipStream_t stream) {
+                          hipStream_t stream, int final_step) {
   hipLaunchKernelGGL(gmres_lag_red_kernel, dim3(1), dim3(kLagRedThreads), 0, stream, g, j,
-                     partials, count, width, cols, red, eps, ptol, stop_col);
+                     partials, count, width, cols, red, eps, ptol, stop_col, final_step);
 }
 void launch_gmres_lag(const GivensState& g, int j, const double* red_dots, const double* sig2,
                       bool final_step, double eps, double ptol, int stop_col, hipStream_t stream) {

@@ -529,9 +529,13 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       double2* Wb[2] = {op->fw, op->fw + L};
       apply_MA(op, V, g.sscale, Wb[0]);  // w_0 = M A (s_0 u_0)
       launch_multidot(V, ldv, 1, Wb[0], L, op->partials, blocks, s, stp);
-      launch_reduce(op->partials, blocks, 4, 3, op->red + 16, s, stp);
-      allreduce_sum_dev(op, op->red + 16, 3);
-      launch_gmres_lag(g, 0, op->red + 16, op->red + 16 + 3, false, eps, ptol, stop_col, s);
+      if (c->world == 1 && lag_red_merge()) {  // (one rank: reduce + lag step in one launch)
+        launch_gmres_lag_red(g, 0, op->partials, blocks, 4, 3, op->red + 16, eps, ptol, stop_col, s);
+      } else {
+        launch_reduce(op->partials, blocks, 4, 3, op->red + 16, s, stp);
+        allreduce_sum_dev(op, op->red + 16, 3);
+        launch_gmres_lag(g, 0, op->red + 16, op->red + 16 + 3, false, eps, ptol, stop_col, s);
+      }
       check_site(c, "one-pass: first projection + column", s);
       // HH_LAG_RED=2, one slab of one rank: the pass's own blocks reduce its partial rows (in
       // reduce_kernel's order) and run the column (hh_fused.hpp pass_fold) -- no reduce / column
@@ -591,9 +595,14 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
                         V + (size_t)K * ldv, L, op->npart, blocks, s, stp);
         }
         tspan(op, HH_SPAN_UPDATE, k0, tmark(op, s));
-        launch_reduce(op->npart, blocks, kMaxNorms, 1, op->red + 8, s, stp);
-        allreduce_sum_dev(op, op->red + 8, 1);
-        launch_gmres_lag(g, stop_col + 1, nullptr, op->red + 8, true, eps, ptol, stop_col, s);
+        if (c->world == 1 && lag_red_merge()) {  // (the norm's reduce + the final lag step)
+          launch_gmres_lag_red(g, stop_col + 1, op->npart, blocks, kMaxNorms, 1, op->red + 8, eps,
+                               ptol, stop_col, s, 1);
+        } else {
+          launch_reduce(op->npart, blocks, kMaxNorms, 1, op->red + 8, s, stp);
+          allreduce_sum_dev(op, op->red + 8, 1);
+          launch_gmres_lag(g, stop_col + 1, nullptr, op->red + 8, true, eps, ptol, stop_col, s);
+        }
         HIPC(hipGetLastError());
         check_site(c, "one-pass: cycle end", s);
       }
