@@ -667,7 +667,7 @@ __global__ __launch_bounds__(kT) void cycle_end_kernel(const double2* __restrict
                                                        const double2* __restrict__ ab,
                                                        const double2* w, double2* x, double2* vb,
                                                        size_t len, double* partials,
-                                                       const int* stop) {
+                                                       const int* stop, const PassFold fold) {
   if (stop && *stop) return;
   __shared__ double2 cu[K], ca[K], cb[K];
   const int t = threadIdx.x;
@@ -700,7 +700,37 @@ __global__ __launch_bounds__(kT) void cycle_end_kernel(const double2* __restrict
     vb[p] = b;
   }
   double v1[1] = {nrm};
-  block_reduce_vec<1>(v1, partials, kMaxNorms);
+  if (fold.tickets) {  // one rank: the norm's reduce and the final lag step in this launch
+    block_reduce_vec<1, true>(v1, partials, kMaxNorms);
+    fold_reduce_lag(fold, partials, kMaxNorms, 1, true);
+  } else {
+    block_reduce_vec<1>(v1, partials, kMaxNorms);
+  }
+}
+
+// The one-pass cycle's first dots (u_0^H w_0 and |w_0|^2: multidot_kernel<1, NT>'s loop and
+// partial row, bit for bit) with the reduce and the first lag step folded in (one rank).
+template <bool NT>
+__global__ __launch_bounds__(kT) void cycle_start_dots_kernel(const double2* __restrict__ V,
+                                                              const double2* __restrict__ w,
+                                                              size_t len, double* partials,
+                                                              const int* stop,
+                                                              const PassFold fold) {
+  if (stop && *stop) return;
+  double2 acc = make_double2(0.0, 0.0);
+  double nrm = 0.0;
+  const size_t stride = (size_t)gridDim.x * kT;
+  for (size_t p = (size_t)blockIdx.x * kT + threadIdx.x; p < len; p += stride) {
+    const double2 wv = w[p];
+    nrm = fma(wv.x, wv.x, fma(wv.y, wv.y, nrm));
+    const double2 vv = NT ? make_double2(__builtin_nontemporal_load(&V[p].x),
+                                         __builtin_nontemporal_load(&V[p].y))
+                          : V[p];
+    acc = cfma_conj(vv, wv, acc);
+  }
+  double v[3] = {acc.x, acc.y, nrm};
+  block_reduce_vec<3, true>(v, partials, 4);
+  fold_reduce_lag(fold, partials, 4, 3, false);
 }
 
 // x += y_col vb once column col is finished: y_col = S[col] / H[col][col] (scipy's rule: S[col]
@@ -723,15 +753,16 @@ __global__ __launch_bounds__(kT) void cycle_finish_kernel(GivensState g, int col
 template <int K>
 void cycle_end_launch(const double2* V, size_t ldv, const double* raw, const double* vscale,
                       const double2* ab, const double2* w, double2* x, double2* vb, size_t len,
-                      double* partials, int blocks, hipStream_t s, const int* stop) {
+                      double* partials, int blocks, hipStream_t s, const int* stop,
+                      const PassFold& fold) {
   hipLaunchKernelGGL((cycle_end_kernel<K>), dim3(blocks), dim3(kT), 0, s, V, ldv, raw, vscale,
-                     ab, w, x, vb, len, partials, stop);
+                     ab, w, x, vb, len, partials, stop, fold);
 }
 template <int... Ks>
 struct CTable {
   using FN = void (*)(const double2*, size_t, const double*, const double*, const double2*,
                       const double2*, double2*, double2*, size_t, double*, int, hipStream_t,
-                      const int*);
+                      const int*, const PassFold&);
   static constexpr FN f[] = {cycle_end_launch<Ks>...};
 };
 using CycleTable = CTable<1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21>;
@@ -818,8 +849,21 @@ void launch_cycle_coef(const GivensState& g, int col, double2* ab, hipStream_t s
 }
 void launch_cycle_end(int K, const double2* V, size_t ldv, const double* raw, const double* vscale,
                       const double2* ab, const double2* w, double2* x, double2* vb, size_t len,
-                      double* partials, int blocks, hipStream_t stream, const int* stop) {
-  CycleTable::f[K - 1](V, ldv, raw, vscale, ab, w, x, vb, len, partials, blocks, stream, stop);
+                      double* partials, int blocks, hipStream_t stream, const int* stop,
+                      const PassFold* fold) {
+  const PassFold none{};
+  CycleTable::f[K - 1](V, ldv, raw, vscale, ab, w, x, vb, len, partials, blocks, stream, stop,
+                       fold ? *fold : none);
+}
+void launch_cycle_start_dots(const double2* V, const double2* w, size_t len, double* partials,
+                             int blocks, bool nt, hipStream_t stream, const int* stop,
+                             const PassFold& fold) {
+  if (nt)
+    hipLaunchKernelGGL((cycle_start_dots_kernel<true>), dim3(blocks), dim3(kT), 0, stream, V, w,
+                       len, partials, stop, fold);
+  else
+    hipLaunchKernelGGL((cycle_start_dots_kernel<false>), dim3(blocks), dim3(kT), 0, stream, V, w,
+                       len, partials, stop, fold);
 }
 void launch_cycle_finish(const GivensState& g, int col, const double2* vb, double2* x, size_t len,
                          int blocks, hipStream_t stream) {

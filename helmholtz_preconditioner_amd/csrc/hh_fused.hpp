@@ -159,20 +159,25 @@ __device__ __forceinline__ bool fold_ticket(unsigned* counter, unsigned last) {
   __syncthreads();
   return is_last;
 }
-__device__ __forceinline__ void pass_fold(const FusedArgs& a, int width) {
-  const PassFold& f = a.fold;
+// The fold over `cols` columns of partial rows `width` apart, then the lag step of column f.j:
+// gmres_lag_kernel's (final_step: only the subdiagonal's |w|^2 = the reduced column 0, as
+// gmres_lag_red_kernel's final-step mode).  Used by the passes (pass_fold) and, on one rank, by
+// the one-pass cycle's first dots and its end (fused.hip cycle_start_dots_kernel,
+// cycle_end_kernel).
+__device__ __forceinline__ void fold_reduce_lag(const PassFold& f, const double* partials,
+                                                int width, int cols, bool final_step) {
   const int nb = gridDim.x, r = blockIdx.x % kFoldClasses;
   const int ncls = min(nb, kFoldClasses);
   const int cnt = (nb - r + kFoldClasses - 1) / kFoldClasses;  // blocks r, r + 64, ... < nb
   const int t = threadIdx.x;
   if (!fold_ticket(f.tickets + 1 + r, (unsigned)cnt - 1)) return;
-  if (t < width) {  // U_r of column t
+  if (t < cols) {  // U_r of column t
     double S[4] = {0.0, 0.0, 0.0, 0.0};
     for (int j0 = 0; j0 < cnt; j0 += 16) {  // (16 row loads in flight)
       double v[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q)
-        v[q] = ld_agent(a.partials +
+        v[q] = ld_agent(partials +
                         (size_t)(r + kFoldClasses * min(j0 + q, cnt - 1)) * width + t);
 #pragma unroll
       for (int q = 0; q < 16; ++q)
@@ -189,12 +194,12 @@ __device__ __forceinline__ void pass_fold(const FusedArgs& a, int width) {
 #pragma unroll
   for (int k = 0; k < kCols; ++k) {
     const int c = w + (kT / kWave) * k;
-    u[k] = (c < width && lane < ncls) ? ld_agent(f.gpart + (size_t)c * kFoldClasses + lane) : 0.0;
+    u[k] = (c < cols && lane < ncls) ? ld_agent(f.gpart + (size_t)c * kFoldClasses + lane) : 0.0;
   }
 #pragma unroll
   for (int k = 0; k < kCols; ++k) {
     const int c = w + (kT / kWave) * k;
-    if (c < width) {  // (wave-uniform)
+    if (c < cols) {  // (wave-uniform)
       double x = u[k];
 #pragma unroll
       for (int off = kWave / 2; off > 0; off >>= 1) x += __shfl_down(x, off);
@@ -210,11 +215,20 @@ __device__ __forceinline__ void pass_fold(const FusedArgs& a, int width) {
     using namespace givens;
     const LagIn L = lag_load(f.g, f.j);
     if (!L.stopped) {
-      const int kj = min(t, f.j);
-      lag_compute(f.g, f.j, L, make_double2(sred[2 * kj], sred[2 * kj + 1]), sred[2 * (f.j + 1)],
-                  sred[2 * (f.j + 1) + 1], 0, f.eps, f.ptol, f.stop_col);
+      if (final_step) {
+        lag_compute(f.g, f.j, L, make_double2(0.0, 0.0), 0.0, sred[0], 1, f.eps, f.ptol,
+                    f.stop_col);
+      } else {
+        const int kj = min(t, f.j);
+        const int is = 2 * (f.j + 1) + 1;  // (the first column's sig: not read at j = 0)
+        lag_compute(f.g, f.j, L, make_double2(sred[2 * kj], sred[2 * kj + 1]), sred[2 * (f.j + 1)],
+                    is < cols ? sred[is] : 0.0, 0, f.eps, f.ptol, f.stop_col);
+      }
     }
   }
+}
+__device__ __forceinline__ void pass_fold(const FusedArgs& a, int width) {
+  fold_reduce_lag(a.fold, a.partials, width, width, false);
 }
 // the pass's partial row: plain stores, or write-through stores + the in-pass column
 template <int NV>

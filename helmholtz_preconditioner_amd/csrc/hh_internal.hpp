@@ -313,7 +313,14 @@ void launch_fused_edge(int K, const FusedArgs& a, int r0, int c0, int r1, int c1
 void launch_cycle_coef(const GivensState& g, int col, double2* ab, hipStream_t stream);
 void launch_cycle_end(int K, const double2* V, size_t ldv, const double* raw, const double* vscale,
                       const double2* ab, const double2* w, double2* x, double2* vb, size_t len,
-                      double* partials, int blocks, hipStream_t stream, const int* stop);
+                      double* partials, int blocks, hipStream_t stream, const int* stop,
+                      const PassFold* fold = nullptr);
+// the one-pass cycle's first dots (multidot_kernel<1>'s partial row) with the reduce and the
+// first lag step folded in (one rank; fold_reduce_lag)
+void launch_cycle_start_dots(const double2* V, const double2* w, size_t len, double* partials,
+                             int blocks, bool nt, hipStream_t stream, const int* stop,
+                             const PassFold& fold);
+bool krylov_nt_for(size_t len);  // the Krylov kernels' NT basis loads at this length
 // x += y_col vb, only if the cycle reached its last column col (g.ctrl[1] == col)
 void launch_cycle_finish(const GivensState& g, int col, const double2* vb, double2* x, size_t len,
                          int blocks, hipStream_t stream);

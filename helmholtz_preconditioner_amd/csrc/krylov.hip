@@ -582,6 +582,8 @@ static_assert(kMaxProj == 32, "table covers 1..kMaxProj");
 
 }  // namespace
 
+bool krylov_nt_for(size_t len) { return krylov_nt(len); }
+
 void tune_krylov(int nt, int blocks) {
   g_krylov_nt = nt < 0 ? -1 : (nt != 0);
   g_krylov_blocks = blocks > 0 ? (blocks < kMaxStreamBlocks ? blocks : kMaxStreamBlocks) : 0;

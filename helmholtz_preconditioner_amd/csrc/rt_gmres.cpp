@@ -527,38 +527,47 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       // (the pass writes u_{j+1} there while other tiles still read their halo rows of w_j)
       const int* stp = g.ctrl;
       double2* Wb[2] = {op->fw, op->fw + L};
-      apply_MA(op, V, g.sscale, Wb[0]);  // w_0 = M A (s_0 u_0)
-      launch_multidot(V, ldv, 1, Wb[0], L, op->partials, blocks, s, stp);
-      if (c->world == 1 && lag_red_merge()) {  // (one rank: reduce + lag step in one launch)
-        launch_gmres_lag_red(g, 0, op->partials, blocks, 4, 3, op->red + 16, eps, ptol, stop_col, s);
-      } else {
-        launch_reduce(op->partials, blocks, 4, 3, op->red + 16, s, stp);
-        allreduce_sum_dev(op, op->red + 16, 3);
-        launch_gmres_lag(g, 0, op->red + 16, op->red + 16 + 3, false, eps, ptol, stop_col, s);
-      }
-      check_site(c, "one-pass: first projection + column", s);
       // HH_LAG_RED=2, one slab of one rank: the pass's own blocks reduce its partial rows (in
       // reduce_kernel's order) and run the column (hh_fused.hpp pass_fold) -- no reduce / column
-      // launch between two passes
+      // launch between two passes, nor after the cycle's first dots and its end
       const bool fold = c->world == 1 && op->slabs.size() == 1 && knobs().lag_red == 2;
       if (fold && !op->fold_tickets) {
         op->fold_tickets = dalloc<unsigned>(1 + kFoldClasses);
         op->fold_gpart = dalloc<double>((size_t)64 * kFoldClasses);
         HIPC(hipMemsetAsync(op->fold_tickets, 0, (1 + kFoldClasses) * sizeof(unsigned), s));
       }
+      auto fold_at = [&](int j, double* red) {
+        PassFold pf{};
+        pf.tickets = op->fold_tickets;
+        pf.gpart = op->fold_gpart;
+        pf.red = red;
+        pf.g = g;
+        pf.j = j;
+        pf.stop_col = stop_col;
+        pf.eps = eps;
+        pf.ptol = ptol;
+        return pf;
+      };
+      apply_MA(op, V, g.sscale, Wb[0]);  // w_0 = M A (s_0 u_0)
+      if (fold) {
+        launch_cycle_start_dots(V, Wb[0], L, op->partials, blocks, krylov_nt_for(L), s, stp,
+                                fold_at(0, op->red + 16));
+      } else {
+        launch_multidot(V, ldv, 1, Wb[0], L, op->partials, blocks, s, stp);
+        if (c->world == 1 && lag_red_merge()) {  // (one rank: reduce + lag step in one launch)
+          launch_gmres_lag_red(g, 0, op->partials, blocks, 4, 3, op->red + 16, eps, ptol, stop_col,
+                               s);
+        } else {
+          launch_reduce(op->partials, blocks, 4, 3, op->red + 16, s, stp);
+          allreduce_sum_dev(op, op->red + 16, 3);
+          launch_gmres_lag(g, 0, op->red + 16, op->red + 16 + 3, false, eps, ptol, stop_col, s);
+        }
+      }
+      check_site(c, "one-pass: first projection + column", s);
       for (int c2 = 0; c2 < stop_col; ++c2) {
         const int K = c2 + 1, K2 = K + 1;
         PassFold pf{};
-        if (fold) {
-          pf.tickets = op->fold_tickets;
-          pf.gpart = op->fold_gpart;
-          pf.red = op->red + 16;
-          pf.g = g;
-          pf.j = c2 + 1;
-          pf.stop_col = stop_col;
-          pf.eps = eps;
-          pf.ptol = ptol;
-        }
+        if (fold) pf = fold_at(c2 + 1, op->red + 16);
         const int np = run_fused(op, K, Wb[c2 & 1], Wb[(c2 + 1) & 1], op->red + 16, g.sscale + K,
                                  fold ? &pf : nullptr);
         // (dots, |w|^2 and |u|^2 in one partial row: one reduce, one allreduce; on one rank the
@@ -586,16 +595,21 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
       {  // the last column's update and the norm that completes it
         const int K = stop_col + 1;
         hipEvent_t k0 = tmark(op, s);
+        const bool fold_end = fold && merge_end;
         if (merge_end) {  // (with x += V a, V b: see cycle_coef_kernel)
           launch_cycle_coef(g, stop_col, op->cab, s);
+          const PassFold pe = fold_end ? fold_at(stop_col + 1, op->red + 8) : PassFold{};
           launch_cycle_end(K, V, ldv, op->red + 16, g.vscale, op->cab, Wb[stop_col & 1], x,
-                           V + (size_t)K * ldv, L, op->npart, blocks, s, stp);
+                           V + (size_t)K * ldv, L, op->npart, blocks, s, stp,
+                           fold_end ? &pe : nullptr);
         } else {
           launch_update(V, ldv, K, op->red + 16, g.vscale, Wb[stop_col & 1],
                         V + (size_t)K * ldv, L, op->npart, blocks, s, stp);
         }
         tspan(op, HH_SPAN_UPDATE, k0, tmark(op, s));
-        if (c->world == 1 && lag_red_merge()) {  // (the norm's reduce + the final lag step)
+        if (fold_end) {
+          // (the cycle end's own blocks reduced the norm and ran the final lag step)
+        } else if (c->world == 1 && lag_red_merge()) {  // (the norm's reduce + the final lag step)
           launch_gmres_lag_red(g, stop_col + 1, op->npart, blocks, kMaxNorms, 1, op->red + 8, eps,
                                ptol, stop_col, s, 1);
         } else {
