@@ -737,10 +737,27 @@ __global__ __launch_bounds__(kT) void cycle_start_dots_kernel(const double2* __r
 // = 0 when H[col][col] == 0, iterative.py:815-816)
 // (a cycle that stopped before its last column col takes the solve + xupdate instead: decided
 // here, from the last column it executed, so the host need not read it first)
+// Its first block also does gmres_solve_kernel's work (the merged form, one launch fewer per
+// cycle): ctl[2] raised when the cycle reached `col` (xupdate_kernel then skips), else the
+// triangular solve of the columns it executed.
 __global__ __launch_bounds__(kT) void cycle_finish_kernel(GivensState g, int col,
                                                           const double2* vb, double2* x,
                                                           size_t len) {
-  if (g.ctrl[1] != col) return;
+  __shared__ double2 sH[(kMaxProj + 1) * (kMaxProj + 2)];
+  const int c1 = g.ctrl[1];
+  if (blockIdx.x == 0) {
+    const int cs = min(max(c1, 0), col);  // (gmres_solve_kernel's column)
+    const bool skip = cs == col;
+    if (threadIdx.x == 0) g.ctrl[2] = skip;
+    if (!skip) {
+      const int R1 = g.restart + 1;
+      for (int e = threadIdx.x; e < (cs + 1) * R1; e += kT) sH[e] = g.H[e];
+      __syncthreads();
+      if (threadIdx.x < kWave) givens::solve_columns_wave(g, cs, sH);
+      return;
+    }
+  }
+  if (c1 != col) return;
   const int R1 = g.restart + 1;
   const double2 hcc = g.H[(size_t)col * R1 + col];
   const double2 sc = g.S[col];

@@ -189,5 +189,33 @@ __device__ __forceinline__ void lag_compute(const GivensState& g, int j, const L
   }
 }
 
+// The triangular solve H y = S of columns 0 .. col and y_k s_k into g.ycoef (lane k: y_k), on
+// one wave, from H's columns already in LDS (sH, R1 = restart + 1 per column) -- gmres_solve
+// _kernel's body, also run by cycle_finish_kernel's first block when a cycle stopped early.
+__device__ __forceinline__ void solve_columns_wave(const GivensState& g, int col,
+                                                   const double2* sH) {
+  const int R1 = g.restart + 1;
+  const int lane = threadIdx.x & (kWave - 1), me = min(lane, col);
+  double2 y = g.S[me];
+  const double sv = g.vscale[me];
+  auto H = [&](int c, int k) { return sH[c * R1 + k]; };
+  const double2 hcc = H(col, col);
+  if (hcc.x == 0.0 && hcc.y == 0.0) {
+    if (lane == 0) g.S[col] = make_double2(0.0, 0.0);
+    if (lane == col) y = make_double2(0.0, 0.0);
+  }
+  const Smith f = smith_of(H(me, me));
+  for (int k = col; k >= 0; --k) {
+    const double2 t0 = rlane2(y, k);
+    if (t0.x != 0.0 || t0.y != 0.0) {  // (uniform)
+      if (lane == k) y = smith_apply(y, f);
+      if (k == 0) break;
+      const double2 t = rlane2(y, k);
+      if (lane < k) y = csub(y, cmul(t, H(k, lane)));
+    }
+  }
+  if (lane <= col) g.ycoef[lane] = cscale(y, sv);
+}
+
 }  // namespace givens
 }  // namespace hh

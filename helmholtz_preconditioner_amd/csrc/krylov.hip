@@ -472,28 +472,9 @@ __global__ void gmres_solve_kernel(GivensState g, int stop_col, int merged) {
   if (threadIdx.x == 0) g.ctrl[2] = skip;
   if (skip) return;
   const int R1 = g.restart + 1;
-  const int lane = threadIdx.x, me = min(lane, col);
-  for (int e = lane; e < (col + 1) * R1; e += kWave) sH[e] = g.H[e];
-  double2 y = g.S[me];
-  const double sv = g.vscale[me];
+  for (int e = threadIdx.x; e < (col + 1) * R1; e += kWave) sH[e] = g.H[e];
   __syncthreads();
-  auto H = [&](int c, int k) { return sH[c * R1 + k]; };
-  const double2 hcc = H(col, col);
-  if (hcc.x == 0.0 && hcc.y == 0.0) {
-    if (lane == 0) g.S[col] = make_double2(0.0, 0.0);
-    if (lane == col) y = make_double2(0.0, 0.0);
-  }
-  const Smith f = smith_of(H(me, me));
-  for (int k = col; k >= 0; --k) {
-    const double2 t0 = rlane2(y, k);
-    if (t0.x != 0.0 || t0.y != 0.0) {  // (uniform)
-      if (lane == k) y = smith_apply(y, f);
-      if (k == 0) break;
-      const double2 t = rlane2(y, k);
-      if (lane < k) y = csub(y, cmul(t, H(k, lane)));
-    }
-  }
-  if (lane <= col) g.ycoef[lane] = cscale(y, sv);
+  solve_columns_wave(g, col, sH);
 }
 
 // Krylov tuning knobs (hh_tune_krylov): non-temporal basis loads, streaming grid size;

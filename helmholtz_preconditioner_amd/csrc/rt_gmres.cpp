@@ -724,9 +724,10 @@ HH_API int hh_gmres(hh_op* op, const hh_vec* bv, hh_vec* xv, double rtol, double
     // one sync per cycle is the residual norm's, below; the report is read after it.
     HIPC(hipMemcpyAsync(op->status_h, op->red, kRedReport * sizeof(double), hipMemcpyDeviceToHost,
                         s));
-    if (merge_end)
+    if (merge_end)  // (with the triangular solve's decision and work: gmres_solve_kernel's)
       launch_cycle_finish(g, stop_col, V + (size_t)(stop_col + 1) * ldv, x, L, blocks, s);
-    launch_gmres_solve(g, stop_col, merge_end, s);
+    else
+      launch_gmres_solve(g, stop_col, false, s);
     launch_xupdate(V, ldv, stop_col + 1, g.ycoef, x, L, blocks, s, g.ctrl);
     check_site(c, "cycle finish + triangular solve + x update", s);
     residual(op, b, x, V, 4);  // r = b - A x; V[0] = M r for the next cycle
